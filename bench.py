@@ -1,0 +1,214 @@
+"""Benchmark of the erasure hot path (BASELINE.json metric).
+
+Default workload = BASELINE configs[1]: RS(k=8,m=4) encode of device-resident
+1 MiB stripes (S = 131072 B per shard), batch 4096 per GPU.  One step = one
+encode pass over the whole batch (one rsg_encode_batch_dev call).  value =
+payload (data) GiB/s over all ranks, the reference benches' convention
+(crates/ecstore/benches/erasure_benchmark.rs:112 Throughput::Bytes(data_size)).
+
+Multi-GPU: one process per GPU (torch.distributed.run), independent stripes,
+no data-path collective ("scaling": "weak"); a gloo barrier brackets the timed
+region and the elapsed time is the max over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+GiB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--m", type=int, default=4)
+    ap.add_argument("--stripe-bytes", type=int, default=1 << 20)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--digests", action="store_true", help="fused HH256S digests (config 4)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-stripes", type=int, default=256)
+    ap.add_argument("--cpu-threads", type=int, default=16, help="the GPU box's CPU share per GPU")
+    ap.add_argument("--no-extras", action="store_true", help="skip the reconstruct side measurements")
+    return ap.parse_args()
+
+
+def dist_init():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    return rank, world, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_baseline(k, m, S, stripes, threads):
+    """Restated reference algorithm (oracle/rs_oracle_simd.c: split-nibble
+    pshufb GF MAC, one stripe per thread) on a bounded sample of the workload."""
+    import numpy as np
+    from oracle import oracle as O
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    buf = np.zeros((stripes, k + m, S), dtype=np.uint8)
+    buf[:, :k] = np.random.default_rng(0).integers(0, 256, (stripes, k, S), dtype=np.uint8)
+    O.encode_batch_mt(k, m, S, buf, None, threads)  # warm-up
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        O.encode_batch_mt(k, m, S, buf, None, threads)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el > 8.0 or reps >= 40:
+            break
+    gibs = reps * stripes * k * S / el / GiB
+    return {"value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} passes x {stripes} stripes RS({k},{m}) S={S} ({el:.1f}s), "
+                      f"AVX2={'yes' if O.lib().ro_simd_level() >= 2 else 'no'}"}
+
+
+def main():
+    a = parse()
+    rank, world, local = dist_init()
+    import torch
+    from rustfs_amd import Erasure, RSG_RECONSTRUCT_MISSING, _lib
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    k, m = a.k, a.m
+    S = -(-a.stripe_bytes // k)
+    n = a.batch
+    e = Erasure(k, m, a.stripe_bytes, device=local)
+
+    # synthetic stripes, a3 layout (n, k+m, S), data random, resident in HBM
+    stripes = torch.empty((n, k + m, S), dtype=torch.uint8, device=dev)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    for s0 in range(0, n, 256):
+        s1 = min(n, s0 + 256)
+        stripes[s0:s1, :k] = torch.randint(0, 256, (s1 - s0, k, S), dtype=torch.uint8, device=dev, generator=g)
+    digests = torch.empty((n, k + m, 32), dtype=torch.uint8, device=dev) if a.digests else None
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        e.encode_batch(stripes, digests, stream=stream)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # per-launch device time with HIP events on the launch stream
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    barrier(world)
+    elapsed = max_over_ranks(elapsed, world)
+    kern_ms = sorted(s.elapsed_time(t) for s, t in ev)
+    avg_ms = sum(kern_ms) / len(kern_ms)
+
+    payload = n * k * S
+    value = world * a.steps * payload / elapsed / GiB
+    alg_bytes = n * (k + m) * S + (n * (k + m) * 32 if a.digests else 0)
+    achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
+
+    extras = {}
+    if not a.no_extras:
+        # config 3: reconstruct with 1-4 missing data shards (same buffer)
+        for miss in ((0,), (0, 3), (0, 3, 5), (0, 3, 5, 7)):
+            present = [i not in miss for i in range(k + m)]
+            for _ in range(2):
+                e.reconstruct_batch(stripes, present, RSG_RECONSTRUCT_MISSING, stream=stream)
+            torch.cuda.synchronize()
+            reps = max(3, a.steps // 4)
+            s_ev, t_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s_ev.record(stream)
+            for _ in range(reps):
+                e.reconstruct_batch(stripes, present, RSG_RECONSTRUCT_MISSING, stream=stream)
+            t_ev.record(stream)
+            torch.cuda.synchronize()
+            ms = s_ev.elapsed_time(t_ev) / reps
+            extras[f"reconstruct_e{len(miss)}"] = {
+                "GiB_s_payload": round(payload / (ms * 1e-3) / GiB, 2),
+                "ms": round(ms, 4),
+                "hbm_GB_s": round(n * (k + len(miss)) * S / (ms * 1e-3) / 1e9, 1)}
+        # round trip correctness of the last pattern (cheap, on device)
+        ok = e.verify_batch(stripes, stream=stream)
+        torch.cuda.synchronize()
+        extras["verify_all_ok_after_reconstruct"] = bool(ok.all().item())
+
+    traffic = None
+    prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    key = f"rs{k}{m}_S{S}_n{n}{'_hash' if a.digests else ''}"
+    if os.path.exists(prof):
+        try:
+            traffic = json.load(open(prof)).get(key, {}).get("bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(k, m, S, min(a.cpu_sample_stripes, n), a.cpu_threads)
+
+    if rank == 0:
+        line = {
+            "metric": "GiB/s RS(8,4) encode+reconstruct, device-resident 1 MiB stripes, 1/2/4/8 GPU",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (uniform random bytes, torch generator), device-resident",
+            "config": {"workload": f"RS(k={k},m={m}) encode{' + fused HH256S' if a.digests else ''}, "
+                                   f"{a.stripe_bytes} B stripes (S={S}), batch {n} per GPU",
+                       "k": k, "m": m, "shard_bytes": S, "stripes_per_gpu": n,
+                       "parallelism": f"stripe-split x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel_ms_avg": round(avg_ms, 4), "kernel_ms_min": round(kern_ms[0], 4),
+                         "alg_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+            "extras": extras,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

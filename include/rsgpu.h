@@ -1,0 +1,147 @@
+/*
+ * rsgpu.h — C ABI of the MI355X-native Reed–Solomon GF(2^8) erasure engine.
+ *
+ * This is the drop-in boundary for the erasure hot path of rustfs
+ * (crates/ecstore/src/erasure/).  Every entry point names the reference
+ * interface it replaces; the Rust-side `extern "C"` binding a maintainer would
+ * add is in INTEGRATION.md.  Plain pointers and sizes only; no torch types.
+ *
+ * Codec: GF(2^8) with polynomial 0x11D, generator 2, systematic matrix
+ * V * inv(V[0..k]) with V[r][c] = r^c ("rs-vandermonde", the construction of
+ * reed_solomon_erasure::galois_8::ReedSolomon used by rustfs and MinIO;
+ * docs/architecture/erasure-coding.md:41-50).  Outputs are bit-exact with it.
+ *
+ * Threading: every function is thread-safe.  A context owns one device, a
+ * stream and per-geometry coefficient caches; concurrent host-buffer calls on
+ * one context are serialised internally (the reference calls encode from many
+ * tokio workers concurrently, encode.rs:511-526).  Device-batch calls are
+ * asynchronous on the caller's stream.
+ *
+ * Errors: functions return an rsg_status; rsg_strerror() gives the message
+ * fragment the reference uses for the same condition (erasure.rs:87-121,
+ * 396-446, 505-594; bridge.rs:202-235; bitrot.rs:227-247).
+ */
+#ifndef RSGPU_H
+#define RSGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSG_ABI_VERSION 1
+#define RSG_MAX_TOTAL_SHARDS 256 /* galois_8::Field::ORDER, erasure.rs:72 */
+#define RSG_DIGEST_BYTES 32      /* HighwayHash-256 */
+
+typedef enum rsg_status {
+    RSG_OK = 0,
+    RSG_ERR_INVALID_ARG = 1,           /* null pointer / bad flag */
+    RSG_ERR_ZERO_DATA_SHARDS = 2,      /* ErasureConstructionError::ZeroDataShards, erasure.rs:90 */
+    RSG_ERR_ZERO_PARITY_SHARDS = 3,    /* reed_solomon_erasure::Error::TooFewParityShards */
+    RSG_ERR_TOO_MANY_SHARDS = 4,       /* UnsupportedModernShardCount, erasure.rs:102 */
+    RSG_ERR_INVALID_SHARD_COUNT = 5,   /* "invalid shard count", erasure.rs:510 */
+    RSG_ERR_INCONSISTENT_LENGTH = 6,   /* "inconsistent shard length", erasure.rs:527 */
+    RSG_ERR_EMPTY_SHARD = 7,           /* reed_solomon_erasure::Error::EmptyShard */
+    RSG_ERR_TOO_FEW_SHARDS = 8,        /* Error::TooFewShardsPresent -> "Reed-Solomon reconstruct failed" */
+    RSG_ERR_NO_VALID_SHARDS = 9,       /* "No valid shards found", erasure.rs:519 */
+    RSG_ERR_INCONSISTENT_SOURCES = 10, /* InvalidData "inconsistent read source shards", bridge.rs:231 */
+    RSG_ERR_BITROT_MISMATCH = 11,      /* InvalidData "bitrot hash mismatch", bitrot.rs:241 */
+    RSG_ERR_NO_DEVICE = 12,            /* no HIP device / bad ordinal */
+    RSG_ERR_DEVICE = 13,               /* HIP runtime failure */
+    RSG_ERR_OUT_OF_MEMORY = 14,
+    RSG_ERR_UNSUPPORTED = 15
+} rsg_status;
+
+/* Bitrot hash selector (crates/utils/src/hash.rs:52-68). */
+typedef enum rsg_hash_algo {
+    RSG_HASH_NONE = 0,
+    RSG_HASH_HIGHWAY256S = 1,        /* HashAlgorithm::HighwayHash256S (default), pi-derived key */
+    RSG_HASH_HIGHWAY256S_LEGACY = 2  /* HashAlgorithm::HighwayHash256SLegacy, key [3,4,2,1] */
+} rsg_hash_algo;
+
+/* Reconstruct modes. */
+typedef enum rsg_reconstruct_mode {
+    /* ReedSolomonEncoder::reconstruct_data (erasure.rs:411-422): rebuild missing
+     * data shards only; missing parity buffers are left untouched. */
+    RSG_RECONSTRUCT_DATA = 0,
+    /* reconstruct_opt (bridge.rs:296): rebuild every missing shard, data and parity. */
+    RSG_RECONSTRUCT_MISSING = 1,
+    /* ReedSolomonEncoder::reconstruct (erasure.rs:425-428): rebuild missing data,
+     * then re-encode ALL parity shards from the data (present ones are overwritten). */
+    RSG_RECONSTRUCT_REENCODE_PARITY = 2
+} rsg_reconstruct_mode;
+
+typedef struct rsg_ctx rsg_ctx;
+
+/* ---- library / context ---- */
+int rsg_abi_version(void);
+const char *rsg_strerror(int status);
+int rsg_device_count(int *count);
+/* Create a context bound to HIP device `device`. */
+int rsg_create(int device, rsg_ctx **out);
+void rsg_destroy(rsg_ctx *ctx);
+
+/* Encoding matrix ((k+m) x k, row-major) as reed_solomon_erasure::ReedSolomon::new
+ * builds it (erasure.rs:448-470 cached_modern_reed_solomon).  Host only. */
+int rsg_matrix(int k, int m, uint8_t *out);
+/* Validate a geometry like Erasure::try_new_with_options (erasure.rs:708-773):
+ * k > 0, k+m <= 256.  m == 0 is valid (no codec; encode is a no-op). */
+int rsg_check_geometry(int k, int m);
+
+/* ---- host-buffer API: drop-in for ReedSolomonEncoder (erasure.rs:358-446) ----
+ * `shards` holds k+m host pointers of shard_len bytes each: k data then m parity. */
+
+/* ReedSolomonEncoder::encode (erasure.rs:396-408): overwrite shards[k..k+m). */
+int rsg_encode(rsg_ctx *ctx, int k, int m, size_t shard_len, uint8_t *const *shards);
+
+/* ReedSolomonEncoder::reconstruct_data / reconstruct and reconstruct_opt
+ * (erasure.rs:411-428, bridge.rs:295-301).  present[i] != 0 marks shard i valid;
+ * every pointer must be a writable shard_len buffer; rebuilt shards are written
+ * in place.  Fewer than k present -> RSG_ERR_TOO_FEW_SHARDS. */
+int rsg_reconstruct(rsg_ctx *ctx, int k, int m, size_t shard_len, uint8_t *const *shards,
+                    const uint8_t *present, int mode);
+
+/* ReedSolomonEncoder::verify (erasure.rs:430-441): *ok = 1 when every parity
+ * shard equals the parity re-encoded from the data shards. */
+int rsg_verify(rsg_ctx *ctx, int k, int m, size_t shard_len, const uint8_t *const *shards, int *ok);
+
+/* HashAlgorithm::hash_encode for the Highway variants (hash.rs:114-141). */
+int rsg_hash(rsg_ctx *ctx, int algo, const uint8_t *data, size_t len, uint8_t out[32]);
+
+/* ---- device-batch API: the batched GPU path (encode.rs:795-919 dispatch point) ----
+ * d_stripes: device memory holding n stripes.  Stripe s, shard i starts at
+ *   d_stripes + s*stripe_stride + i*shard_pitch   (a3 layout: shard_pitch = shard_len,
+ *   stripe_stride = (k+m)*shard_len, erasure.rs:848-887).
+ * stream: a hipStream_t (NULL = the context's stream).  Calls are asynchronous. */
+
+/* Encode parity for n stripes; if d_digests != NULL and algo != NONE also write
+ * the (k+m) per-shard bitrot digests of every stripe, [n][k+m][32] — identical to
+ * BitrotWriter::write's prefix (bitrot.rs:496-502) — in the same pass. */
+int rsg_encode_batch_dev(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t n,
+                         uint8_t *d_stripes, size_t shard_pitch, size_t stripe_stride,
+                         uint8_t *d_digests, int algo, void *stream);
+
+/* Reconstruct n stripes that share one erasure pattern `present` (k+m host bytes). */
+int rsg_reconstruct_batch_dev(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t n,
+                              uint8_t *d_stripes, size_t shard_pitch, size_t stripe_stride,
+                              const uint8_t *present, int mode, void *stream);
+
+/* Per-stripe parity check of n complete stripes: d_ok[s] = 1 if consistent. */
+int rsg_verify_batch_dev(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t n,
+                         const uint8_t *d_stripes, size_t shard_pitch, size_t stripe_stride,
+                         uint8_t *d_ok, void *stream);
+
+/* Hash n messages of len bytes each (message j at d_data + j*stride) into
+ * d_out[n][32] (HashAlgorithm::hash_encode, hash.rs:114). */
+int rsg_hash_batch_dev(rsg_ctx *ctx, int algo, const uint8_t *d_data, size_t len, size_t stride,
+                       size_t n, uint8_t *d_out, void *stream);
+
+/* Block until all work queued on `stream` (NULL = context stream) is done. */
+int rsg_sync(rsg_ctx *ctx, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSGPU_H */

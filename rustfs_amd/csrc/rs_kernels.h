@@ -1,0 +1,51 @@
+// rs_kernels.h — kernel parameter blocks and launchers (internal to librsgpu).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rsg {
+
+constexpr int kMaxC = 16;  // inputs per launch (more are chained with GF_MODE_XOR)
+constexpr int kMaxR = 4;   // outputs per launch (more are split over launches)
+
+enum GfMode : uint32_t {
+    GF_MODE_STORE = 0,    // out = M * in
+    GF_MODE_XOR = 1,      // out ^= M * in  (continuation of a C > 16 product)
+    GF_MODE_COMPARE = 2,  // ok_flags[stripe] = 0 where out != M * in  (verify)
+};
+
+// Passed by value: lands in the kernel-argument segment (SGPR-loaded).
+struct GfApplyParams {
+    const uint8_t* base;         // input stripe 0
+    uint8_t* out_base;           // output stripe 0
+    uint64_t stripe_stride;      // bytes between input stripes
+    uint64_t out_stripe_stride;  // bytes between output stripes
+    uint64_t in_off[kMaxC];      // byte offset of input c inside a stripe
+    uint64_t out_off[kMaxR];     // byte offset of output r inside a stripe
+    uint32_t tab[kMaxR][kMaxC][5];  // v_perm tables per coefficient (see rs_kernels.hip)
+    uint8_t* ok_flags;           // GF_MODE_COMPARE target, one byte per stripe
+    uint32_t C, R, mode;
+    uint32_t units;              // 16-byte units per shard (vector path)
+    uint32_t units_per_thread;   // vector path work per thread
+    uint32_t chunks_per_stripe;  // set by the launcher
+    uint64_t byte_begin, byte_end;  // byte path column range
+};
+
+struct HashParams {
+    const uint8_t* data;
+    uint64_t len;            // message length
+    uint64_t n;              // messages
+    uint64_t shards;         // messages per stripe (1 for a plain batch)
+    uint64_t shard_pitch;    // bytes between messages of one stripe
+    uint64_t stripe_stride;  // bytes between stripes
+    uint64_t key[4];
+    uint8_t* out;            // n x 32 digests
+    uint32_t aligned16;      // every message 16-B aligned: vector loads
+};
+
+hipError_t launch_gf_apply_vec(GfApplyParams p, uint64_t n_stripes, hipStream_t stream);
+hipError_t launch_gf_apply_byte(GfApplyParams p, uint64_t n_stripes, hipStream_t stream);
+hipError_t launch_hh256(const HashParams& p, hipStream_t stream);
+
+}  // namespace rsg

@@ -1,0 +1,694 @@
+// rsgpu.cpp — host side of the MI355X erasure engine behind include/rsgpu.h.
+//
+// Owns: GF(2^8) host arithmetic for matrix construction and inversion (the
+// part of reed_solomon_erasure::ReedSolomon::new / get_data_decode_matrix that
+// stays on the host), per-(k,m) codec cache (erasure.rs:448-470
+// cached_modern_reed_solomon, <= 64 entries) with a per-codec cache of decode
+// plans keyed by the erasure pattern (the LRU the fork keeps for inverted
+// matrices), per-device contexts, and the launch planning that maps every
+// encode / reconstruct / verify onto one GPU primitive: out = M * in.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <list>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rsgpu.h"
+#include "rs_kernels.h"
+
+namespace {
+
+// --------------------------------------------------------------------------
+// GF(2^8) / 0x11D, generator 2 (docs/architecture/erasure-coding.md:41-50).
+
+struct Gf {
+    uint8_t exp[512];
+    uint8_t log[256];
+    Gf() {
+        unsigned x = 1;
+        for (int i = 0; i < 255; ++i) {
+            exp[i] = (uint8_t)x;
+            log[x] = (uint8_t)i;
+            x <<= 1;
+            if (x & 0x100) x ^= 0x11D;
+        }
+        for (int i = 255; i < 512; ++i) exp[i] = exp[i - 255];
+        log[0] = 0;
+    }
+    uint8_t mul(uint8_t a, uint8_t b) const { return (a && b) ? exp[log[a] + log[b]] : 0; }
+    uint8_t div(uint8_t a, uint8_t b) const {
+        if (!a) return 0;
+        int l = (int)log[a] - (int)log[b];
+        return exp[l < 0 ? l + 255 : l];
+    }
+    uint8_t pow(uint8_t a, int n) const {
+        if (n == 0) return 1;
+        if (a == 0) return 0;
+        return exp[((int)log[a] * n) % 255];
+    }
+};
+
+const Gf& gf() {
+    static const Gf g;
+    return g;
+}
+
+using Mat = std::vector<uint8_t>;  // row-major
+
+bool invert(int n, Mat& a) {
+    const Gf& g = gf();
+    Mat w((size_t)n * 2 * n, 0);
+    for (int r = 0; r < n; ++r) {
+        std::memcpy(&w[(size_t)r * 2 * n], &a[(size_t)r * n], n);
+        w[(size_t)r * 2 * n + n + r] = 1;
+    }
+    for (int c = 0; c < n; ++c) {
+        int p = c;
+        while (p < n && w[(size_t)p * 2 * n + c] == 0) ++p;
+        if (p == n) return false;
+        if (p != c)
+            for (int j = 0; j < 2 * n; ++j) std::swap(w[(size_t)p * 2 * n + j], w[(size_t)c * 2 * n + j]);
+        uint8_t* row = &w[(size_t)c * 2 * n];
+        const uint8_t piv = row[c];
+        if (piv != 1)
+            for (int j = 0; j < 2 * n; ++j) row[j] = g.div(row[j], piv);
+        for (int r = 0; r < n; ++r) {
+            if (r == c) continue;
+            uint8_t* o = &w[(size_t)r * 2 * n];
+            const uint8_t f = o[c];
+            if (!f) continue;
+            for (int j = 0; j < 2 * n; ++j) o[j] ^= g.mul(f, row[j]);
+        }
+    }
+    for (int r = 0; r < n; ++r) std::memcpy(&a[(size_t)r * n], &w[(size_t)r * 2 * n + n], n);
+    return true;
+}
+
+// vandermonde(k+m, k) * inv(top k x k)
+bool build_matrix(int k, int m, Mat& out) {
+    const Gf& g = gf();
+    const int t = k + m;
+    Mat v((size_t)t * k);
+    for (int r = 0; r < t; ++r)
+        for (int c = 0; c < k; ++c) v[(size_t)r * k + c] = g.pow((uint8_t)r, c);
+    Mat top(v.begin(), v.begin() + (size_t)k * k);
+    if (!invert(k, top)) return false;
+    out.assign((size_t)t * k, 0);
+    for (int r = 0; r < t; ++r)
+        for (int c = 0; c < k; ++c) {
+            uint8_t acc = 0;
+            for (int i = 0; i < k; ++i) acc ^= g.mul(v[(size_t)r * k + i], top[(size_t)i * k + c]);
+            out[(size_t)r * k + c] = acc;
+        }
+    return true;
+}
+
+// v_perm_b32 tables of coefficient c (see rs_kernels.hip header).
+void coef_tables(uint8_t c, uint32_t t[5]) {
+    const Gf& g = gf();
+    auto pack = [&](int shift, int first) {
+        uint32_t v = 0;
+        for (int i = 0; i < 4; ++i) v |= (uint32_t)g.mul(c, (uint8_t)((first + i) << shift)) << (8 * i);
+        return v;
+    };
+    t[0] = pack(0, 0);
+    t[1] = pack(0, 4);
+    t[2] = pack(3, 0);
+    t[3] = pack(3, 4);
+    t[4] = pack(6, 0);
+}
+
+// --------------------------------------------------------------------------
+// Codec cache.
+
+struct DecodePlan {
+    std::vector<int> survivors;  // first k present shards, ascending
+    std::vector<int> missing;    // missing shard indices, ascending
+    Mat inv;                     // k x k inverse of the survivor sub-matrix
+};
+
+struct Codec {
+    int k, m;
+    Mat matrix;  // (k+m) x k
+    std::mutex mu;
+    std::list<std::pair<std::string, std::shared_ptr<DecodePlan>>> lru;
+    std::map<std::string, decltype(lru)::iterator> index;
+    static constexpr size_t kMaxPlans = 254;
+
+    std::shared_ptr<DecodePlan> plan(const uint8_t* present) {
+        std::string key((size_t)(k + m), '\0');
+        for (int i = 0; i < k + m; ++i) key[i] = present[i] ? 1 : 0;
+        std::lock_guard<std::mutex> g(mu);
+        auto it = index.find(key);
+        if (it != index.end()) {
+            lru.splice(lru.begin(), lru, it->second);
+            return it->second->second;
+        }
+        auto p = std::make_shared<DecodePlan>();
+        for (int i = 0; i < k + m; ++i) {
+            if (present[i]) {
+                if ((int)p->survivors.size() < k) p->survivors.push_back(i);
+            } else {
+                p->missing.push_back(i);
+            }
+        }
+        if ((int)p->survivors.size() < k) return nullptr;
+        p->inv.assign((size_t)k * k, 0);
+        for (int s = 0; s < k; ++s)
+            std::memcpy(&p->inv[(size_t)s * k], &matrix[(size_t)p->survivors[s] * k], k);
+        if (!invert(k, p->inv)) return nullptr;
+        lru.emplace_front(key, p);
+        index[key] = lru.begin();
+        if (lru.size() > kMaxPlans) {
+            index.erase(lru.back().first);
+            lru.pop_back();
+        }
+        return p;
+    }
+};
+
+std::mutex g_codec_mu;
+std::map<std::pair<int, int>, std::shared_ptr<Codec>> g_codecs;
+constexpr size_t kMaxCodecs = 64;  // MODERN_REED_SOLOMON_CACHE_MAX_ENTRIES, erasure.rs:73
+
+int check_geometry(int k, int m) {
+    if (k <= 0) return RSG_ERR_ZERO_DATA_SHARDS;
+    if (m < 0) return RSG_ERR_INVALID_ARG;
+    if (k + m > RSG_MAX_TOTAL_SHARDS) return RSG_ERR_TOO_MANY_SHARDS;
+    return RSG_OK;
+}
+
+std::shared_ptr<Codec> get_codec(int k, int m) {
+    std::lock_guard<std::mutex> g(g_codec_mu);
+    auto it = g_codecs.find({k, m});
+    if (it != g_codecs.end()) return it->second;
+    auto c = std::make_shared<Codec>();
+    c->k = k;
+    c->m = m;
+    if (!build_matrix(k, m, c->matrix)) return nullptr;
+    if (g_codecs.size() < kMaxCodecs) g_codecs[{k, m}] = c;
+    return c;
+}
+
+// Row r of out = rows[r] . in  (R x C coefficient matrix).
+struct RowSet {
+    int R = 0, C = 0;
+    Mat coef;                    // R x C
+    std::vector<uint64_t> in_off, out_off;
+};
+
+// Parity rows of the encode matrix over the data shards.
+RowSet encode_rows(const Codec& cd, uint64_t pitch) {
+    RowSet rs;
+    rs.R = cd.m;
+    rs.C = cd.k;
+    rs.coef.assign(cd.matrix.begin() + (size_t)cd.k * cd.k, cd.matrix.end());
+    for (int c = 0; c < cd.k; ++c) rs.in_off.push_back((uint64_t)c * pitch);
+    for (int r = 0; r < cd.m; ++r) rs.out_off.push_back((uint64_t)(cd.k + r) * pitch);
+    return rs;
+}
+
+// Rows producing shard `idx` from the survivors: inv[idx] for data shards,
+// G[idx] * inv for parity shards (identical bytes to re-encoding from the
+// rebuilt data, because inv maps each present data shard to itself).
+void plan_row(const Codec& cd, const DecodePlan& p, int idx, uint8_t* row) {
+    const int k = cd.k;
+    if (idx < k) {
+        std::memcpy(row, &p.inv[(size_t)idx * k], k);
+        return;
+    }
+    const Gf& g = gf();
+    for (int c = 0; c < k; ++c) {
+        uint8_t acc = 0;
+        for (int i = 0; i < k; ++i) acc ^= g.mul(cd.matrix[(size_t)idx * k + i], p.inv[(size_t)i * k + c]);
+        row[c] = acc;
+    }
+}
+
+RowSet reconstruct_rows(const Codec& cd, const DecodePlan& p, const uint8_t* present, int mode, uint64_t pitch) {
+    RowSet rs;
+    rs.C = cd.k;
+    for (int s : p.survivors) rs.in_off.push_back((uint64_t)s * pitch);
+    std::vector<int> targets;
+    for (int i = 0; i < cd.k + cd.m; ++i) {
+        const bool is_data = i < cd.k;
+        if (is_data && !present[i]) targets.push_back(i);
+        else if (!is_data && mode == RSG_RECONSTRUCT_MISSING && !present[i]) targets.push_back(i);
+        else if (!is_data && mode == RSG_RECONSTRUCT_REENCODE_PARITY) targets.push_back(i);
+    }
+    rs.R = (int)targets.size();
+    rs.coef.assign((size_t)rs.R * cd.k, 0);
+    for (int r = 0; r < rs.R; ++r) {
+        plan_row(cd, p, targets[r], &rs.coef[(size_t)r * cd.k]);
+        rs.out_off.push_back((uint64_t)targets[r] * pitch);
+    }
+    return rs;
+}
+
+// --------------------------------------------------------------------------
+// GPU dispatch of out = M * in over n stripes.
+
+int hip_status(hipError_t e) {
+    if (e == hipSuccess) return RSG_OK;
+    if (e == hipErrorOutOfMemory) return RSG_ERR_OUT_OF_MEMORY;
+    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return RSG_ERR_NO_DEVICE;
+    return RSG_ERR_DEVICE;
+}
+
+// Units per thread for the vector path (env RSG_UNITS_PER_THREAD overrides).
+uint32_t units_per_thread() {
+    static const uint32_t v = [] {
+        const char* s = std::getenv("RSG_UNITS_PER_THREAD");
+        long x = s ? std::strtol(s, nullptr, 10) : 1;
+        return (uint32_t)(x < 1 ? 1 : (x > 64 ? 64 : x));
+    }();
+    return v;
+}
+
+int apply_rows(const RowSet& rs, const uint8_t* base, uint8_t* out_base, uint64_t stride, uint64_t out_stride,
+               uint64_t len, uint64_t n, uint32_t mode, uint8_t* ok_flags, hipStream_t stream) {
+    if (rs.R == 0 || n == 0 || len == 0) return RSG_OK;
+    if (mode == rsg::GF_MODE_COMPARE && rs.C > rsg::kMaxC) return RSG_ERR_UNSUPPORTED;
+    bool aligned = ((uintptr_t)base % 16 == 0) && ((uintptr_t)out_base % 16 == 0) && (stride % 16 == 0) &&
+                   (out_stride % 16 == 0);
+    for (uint64_t o : rs.in_off) aligned = aligned && (o % 16 == 0);
+    for (uint64_t o : rs.out_off) aligned = aligned && (o % 16 == 0);
+    const uint64_t units = aligned ? len / 16 : 0;
+    if (units > 0xffffffffull) return RSG_ERR_UNSUPPORTED;
+
+    for (int r0 = 0; r0 < rs.R; r0 += rsg::kMaxR) {
+        const int R = std::min(rsg::kMaxR, rs.R - r0);
+        for (int c0 = 0; c0 < rs.C; c0 += rsg::kMaxC) {
+            const int C = std::min(rsg::kMaxC, rs.C - c0);
+            rsg::GfApplyParams p;
+            std::memset(&p, 0, sizeof(p));
+            p.base = base;
+            p.out_base = out_base;
+            p.stripe_stride = stride;
+            p.out_stripe_stride = out_stride;
+            for (int c = 0; c < C; ++c) p.in_off[c] = rs.in_off[c0 + c];
+            for (int r = 0; r < R; ++r) p.out_off[r] = rs.out_off[r0 + r];
+            for (int r = 0; r < R; ++r)
+                for (int c = 0; c < C; ++c) coef_tables(rs.coef[(size_t)(r0 + r) * rs.C + c0 + c], p.tab[r][c]);
+            p.ok_flags = ok_flags;
+            p.C = (uint32_t)C;
+            p.R = (uint32_t)R;
+            p.mode = mode == rsg::GF_MODE_COMPARE ? mode : (c0 == 0 ? rsg::GF_MODE_STORE : rsg::GF_MODE_XOR);
+            if (units) {
+                p.units = (uint32_t)units;
+                p.units_per_thread = units_per_thread();
+                int st = hip_status(rsg::launch_gf_apply_vec(p, n, stream));
+                if (st) return st;
+            }
+            if (units * 16 < len) {
+                p.byte_begin = units * 16;
+                p.byte_end = len;
+                int st = hip_status(rsg::launch_gf_apply_byte(p, n, stream));
+                if (st) return st;
+            }
+        }
+    }
+    return RSG_OK;
+}
+
+const uint64_t kMagicKey[4] = {0xcd8a238efa34e74bull, 0x528596bbe6833e26ull, 0x14449fa35d930f04ull,
+                               0xa036de22139de097ull};
+const uint64_t kLegacyKey[4] = {3, 4, 2, 1};
+
+const uint64_t* hash_key(int algo) {
+    if (algo == RSG_HASH_HIGHWAY256S) return kMagicKey;
+    if (algo == RSG_HASH_HIGHWAY256S_LEGACY) return kLegacyKey;
+    return nullptr;
+}
+
+int hash_messages(int algo, const uint8_t* d_data, uint64_t len, uint64_t n, uint64_t shards, uint64_t pitch,
+                  uint64_t stride, uint8_t* d_out, hipStream_t stream) {
+    const uint64_t* key = hash_key(algo);
+    if (!key) return RSG_ERR_INVALID_ARG;
+    rsg::HashParams h;
+    std::memset(&h, 0, sizeof(h));
+    h.data = d_data;
+    h.len = len;
+    h.n = n;
+    h.shards = shards;
+    h.shard_pitch = pitch;
+    h.stripe_stride = stride;
+    std::memcpy(h.key, key, sizeof(h.key));
+    h.out = d_out;
+    h.aligned16 = ((uintptr_t)d_data % 16 == 0) && (pitch % 16 == 0) && (stride % 16 == 0);
+    return hip_status(rsg::launch_hh256(h, stream));
+}
+
+uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace
+
+// --------------------------------------------------------------------------
+// Context.
+
+struct rsg_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;  // serialises the host-buffer API on this context
+    uint8_t* d_scratch = nullptr;
+    size_t scratch_cap = 0;
+
+    int ensure_scratch(size_t bytes) {
+        if (bytes <= scratch_cap) return RSG_OK;
+        if (d_scratch) (void)hipFree(d_scratch);
+        d_scratch = nullptr;
+        scratch_cap = 0;
+        size_t cap = std::max(bytes, (size_t)1 << 20);
+        hipError_t e = hipMalloc((void**)&d_scratch, cap);
+        if (e != hipSuccess) return hip_status(e);
+        scratch_cap = cap;
+        return RSG_OK;
+    }
+};
+
+namespace {
+int enter(rsg_ctx* ctx) {
+    if (!ctx) return RSG_ERR_INVALID_ARG;
+    return hip_status(hipSetDevice(ctx->device));
+}
+hipStream_t pick_stream(rsg_ctx* ctx, void* s) { return s ? (hipStream_t)s : ctx->stream; }
+}  // namespace
+
+extern "C" {
+
+int rsg_abi_version(void) { return RSG_ABI_VERSION; }
+
+const char* rsg_strerror(int status) {
+    switch (status) {
+        case RSG_OK: return "ok";
+        case RSG_ERR_INVALID_ARG: return "invalid argument";
+        case RSG_ERR_ZERO_DATA_SHARDS: return "data_shards must be greater than zero";
+        case RSG_ERR_ZERO_PARITY_SHARDS: return "Reed-Solomon encode failed: TooFewParityShards";
+        case RSG_ERR_TOO_MANY_SHARDS: return "modern codec does not support this shard count (data + parity > 256)";
+        case RSG_ERR_INVALID_SHARD_COUNT: return "invalid shard count";
+        case RSG_ERR_INCONSISTENT_LENGTH: return "inconsistent shard length";
+        case RSG_ERR_EMPTY_SHARD: return "Reed-Solomon encode failed: EmptyShard";
+        case RSG_ERR_TOO_FEW_SHARDS: return "Reed-Solomon reconstruct failed: TooFewShardsPresent";
+        case RSG_ERR_NO_VALID_SHARDS: return "No valid shards found";
+        case RSG_ERR_INCONSISTENT_SOURCES: return "inconsistent read source shards";
+        case RSG_ERR_BITROT_MISMATCH: return "bitrot hash mismatch";
+        case RSG_ERR_NO_DEVICE: return "no HIP device";
+        case RSG_ERR_DEVICE: return "HIP runtime error";
+        case RSG_ERR_OUT_OF_MEMORY: return "out of device memory";
+        case RSG_ERR_UNSUPPORTED: return "unsupported configuration";
+    }
+    return "unknown rsgpu status";
+}
+
+int rsg_device_count(int* count) {
+    if (!count) return RSG_ERR_INVALID_ARG;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    *count = (e == hipSuccess) ? n : 0;
+    return e == hipSuccess ? RSG_OK : RSG_ERR_NO_DEVICE;
+}
+
+int rsg_create(int device, rsg_ctx** out) {
+    if (!out) return RSG_ERR_INVALID_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return RSG_ERR_NO_DEVICE;
+    if (hipSetDevice(device) != hipSuccess) return RSG_ERR_NO_DEVICE;
+    auto* c = new rsg_ctx();
+    c->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return hip_status(e);
+    }
+    *out = c;
+    return RSG_OK;
+}
+
+void rsg_destroy(rsg_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipStreamDestroy(ctx->stream);
+    }
+    if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+    delete ctx;
+}
+
+int rsg_check_geometry(int k, int m) { return check_geometry(k, m); }
+
+int rsg_matrix(int k, int m, uint8_t* out) {
+    if (!out) return RSG_ERR_INVALID_ARG;
+    int st = check_geometry(k, m);
+    if (st) return st;
+    if (m == 0) return RSG_ERR_ZERO_PARITY_SHARDS;
+    auto cd = get_codec(k, m);
+    if (!cd) return RSG_ERR_INVALID_ARG;
+    std::memcpy(out, cd->matrix.data(), cd->matrix.size());
+    return RSG_OK;
+}
+
+int rsg_sync(rsg_ctx* ctx, void* stream) {
+    int st = enter(ctx);
+    if (st) return st;
+    return hip_status(hipStreamSynchronize(pick_stream(ctx, stream)));
+}
+
+// ---- device-batch API ----
+
+int rsg_encode_batch_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n, uint8_t* d_stripes,
+                         size_t shard_pitch, size_t stripe_stride, uint8_t* d_digests, int algo, void* stream) {
+    int st = enter(ctx);
+    if (st) return st;
+    if ((st = check_geometry(k, m))) return st;
+    if (n && !d_stripes) return RSG_ERR_INVALID_ARG;
+    if (shard_pitch < shard_len) return RSG_ERR_INCONSISTENT_LENGTH;
+    hipStream_t s = pick_stream(ctx, stream);
+    if (m > 0 && shard_len > 0) {
+        auto cd = get_codec(k, m);
+        if (!cd) return RSG_ERR_INVALID_ARG;
+        RowSet rs = encode_rows(*cd, shard_pitch);
+        st = apply_rows(rs, d_stripes, d_stripes, stripe_stride, stripe_stride, shard_len, n, rsg::GF_MODE_STORE,
+                        nullptr, s);
+        if (st) return st;
+    }
+    if (d_digests && algo != RSG_HASH_NONE) {
+        st = hash_messages(algo, d_stripes, shard_len, n * (uint64_t)(k + m), (uint64_t)(k + m), shard_pitch,
+                           stripe_stride, d_digests, s);
+        if (st) return st;
+    }
+    return RSG_OK;
+}
+
+int rsg_reconstruct_batch_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n, uint8_t* d_stripes,
+                              size_t shard_pitch, size_t stripe_stride, const uint8_t* present, int mode,
+                              void* stream) {
+    int st = enter(ctx);
+    if (st) return st;
+    if ((st = check_geometry(k, m))) return st;
+    if (!present || (n && !d_stripes)) return RSG_ERR_INVALID_ARG;
+    if (mode < RSG_RECONSTRUCT_DATA || mode > RSG_RECONSTRUCT_REENCODE_PARITY) return RSG_ERR_INVALID_ARG;
+    int npresent = 0;
+    for (int i = 0; i < k + m; ++i) npresent += present[i] ? 1 : 0;
+    if (npresent < k) return RSG_ERR_TOO_FEW_SHARDS;
+    if (m == 0 || shard_len == 0 || n == 0) return RSG_OK;
+    if (npresent == k + m && mode != RSG_RECONSTRUCT_REENCODE_PARITY) return RSG_OK;
+    auto cd = get_codec(k, m);
+    if (!cd) return RSG_ERR_INVALID_ARG;
+    auto plan = cd->plan(present);
+    if (!plan) return RSG_ERR_TOO_FEW_SHARDS;
+    RowSet rs = reconstruct_rows(*cd, *plan, present, mode, shard_pitch);
+    return apply_rows(rs, d_stripes, d_stripes, stripe_stride, stripe_stride, shard_len, n, rsg::GF_MODE_STORE,
+                      nullptr, pick_stream(ctx, stream));
+}
+
+int rsg_verify_batch_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n, const uint8_t* d_stripes,
+                         size_t shard_pitch, size_t stripe_stride, uint8_t* d_ok, void* stream) {
+    int st = enter(ctx);
+    if (st) return st;
+    if ((st = check_geometry(k, m))) return st;
+    if (n && (!d_stripes || !d_ok)) return RSG_ERR_INVALID_ARG;
+    hipStream_t s = pick_stream(ctx, stream);
+    if (n == 0) return RSG_OK;
+    if ((st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
+    if (m == 0 || shard_len == 0) return RSG_OK;
+    auto cd = get_codec(k, m);
+    if (!cd) return RSG_ERR_INVALID_ARG;
+    RowSet rs = encode_rows(*cd, shard_pitch);
+    return apply_rows(rs, d_stripes, const_cast<uint8_t*>(d_stripes), stripe_stride, stripe_stride, shard_len, n,
+                      rsg::GF_MODE_COMPARE, d_ok, s);
+}
+
+int rsg_hash_batch_dev(rsg_ctx* ctx, int algo, const uint8_t* d_data, size_t len, size_t stride, size_t n,
+                       uint8_t* d_out, void* stream) {
+    int st = enter(ctx);
+    if (st) return st;
+    if (n && (!d_out || (len && !d_data))) return RSG_ERR_INVALID_ARG;
+    if (!hash_key(algo)) return RSG_ERR_INVALID_ARG;
+    return hash_messages(algo, d_data, len, n, 1, 0, stride, d_out, pick_stream(ctx, stream));
+}
+
+// ---- host-buffer API ----
+
+int rsg_encode(rsg_ctx* ctx, int k, int m, size_t shard_len, uint8_t* const* shards) {
+    int st = enter(ctx);
+    if (st) return st;
+    if ((st = check_geometry(k, m))) return st;
+    if (m == 0) return RSG_ERR_ZERO_PARITY_SHARDS;
+    if (!shards) return RSG_ERR_INVALID_ARG;
+    for (int i = 0; i < k + m; ++i)
+        if (!shards[i]) return RSG_ERR_INVALID_ARG;
+    if (shard_len == 0) return RSG_ERR_EMPTY_SHARD;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    const uint64_t pitch = round_up(shard_len, 256);
+    if ((st = ctx->ensure_scratch((size_t)pitch * (k + m)))) return st;
+    hipStream_t s = ctx->stream;
+    for (int i = 0; i < k; ++i)
+        if ((st = hip_status(hipMemcpyAsync(ctx->d_scratch + i * pitch, shards[i], shard_len,
+                                            hipMemcpyHostToDevice, s))))
+            return st;
+    auto cd = get_codec(k, m);
+    if (!cd) return RSG_ERR_INVALID_ARG;
+    RowSet rs = encode_rows(*cd, pitch);
+    if ((st = apply_rows(rs, ctx->d_scratch, ctx->d_scratch, 0, 0, shard_len, 1, rsg::GF_MODE_STORE, nullptr, s)))
+        return st;
+    for (int p = 0; p < m; ++p)
+        if ((st = hip_status(hipMemcpyAsync(shards[k + p], ctx->d_scratch + (k + p) * pitch, shard_len,
+                                            hipMemcpyDeviceToHost, s))))
+            return st;
+    return hip_status(hipStreamSynchronize(s));
+}
+
+int rsg_reconstruct(rsg_ctx* ctx, int k, int m, size_t shard_len, uint8_t* const* shards, const uint8_t* present,
+                    int mode) {
+    int st = enter(ctx);
+    if (st) return st;
+    if ((st = check_geometry(k, m))) return st;
+    if (!shards || !present) return RSG_ERR_INVALID_ARG;
+    if (mode < RSG_RECONSTRUCT_DATA || mode > RSG_RECONSTRUCT_REENCODE_PARITY) return RSG_ERR_INVALID_ARG;
+    int npresent = 0;
+    for (int i = 0; i < k + m; ++i) npresent += present[i] ? 1 : 0;
+    if (shard_len == 0) {
+        // recover_empty_payload_data_shards: erasure.rs:563-594 (any present shard
+        // suffices) and bridge.rs:54-84 (reconstruct_opt path: needs k present).
+        if (mode == RSG_RECONSTRUCT_MISSING) return npresent >= k ? RSG_OK : RSG_ERR_TOO_FEW_SHARDS;
+        return npresent >= 1 ? RSG_OK : RSG_ERR_TOO_FEW_SHARDS;
+    }
+    if (npresent < k) return RSG_ERR_TOO_FEW_SHARDS;
+    if (m == 0) return RSG_OK;
+    if (npresent == k + m && mode != RSG_RECONSTRUCT_REENCODE_PARITY) return RSG_OK;
+    for (int i = 0; i < k + m; ++i)
+        if (!shards[i]) return RSG_ERR_INVALID_ARG;
+    auto cd = get_codec(k, m);
+    if (!cd) return RSG_ERR_INVALID_ARG;
+    auto plan = cd->plan(present);
+    if (!plan) return RSG_ERR_TOO_FEW_SHARDS;
+    RowSet rs = reconstruct_rows(*cd, *plan, present, mode, 0);
+    if (rs.R == 0) return RSG_OK;
+
+    std::vector<int> targets;
+    for (int i = 0; i < k + m; ++i) {
+        const bool is_data = i < k;
+        if ((is_data && !present[i]) || (!is_data && mode == RSG_RECONSTRUCT_MISSING && !present[i]) ||
+            (!is_data && mode == RSG_RECONSTRUCT_REENCODE_PARITY))
+            targets.push_back(i);
+    }
+    std::lock_guard<std::mutex> g(ctx->mu);
+    const uint64_t pitch = round_up(shard_len, 256);
+    if ((st = ctx->ensure_scratch((size_t)pitch * (k + targets.size())))) return st;
+    hipStream_t s = ctx->stream;
+    rs.in_off.clear();
+    rs.out_off.clear();
+    // Survivors go to slots 0..k-1 of the scratch, outputs to slots k.. .
+    for (int c = 0; c < k; ++c) {
+        if ((st = hip_status(hipMemcpyAsync(ctx->d_scratch + c * pitch, shards[plan->survivors[c]], shard_len,
+                                            hipMemcpyHostToDevice, s))))
+            return st;
+        rs.in_off.push_back((uint64_t)c * pitch);
+    }
+    for (size_t r = 0; r < targets.size(); ++r) rs.out_off.push_back((uint64_t)(k + r) * pitch);
+    if ((st = apply_rows(rs, ctx->d_scratch, ctx->d_scratch, 0, 0, shard_len, 1, rsg::GF_MODE_STORE, nullptr, s)))
+        return st;
+    for (size_t r = 0; r < targets.size(); ++r)
+        if ((st = hip_status(hipMemcpyAsync(shards[targets[r]], ctx->d_scratch + (k + r) * pitch, shard_len,
+                                            hipMemcpyDeviceToHost, s))))
+            return st;
+    return hip_status(hipStreamSynchronize(s));
+}
+
+int rsg_verify(rsg_ctx* ctx, int k, int m, size_t shard_len, const uint8_t* const* shards, int* ok) {
+    int st = enter(ctx);
+    if (st) return st;
+    if ((st = check_geometry(k, m))) return st;
+    if (!shards || !ok) return RSG_ERR_INVALID_ARG;
+    *ok = 0;
+    if (m == 0 || shard_len == 0) {
+        *ok = 1;
+        return RSG_OK;
+    }
+    for (int i = 0; i < k + m; ++i)
+        if (!shards[i]) return RSG_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    const uint64_t pitch = round_up(shard_len, 256);
+    const uint64_t flag_off = pitch * (uint64_t)(2 * m + k);
+    if ((st = ctx->ensure_scratch((size_t)flag_off + 256))) return st;
+    hipStream_t s = ctx->stream;
+    for (int i = 0; i < k + m; ++i)
+        if ((st = hip_status(hipMemcpyAsync(ctx->d_scratch + i * pitch, shards[i], shard_len, hipMemcpyHostToDevice,
+                                            s))))
+            return st;
+    auto cd = get_codec(k, m);
+    if (!cd) return RSG_ERR_INVALID_ARG;
+    RowSet rs = encode_rows(*cd, pitch);
+    uint8_t* d_flag = ctx->d_scratch + flag_off;
+    if (k <= rsg::kMaxC) {
+        if ((st = hip_status(hipMemsetAsync(d_flag, 1, 1, s)))) return st;
+        if ((st = apply_rows(rs, ctx->d_scratch, ctx->d_scratch, 0, 0, shard_len, 1, rsg::GF_MODE_COMPARE, d_flag,
+                             s)))
+            return st;
+        uint8_t h = 0;
+        if ((st = hip_status(hipMemcpyAsync(&h, d_flag, 1, hipMemcpyDeviceToHost, s)))) return st;
+        if ((st = hip_status(hipStreamSynchronize(s)))) return st;
+        *ok = h ? 1 : 0;
+        return RSG_OK;
+    }
+    // k > 16: re-encode into spare slots and compare on the device copy.
+    for (int p = 0; p < m; ++p) rs.out_off[p] = (uint64_t)(k + m + p) * pitch;
+    if ((st = apply_rows(rs, ctx->d_scratch, ctx->d_scratch, 0, 0, shard_len, 1, rsg::GF_MODE_STORE, nullptr, s)))
+        return st;
+    std::vector<uint8_t> buf(shard_len);
+    int good = 1;
+    for (int p = 0; p < m && good; ++p) {
+        if ((st = hip_status(hipMemcpyAsync(buf.data(), ctx->d_scratch + (k + m + p) * pitch, shard_len,
+                                            hipMemcpyDeviceToHost, s))))
+            return st;
+        if ((st = hip_status(hipStreamSynchronize(s)))) return st;
+        good = std::memcmp(buf.data(), shards[k + p], shard_len) == 0;
+    }
+    *ok = good;
+    return RSG_OK;
+}
+
+int rsg_hash(rsg_ctx* ctx, int algo, const uint8_t* data, size_t len, uint8_t out[32]) {
+    int st = enter(ctx);
+    if (st) return st;
+    if (!out || (len && !data) || !hash_key(algo)) return RSG_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    const uint64_t data_bytes = round_up(len ? len : 1, 256);
+    if ((st = ctx->ensure_scratch((size_t)data_bytes + 256))) return st;
+    hipStream_t s = ctx->stream;
+    if (len && (st = hip_status(hipMemcpyAsync(ctx->d_scratch, data, len, hipMemcpyHostToDevice, s)))) return st;
+    if ((st = hash_messages(algo, ctx->d_scratch, len, 1, 1, 0, 0, ctx->d_scratch + data_bytes, s))) return st;
+    if ((st = hip_status(hipMemcpyAsync(out, ctx->d_scratch + data_bytes, 32, hipMemcpyDeviceToHost, s)))) return st;
+    return hip_status(hipStreamSynchronize(s));
+}
+
+}  // extern "C"

@@ -1,0 +1,330 @@
+"""Host-side mirror of rustfs's erasure codec surface, running on librsgpu.so.
+
+Mirrors, name for name and error for error:
+  * ``Erasure``            crates/ecstore/src/erasure/coding/erasure.rs:617-1095
+  * ``ReedSolomonEncoder`` erasure.rs:358-446
+  * ``calc_shard_size``    erasure.rs:655
+  * ``RustfsCodecDecodeEngine.reconstruct_into``  crates/ecstore/src/erasure/codec/bridge.rs:274-307
+
+Every GF(2^8) byte is computed by the HIP kernels behind include/rsgpu.h; this
+module only validates, marshals pointers and maps status codes to exceptions.
+The device-batch entry points (``*_batch``) take torch uint8 tensors resident
+on the GPU and run asynchronously on the current torch stream.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import InvalidDataError, RsgError, check
+
+MODERN_MAX_TOTAL_SHARDS = 256  # galois_8::Field::ORDER, erasure.rs:72
+
+
+# ---------------------------------------------------------------------------
+# ErasureConstructionError (erasure.rs:87-121)
+
+class ErasureConstructionError(ValueError):
+    pass
+
+
+class ZeroDataShards(ErasureConstructionError):
+    def __init__(self):
+        super().__init__("data_shards must be greater than zero")
+
+
+class ZeroBlockSize(ErasureConstructionError):
+    def __init__(self):
+        super().__init__("block_size must be greater than zero")
+
+
+class UnsupportedModernShardCount(ErasureConstructionError):
+    def __init__(self, data_shards: int, parity_shards: int):
+        super().__init__(f"modern codec does not support {data_shards} data shards and {parity_shards} parity shards")
+
+
+def calc_shard_size(block_size: int, data_shards: int) -> int:
+    """erasure.rs:655 — plain ceiling division (MinIO-compatible sizing)."""
+    return -(-block_size // data_shards)
+
+
+def _as_array(buf) -> np.ndarray:
+    if isinstance(buf, np.ndarray):
+        return buf
+    return np.frombuffer(buf, dtype=np.uint8)
+
+
+def _ptrs(arrs: Sequence[np.ndarray]):
+    return (ctypes.c_void_p * len(arrs))(*[a.ctypes.data if a.size else 0 for a in arrs])
+
+
+def _writable(buf) -> np.ndarray:
+    a = _as_array(buf)
+    if not a.flags.writeable:
+        raise TypeError("shard buffer is read-only; pass bytearray / numpy arrays")
+    return a
+
+
+# ---------------------------------------------------------------------------
+
+class ReedSolomonEncoder:
+    """ReedSolomonEncoder (erasure.rs:358-446) over the GPU codec."""
+
+    def __init__(self, data_shards: int, parity_shards: int, device: Optional[int] = None):
+        st = _lib.load().rsg_check_geometry(data_shards, parity_shards)
+        if st != _lib.RSG_OK:
+            raise RsgError(st, "Failed to create Reed-Solomon encoder")
+        self.data_shards = data_shards
+        self.parity_shards = parity_shards
+        self._device = device
+
+    @property
+    def total(self) -> int:
+        return self.data_shards + self.parity_shards
+
+    def _ctx(self):
+        return _lib.context(self._device)
+
+    def encode(self, shards: List) -> None:
+        """In place: shards[k..k+m) overwritten with parity (erasure.rs:396-408)."""
+        if len(shards) == 0 or self.parity_shards == 0:
+            return
+        if len(shards) != self.total:
+            raise RsgError(_lib.RSG_ERR_INVALID_SHARD_COUNT, "Reed-Solomon encode failed")
+        arrs = [_as_array(s) for s in shards]
+        n = arrs[0].size
+        if any(a.size != n for a in arrs):
+            raise RsgError(_lib.RSG_ERR_INCONSISTENT_LENGTH, "Reed-Solomon encode failed")
+        for a in arrs[self.data_shards:]:
+            _writable(a)
+        check(_lib.load().rsg_encode(self._ctx().handle, self.data_shards, self.parity_shards, n, _ptrs(arrs)),
+              "Reed-Solomon encode failed")
+
+    def _reconstruct(self, shards: List, mode: int) -> None:
+        if len(shards) != self.total:
+            raise RsgError(_lib.RSG_ERR_INVALID_SHARD_COUNT,
+                           f"invalid shard count: got {len(shards)}, expected {self.total}")
+        present = [s is not None for s in shards]
+        lens = {len(s) for s in shards if s is not None}
+        if len(lens) > 1:
+            raise RsgError(_lib.RSG_ERR_INCONSISTENT_LENGTH, "Reed-Solomon reconstruct failed")
+        n = lens.pop() if lens else 0
+        if n == 0:
+            # recover_empty_payload_data_shards (erasure.rs:563-594 / bridge.rs:54-84)
+            st = _lib.load().rsg_reconstruct(self._ctx().handle, self.data_shards, self.parity_shards, 0,
+                                             None, (ctypes.c_uint8 * self.total)(*present), mode)
+            check(st, "Reed-Solomon reconstruct failed")
+            fill = range(self.data_shards) if mode == _lib.RSG_RECONSTRUCT_DATA else range(self.total)
+            for i in fill:
+                if shards[i] is None and (i < self.data_shards or mode != _lib.RSG_RECONSTRUCT_DATA):
+                    shards[i] = bytearray()
+            return
+        if self.parity_shards == 0:
+            return
+        arrs = []
+        for i, s in enumerate(shards):
+            is_parity = i >= self.data_shards
+            if s is None:
+                s = bytearray(n)  # Option::None -> freshly allocated Vec (filled by the codec)
+                if not is_parity or mode != _lib.RSG_RECONSTRUCT_DATA:
+                    shards[i] = s
+            elif is_parity and mode == _lib.RSG_RECONSTRUCT_REENCODE_PARITY and not _as_array(s).flags.writeable:
+                s = bytearray(s)  # re-encoded parity replaces the present buffer
+                shards[i] = s
+            arrs.append(_as_array(s))
+        st = _lib.load().rsg_reconstruct(self._ctx().handle, self.data_shards, self.parity_shards, n,
+                                         _ptrs(arrs), (ctypes.c_uint8 * self.total)(*present), mode)
+        check(st, "Reed-Solomon reconstruct failed")
+
+    def reconstruct_data(self, shards: List) -> None:
+        """erasure.rs:411-422: rebuild missing data shards (parity stays None)."""
+        self._reconstruct(shards, _lib.RSG_RECONSTRUCT_DATA)
+
+    def reconstruct(self, shards: List) -> None:
+        """erasure.rs:425-428: reconstruct_data then re-encode every parity shard."""
+        self._reconstruct(shards, _lib.RSG_RECONSTRUCT_REENCODE_PARITY)
+
+    def reconstruct_opt(self, shards: List) -> None:
+        """reconstruct_opt (bridge.rs:296): rebuild every missing shard."""
+        self._reconstruct(shards, _lib.RSG_RECONSTRUCT_MISSING)
+
+    def verify(self, shards: Sequence) -> bool:
+        """erasure.rs:430-441."""
+        if all(len(s) == 0 for s in shards):
+            return True
+        if self.parity_shards == 0:
+            return True
+        if len(shards) != self.total:
+            raise RsgError(_lib.RSG_ERR_INVALID_SHARD_COUNT, "Reed-Solomon verify failed")
+        arrs = [np.ascontiguousarray(_as_array(s)) for s in shards]
+        n = arrs[0].size
+        if any(a.size != n for a in arrs):
+            raise RsgError(_lib.RSG_ERR_INCONSISTENT_LENGTH, "Reed-Solomon verify failed")
+        ok = ctypes.c_int(0)
+        check(_lib.load().rsg_verify(self._ctx().handle, self.data_shards, self.parity_shards, n, _ptrs(arrs),
+                                     ctypes.byref(ok)), "Reed-Solomon verify failed")
+        return bool(ok.value)
+
+
+# ---------------------------------------------------------------------------
+
+class Erasure:
+    """Erasure (erasure.rs:617-1095), modern GF(2^8) backend only."""
+
+    def __init__(self, data_shards: int, parity_shards: int, block_size: int, device: Optional[int] = None):
+        if data_shards == 0:
+            raise ZeroDataShards()
+        if block_size == 0:
+            raise ZeroBlockSize()
+        if parity_shards > 0 and data_shards + parity_shards > MODERN_MAX_TOTAL_SHARDS:
+            raise UnsupportedModernShardCount(data_shards, parity_shards)
+        self.data_shards = data_shards
+        self.parity_shards = parity_shards
+        self.block_size = block_size
+        self.encoder = ReedSolomonEncoder(data_shards, parity_shards, device) if parity_shards > 0 else None
+        self._device = device
+
+    try_new = classmethod(lambda cls, k, m, b, device=None: cls(k, m, b, device))
+
+    # -- geometry (erasure.rs:1021-1095) --
+    def total_shard_count(self) -> int:
+        return self.data_shards + self.parity_shards
+
+    def shard_size(self) -> int:
+        return calc_shard_size(self.block_size, self.data_shards)
+
+    def has_valid_dimensions(self) -> bool:
+        return self.block_size > 0 and self.data_shards > 0
+
+    def shard_file_size(self, total_length: int) -> int:
+        if total_length == 0:
+            return 0
+        if total_length < 0:
+            return total_length
+        num_shards = total_length // self.block_size
+        last = total_length % self.block_size
+        return num_shards * self.shard_size() + calc_shard_size(last, self.data_shards)
+
+    def shard_file_offset(self, start_offset: int, length: int, total_length: int) -> int:
+        shard_size = self.shard_size()
+        shard_file_size = self.shard_file_size(total_length)
+        end_shard = (start_offset + length) // self.block_size
+        till = end_shard * shard_size + shard_size
+        return min(till, shard_file_size)
+
+    # -- encode (erasure.rs:784-887) --
+    def encode_buffer(self, data) -> np.ndarray:
+        """Copy + zero-pad to (k+m)*S and encode; returns the (k+m, S) stripe."""
+        data = _as_array(data)
+        per_shard = calc_shard_size(data.size, self.data_shards)
+        if per_shard == 0:
+            return np.zeros((self.total_shard_count(), 0), dtype=np.uint8)
+        buf = np.zeros((self.total_shard_count(), per_shard), dtype=np.uint8)
+        buf.reshape(-1)[: data.size] = data
+        if self.encoder is not None:
+            self.encoder.encode([buf[i] for i in range(self.total_shard_count())])
+        return buf
+
+    def encode_data(self, data) -> List[bytes]:
+        buf = self.encode_buffer(data)
+        return [buf[i].tobytes() for i in range(buf.shape[0])]
+
+    # -- decode (erasure.rs:897-1019) --
+    def decode_data(self, shards: List) -> None:
+        if self.encoder is not None:
+            self.encoder.reconstruct_data(shards)
+
+    def decode_data_and_parity(self, shards: List) -> None:
+        if self.encoder is not None:
+            self.encoder.reconstruct(shards)
+
+    def decode_data_with_reconstruction_verification(self, shards: List) -> None:
+        k = self.data_shards
+        missing_data = any(s is None for s in shards[:k])
+        available = sum(s is not None for s in shards)
+        source_parity = []
+        if missing_data and available > k:
+            source_parity = [(i, bytes(s)) for i, s in enumerate(shards) if i >= k and s is not None]
+        if not source_parity:
+            self.decode_data(shards)
+            return
+        self.decode_data_and_parity(shards)
+        for i, src in source_parity:
+            if shards[i] is None:
+                raise InvalidDataError(_lib.RSG_ERR_INCONSISTENT_SOURCES,
+                                       "missing rebuilt parity shard after read verification")
+            if bytes(shards[i]) != src:
+                raise InvalidDataError(_lib.RSG_ERR_INCONSISTENT_SOURCES)
+
+    def verify_data_and_parity(self, shards: Sequence) -> bool:
+        if len(shards) != self.total_shard_count():
+            raise RsgError(_lib.RSG_ERR_INVALID_SHARD_COUNT,
+                           f"invalid shard count: got {len(shards)}, expected {self.total_shard_count()}")
+        if self.parity_shards == 0:
+            return True
+        for i, s in enumerate(shards):
+            if s is None:
+                raise RsgError(_lib.RSG_ERR_INVALID_ARG, f"missing shard {i} for data/parity verification")
+        return self.encoder.verify(shards)
+
+    # -- device batches (the GPU dispatch point of encode_batched, encode.rs:795-919) --
+    def encode_batch(self, stripes, digests=None, algo: int = _lib.RSG_HASH_HIGHWAY256S, stream=None) -> None:
+        """stripes: cuda uint8 tensor (n, k+m, S) in the a3 layout; parity written
+        in place.  digests: optional (n, k+m, 32) tensor for the fused HH256S."""
+        n, t, S = _check_batch(stripes, self.total_shard_count())
+        d = digests.data_ptr() if digests is not None else None
+        check(_lib.load().rsg_encode_batch_dev(
+            _lib.context(_device_of(stripes)).handle, self.data_shards, self.parity_shards, S, n,
+            stripes.data_ptr(), S, t * S, d, algo if d else _lib.RSG_HASH_NONE, _stream_of(stripes, stream)),
+            "Reed-Solomon encode failed")
+
+    def reconstruct_batch(self, stripes, present: Sequence[bool], mode: int = _lib.RSG_RECONSTRUCT_MISSING,
+                          stream=None) -> None:
+        n, t, S = _check_batch(stripes, self.total_shard_count())
+        pres = (ctypes.c_uint8 * t)(*[1 if p else 0 for p in present])
+        check(_lib.load().rsg_reconstruct_batch_dev(
+            _lib.context(_device_of(stripes)).handle, self.data_shards, self.parity_shards, S, n,
+            stripes.data_ptr(), S, t * S, pres, mode, _stream_of(stripes, stream)),
+            "Reed-Solomon reconstruct failed")
+
+    def verify_batch(self, stripes, stream=None):
+        import torch
+        n, t, S = _check_batch(stripes, self.total_shard_count())
+        ok = torch.empty(n, dtype=torch.uint8, device=stripes.device)
+        check(_lib.load().rsg_verify_batch_dev(
+            _lib.context(_device_of(stripes)).handle, self.data_shards, self.parity_shards, S, n,
+            stripes.data_ptr(), S, t * S, ok.data_ptr(), _stream_of(stripes, stream)),
+            "Reed-Solomon verify failed")
+        return ok
+
+
+def _check_batch(stripes, total: int):
+    if stripes.dtype.__str__() != "torch.uint8" or stripes.dim() != 3 or not stripes.is_contiguous():
+        raise TypeError("stripes must be a contiguous uint8 tensor of shape (n, k+m, S)")
+    if not stripes.is_cuda:
+        raise TypeError("stripes must be device-resident (the batch path is GPU only)")
+    n, t, S = stripes.shape
+    if t != total:
+        raise RsgError(_lib.RSG_ERR_INVALID_SHARD_COUNT, f"invalid shard count: got {t}, expected {total}")
+    return int(n), int(t), int(S)
+
+
+def _device_of(t) -> int:
+    return t.device.index if t.device.index is not None else 0
+
+
+def _stream_of(t, stream):
+    if stream is not None:
+        return stream if isinstance(stream, int) else stream.cuda_stream
+    import torch
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def matrix(k: int, m: int) -> np.ndarray:
+    """The (k+m) x k encoding matrix (host-side, rsg_matrix)."""
+    out = np.zeros((k + m, k), dtype=np.uint8)
+    check(_lib.load().rsg_matrix(k, m, out.ctypes.data), f"rsg_matrix({k},{m})")
+    return out
