@@ -114,7 +114,8 @@ int rsg_hash(rsg_ctx *ctx, int algo, const uint8_t *data, size_t len, uint8_t ou
  * d_stripes: device memory holding n stripes.  Stripe s, shard i starts at
  *   d_stripes + s*stripe_stride + i*shard_pitch   (a3 layout: shard_pitch = shard_len,
  *   stripe_stride = (k+m)*shard_len, erasure.rs:848-887).
- * stream: a hipStream_t (NULL = the context's stream).  Calls are asynchronous. */
+ * stream: a hipStream_t; NULL = the HIP null (default) stream.  Calls are
+ * asynchronous and ordered with other work on that stream. */
 
 /* Encode parity for n stripes; if d_digests != NULL and algo != NONE also write
  * the (k+m) per-shard bitrot digests of every stripe, [n][k+m][32] — identical to
@@ -138,7 +139,7 @@ int rsg_verify_batch_dev(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t n,
 int rsg_hash_batch_dev(rsg_ctx *ctx, int algo, const uint8_t *d_data, size_t len, size_t stride,
                        size_t n, uint8_t *d_out, void *stream);
 
-/* Block until all work queued on `stream` (NULL = context stream) is done. */
+/* Block until all work queued on `stream` (NULL = the null stream) is done. */
 int rsg_sync(rsg_ctx *ctx, void *stream);
 
 #ifdef __cplusplus

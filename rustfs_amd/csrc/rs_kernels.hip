@@ -192,7 +192,8 @@ __device__ void hh_finish(const uint8_t* tail, uint32_t size_mod32, HHState& s, 
         }
         for (uint32_t i = 0; i < (size_mod32 & ~3u); ++i) packet[i] = tail[i];
         if (size_mod32 & 16u) {
-            for (uint32_t i = 0; i < 4; ++i) packet[28 + i] = rem[i + size_mod4 - 4];
+            // last 4 bytes of the message (size_mod32 >= 16: no underflow)
+            for (uint32_t i = 0; i < 4; ++i) packet[28 + i] = tail[size_mod32 - 4 + i];
         } else if (size_mod4) {
             packet[16] = rem[0];
             packet[17] = rem[size_mod4 >> 1];

@@ -378,7 +378,9 @@ int enter(rsg_ctx* ctx) {
     if (!ctx) return RSG_ERR_INVALID_ARG;
     return hip_status(hipSetDevice(ctx->device));
 }
-hipStream_t pick_stream(rsg_ctx* ctx, void* s) { return s ? (hipStream_t)s : ctx->stream; }
+// Device-batch calls run on the caller's stream; NULL is the HIP null (default)
+// stream, which is also torch's default stream, so ordering with the caller holds.
+hipStream_t pick_stream(rsg_ctx*, void* s) { return (hipStream_t)s; }
 }  // namespace
 
 extern "C" {
@@ -572,7 +574,7 @@ int rsg_reconstruct(rsg_ctx* ctx, int k, int m, size_t shard_len, uint8_t* const
     int st = enter(ctx);
     if (st) return st;
     if ((st = check_geometry(k, m))) return st;
-    if (!shards || !present) return RSG_ERR_INVALID_ARG;
+    if (!present || (shard_len && !shards)) return RSG_ERR_INVALID_ARG;
     if (mode < RSG_RECONSTRUCT_DATA || mode > RSG_RECONSTRUCT_REENCODE_PARITY) return RSG_ERR_INVALID_ARG;
     int npresent = 0;
     for (int i = 0; i < k + m; ++i) npresent += present[i] ? 1 : 0;
