@@ -27,7 +27,6 @@ struct GfApplyParams {
     uint8_t* ok_flags;           // GF_MODE_COMPARE target, one byte per stripe
     uint32_t C, R, mode;
     uint32_t units;              // 16-byte units per shard (vector path)
-    uint32_t units_per_thread;   // vector path work per thread
     uint32_t chunks_per_stripe;  // set by the launcher
     uint64_t byte_begin, byte_end;  // byte path column range
 };
@@ -47,5 +46,13 @@ struct HashParams {
 hipError_t launch_gf_apply_vec(GfApplyParams p, uint64_t n_stripes, hipStream_t stream);
 hipError_t launch_gf_apply_byte(GfApplyParams p, uint64_t n_stripes, hipStream_t stream);
 hipError_t launch_hh256(const HashParams& p, hipStream_t stream);
+
+// Fused encode + per-shard HighwayHash (one pass).  p: the encode RowSet with
+// in_off = data shards, out_off = parity shards, base == out_base; h: key and
+// digest output [n][C+R][32].  Requires shard_len % 512 == 0, C <= 16, R <= 4
+// and 16-B aligned shards.
+bool fused_supported(int C, int R, uint64_t shard_len);
+hipError_t launch_encode_hash_fused(GfApplyParams p, const HashParams& h, uint64_t shard_len, uint64_t n_stripes,
+                                    hipStream_t stream);
 
 }  // namespace rsg

@@ -27,25 +27,27 @@ namespace rsg {
 
 // ---------------------------------------------------------------------------
 // GF(2^8) matrix apply, vector path: 16-byte units, every shard 16-B aligned.
-// Block = 256 threads = 4 waves; thread t of block b handles unit
-// (chunk*UNITS_PER_THREAD + j)*256 + t, j < UNITS_PER_THREAD, so each wave's
-// loads/stores are contiguous 1 KiB per shard (global_load_dwordx4).
+// Block = 256 threads = 4 waves; thread t of block (stripe, chunk) handles unit
+// chunk*256 + t, so each wave's loads/stores are contiguous 1 KiB per shard
+// (global_load_dwordx4 / global_store_dwordx4).
 
 __device__ __forceinline__ uint32_t gf_mul_word(const uint32_t* t, uint32_t s0, uint32_t s1, uint32_t s2) {
     return __builtin_amdgcn_perm(t[1], t[0], s0) ^ __builtin_amdgcn_perm(t[3], t[2], s1) ^
            __builtin_amdgcn_perm(t[4], t[4], s2);
 }
 
+// One 16-byte unit per thread and no loop (126 VGPRs for RS(8,4): 4 waves per
+// SIMD).  A per-thread unit loop pushed it to 130 VGPRs (3 waves per SIMD) and
+// ran ~8 % slower; 2 or 4 units with all loads issued first ran 12-60 % slower
+// (tools/kbench/encode_variants.hip).
 template <int C, int R>
 __global__ __launch_bounds__(256) void k_gf_apply_vec(const GfApplyParams p) {
     const uint32_t stripe = blockIdx.x / p.chunks_per_stripe;
     const uint32_t chunk = blockIdx.x - stripe * p.chunks_per_stripe;
     const uint8_t* sbase = p.base + (uint64_t)stripe * p.stripe_stride;
     uint8_t* obase = p.out_base + (uint64_t)stripe * p.out_stripe_stride;
-
-#pragma unroll 1
-    for (uint32_t j = 0; j < p.units_per_thread; ++j) {
-        const uint32_t u = (chunk * p.units_per_thread + j) * 256u + threadIdx.x;
+    {
+        const uint32_t u = chunk * 256u + threadIdx.x;
         if (u >= p.units) return;
         const uint64_t off = (uint64_t)u * 16u;
 
@@ -119,53 +121,8 @@ __global__ __launch_bounds__(256) void k_gf_apply_byte(const GfApplyParams p) {
 }
 
 // ---------------------------------------------------------------------------
-// HighwayHash-256 (public spec; the `highway` crate 1.3.0 used by
-// crates/utils/src/hash.rs:123-127).  One thread per message (first slice).
-
-struct HHState {
-    uint64_t v0[4], v1[4], mul0[4], mul1[4];
-};
-
-__device__ __forceinline__ void hh_reset(const uint64_t* key, HHState& s) {
-    const uint64_t i0[4] = {0xdbe6d5d5fe4cce2full, 0xa4093822299f31d0ull, 0x13198a2e03707344ull,
-                            0x243f6a8885a308d3ull};
-    const uint64_t i1[4] = {0x3bd39e10cb0ef593ull, 0xc0acf169b5f18a8cull, 0xbe5466cf34e90c6cull,
-                            0x452821e638d01377ull};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        s.mul0[i] = i0[i];
-        s.mul1[i] = i1[i];
-        s.v0[i] = i0[i] ^ key[i];
-        s.v1[i] = i1[i] ^ ((key[i] >> 32) | (key[i] << 32));
-    }
-}
-
-__device__ __forceinline__ void hh_zipper(uint64_t v1, uint64_t v0, uint64_t& add1, uint64_t& add0) {
-    add0 += (((v0 & 0xff000000ull) | (v1 & 0xff00000000ull)) >> 24) |
-            (((v0 & 0xff0000000000ull) | (v1 & 0xff000000000000ull)) >> 16) | (v0 & 0xff0000ull) |
-            ((v0 & 0xff00ull) << 32) | ((v1 & 0xff00000000000000ull) >> 8) | (v0 << 56);
-    add1 += (((v1 & 0xff000000ull) | (v0 & 0xff00000000ull)) >> 24) | (v1 & 0xff0000ull) |
-            ((v1 & 0xff0000000000ull) >> 16) | ((v1 & 0xff00ull) << 24) |
-            ((v0 & 0xff000000000000ull) >> 8) | ((v1 & 0xffull) << 48) | (v0 & 0xff00000000000000ull);
-}
-
-__device__ __forceinline__ uint64_t mul32x32(uint64_t a, uint64_t b) {
-    return (uint64_t)(uint32_t)a * (uint64_t)(uint32_t)b;
-}
-
-__device__ __forceinline__ void hh_update(const uint64_t* lanes, HHState& s) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        s.v1[i] += s.mul0[i] + lanes[i];
-        s.mul0[i] ^= mul32x32(s.v1[i], s.v0[i] >> 32);
-        s.v0[i] += s.mul1[i];
-        s.mul1[i] ^= mul32x32(s.v0[i], s.v1[i] >> 32);
-    }
-    hh_zipper(s.v1[1], s.v1[0], s.v0[1], s.v0[0]);
-    hh_zipper(s.v1[3], s.v1[2], s.v0[3], s.v0[2]);
-    hh_zipper(s.v0[1], s.v0[0], s.v1[1], s.v1[0]);
-    hh_zipper(s.v0[3], s.v0[2], s.v1[3], s.v1[2]);
-}
+// HighwayHash-256 (public spec; the `highway` crate 1.3.0 behind
+// crates/utils/src/hash.rs:123-127).
 
 __device__ __forceinline__ uint64_t ld64_any(const uint8_t* p) {
     uint64_t v = 0;
@@ -174,95 +131,249 @@ __device__ __forceinline__ uint64_t ld64_any(const uint8_t* p) {
     return v;
 }
 
-__device__ void hh_finish(const uint8_t* tail, uint32_t size_mod32, HHState& s, uint8_t* out) {
-    if (size_mod32) {
-        const uint32_t size_mod4 = size_mod32 & 3u;
-        const uint8_t* rem = tail + (size_mod32 & ~3u);
-        uint8_t packet[32];
-#pragma unroll
-        for (int i = 0; i < 32; ++i) packet[i] = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) s.v0[i] += ((uint64_t)size_mod32 << 32) + size_mod32;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            uint32_t h0 = (uint32_t)s.v1[i], h1 = (uint32_t)(s.v1[i] >> 32);
-            h0 = (h0 << size_mod32) | (h0 >> (32u - size_mod32));
-            h1 = (h1 << size_mod32) | (h1 >> (32u - size_mod32));
-            s.v1[i] = (uint64_t)h0 | ((uint64_t)h1 << 32);
-        }
-        for (uint32_t i = 0; i < (size_mod32 & ~3u); ++i) packet[i] = tail[i];
-        if (size_mod32 & 16u) {
-            // last 4 bytes of the message (size_mod32 >= 16: no underflow)
-            for (uint32_t i = 0; i < 4; ++i) packet[28 + i] = tail[size_mod32 - 4 + i];
-        } else if (size_mod4) {
-            packet[16] = rem[0];
-            packet[17] = rem[size_mod4 >> 1];
-            packet[18] = rem[size_mod4 - 1];
-        }
-        uint64_t lanes[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) lanes[i] = ld64_any(packet + 8 * i);
-        hh_update(lanes, s);
-    }
-#pragma unroll 1
-    for (int it = 0; it < 10; ++it) {
-        uint64_t pm[4];
-        pm[0] = (s.v0[2] >> 32) | (s.v0[2] << 32);
-        pm[1] = (s.v0[3] >> 32) | (s.v0[3] << 32);
-        pm[2] = (s.v0[0] >> 32) | (s.v0[0] << 32);
-        pm[3] = (s.v0[1] >> 32) | (s.v0[1] << 32);
-        hh_update(pm, s);
-    }
-    uint64_t h[4];
-    for (int half = 0; half < 2; ++half) {
-        const int a = 2 * half;
-        const uint64_t a3 = (s.v1[a + 1] + s.mul1[a + 1]) & 0x3FFFFFFFFFFFFFFFull;
-        const uint64_t a2 = s.v1[a] + s.mul1[a];
-        const uint64_t a1 = s.v0[a + 1] + s.mul0[a + 1];
-        const uint64_t a0 = s.v0[a] + s.mul0[a];
-        h[a + 1] = a1 ^ ((a3 << 1) | (a2 >> 63)) ^ ((a3 << 2) | (a2 >> 62));
-        h[a] = a0 ^ (a2 << 1) ^ (a2 << 2);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int b = 0; b < 8; ++b) out[i * 8 + b] = (uint8_t)(h[i] >> (8 * b));
+
+// ---------------------------------------------------------------------------
+// HighwayHash-256, lane-parallel: one message per 4-lane quad, lane q holds
+// u64 lane q of v0/v1/mul0/mul1 (8 VGPRs).  The mul/add half of Update is
+// lane-local; ZipperMergeAndAdd mixes lanes (0,1) and (2,3): it needs only the
+// partner's high dword (one DPP quad_perm move) and is three v_perm_b32 with
+// per-lane-parity selectors (derived in DESIGN.md §HighwayHash):
+//   low  dword = (own.b3, other.b4, own.b2, own.b5)                 both parities
+//   high dword = (other.b6, own.b1, other.b7, own.b0)  even lane  (add0)
+//              = (own.b1, other.b6, own.b0, other.b7)  odd lane   (add1)
+
+struct HHQuad {
+    uint64_t v0, v1, mul0, mul1;
+    uint32_t sel_hi;  // per-lane high-dword selector
+};
+
+__device__ __forceinline__ uint32_t quad_swap_pairs(uint32_t x) {  // lane q <- lane q^1
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+}
+__device__ __forceinline__ uint32_t quad_swap_halves(uint32_t x) {  // lane q <- lane q^2
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
 }
 
-// Message j of n: bytes [msg_base(j), msg_base(j) + len).  Messages are
-// addressed either as data + j*stride (plain batch) or, for the per-shard
-// digests of encoded stripes, as data + (j / shards)*stripe_stride +
-// (j % shards)*shard_pitch.
-__global__ __launch_bounds__(64) void k_hh256_thread(const HashParams p) {
-    const uint64_t j = (uint64_t)blockIdx.x * 64u + threadIdx.x;
-    if (j >= p.n) return;
+__device__ __forceinline__ uint64_t hh_zip(uint64_t x, uint32_t sel_hi) {
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    const uint32_t other_hi = quad_swap_pairs(hi);
+    const uint32_t t = __builtin_amdgcn_perm(hi, lo, 0x05020C03u);        // own.b3, 0, own.b2, own.b5
+    const uint32_t zlo = __builtin_amdgcn_perm(other_hi, t, 0x03020400u);  // t.b0, other.b4, t.b2, t.b3
+    const uint32_t zhi = __builtin_amdgcn_perm(other_hi, lo, sel_hi);
+    return (uint64_t)zlo | ((uint64_t)zhi << 32);
+}
+
+__device__ __forceinline__ void hhq_init(HHQuad& s, const uint64_t* key, uint32_t q) {
+    const uint64_t i0[4] = {0xdbe6d5d5fe4cce2full, 0xa4093822299f31d0ull, 0x13198a2e03707344ull,
+                            0x243f6a8885a308d3ull};
+    const uint64_t i1[4] = {0x3bd39e10cb0ef593ull, 0xc0acf169b5f18a8cull, 0xbe5466cf34e90c6cull,
+                            0x452821e638d01377ull};
+    uint64_t kq = key[0], m0 = i0[0], m1 = i1[0];
+    if (q == 1) { kq = key[1]; m0 = i0[1]; m1 = i1[1]; }
+    if (q == 2) { kq = key[2]; m0 = i0[2]; m1 = i1[2]; }
+    if (q == 3) { kq = key[3]; m0 = i0[3]; m1 = i1[3]; }
+    s.mul0 = m0;
+    s.mul1 = m1;
+    s.v0 = m0 ^ kq;
+    s.v1 = m1 ^ ((kq >> 32) | (kq << 32));
+    s.sel_hi = (q & 1) ? 0x07000601u : 0x00070106u;
+}
+
+__device__ __forceinline__ void hhq_update(HHQuad& s, uint64_t a) {
+    s.v1 += s.mul0 + a;
+    s.mul0 ^= (uint64_t)(uint32_t)s.v1 * (s.v0 >> 32);
+    s.v0 += s.mul1;
+    s.mul1 ^= (uint64_t)(uint32_t)s.v0 * (s.v1 >> 32);
+    s.v0 += hh_zip(s.v1, s.sel_hi);
+    s.v1 += hh_zip(s.v0, s.sel_hi);
+}
+
+// Remainder packet word q built from the message tail (size_mod32 = len % 32 > 0).
+__device__ __forceinline__ void hhq_remainder(HHQuad& s, const uint8_t* tail, uint32_t size_mod32, uint32_t q) {
+    s.v0 += ((uint64_t)size_mod32 << 32) + size_mod32;
+    uint32_t h0 = (uint32_t)s.v1, h1 = (uint32_t)(s.v1 >> 32);
+    h0 = (h0 << size_mod32) | (h0 >> (32u - size_mod32));
+    h1 = (h1 << size_mod32) | (h1 >> (32u - size_mod32));
+    s.v1 = (uint64_t)h0 | ((uint64_t)h1 << 32);
+    const uint32_t copy = size_mod32 & ~3u, mod4 = size_mod32 & 3u;
+    uint64_t w = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 8; ++b) {
+        const uint32_t pos = 8 * q + b;
+        uint32_t v = 0;
+        if (pos < copy) v = tail[pos];
+        else if (size_mod32 & 16u) { if (pos >= 28) v = tail[size_mod32 - 32 + pos]; }
+        else if (mod4) {
+            if (pos == 16) v = tail[copy];
+            else if (pos == 17) v = tail[copy + (mod4 >> 1)];
+            else if (pos == 18) v = tail[copy + mod4 - 1];
+        }
+        w |= (uint64_t)v << (8 * b);
+    }
+    hhq_update(s, w);
+}
+
+// 10 x PermuteAndUpdate, ModularReduction; lane q writes digest bytes [8q, 8q+8).
+__device__ __forceinline__ void hhq_finish(HHQuad& s, uint8_t* out, uint32_t q) {
+#pragma unroll 1
+    for (int it = 0; it < 10; ++it) {
+        const uint32_t lo = quad_swap_halves((uint32_t)s.v0), hi = quad_swap_halves((uint32_t)(s.v0 >> 32));
+        hhq_update(s, (uint64_t)hi | ((uint64_t)lo << 32));  // rot32 of v0[q^2]
+    }
+    const uint64_t a_v1 = s.v1 + s.mul1, a_v0 = s.v0 + s.mul0;
+    const uint32_t p_lo = quad_swap_pairs((uint32_t)a_v1), p_hi = quad_swap_pairs((uint32_t)(a_v1 >> 32));
+    const uint64_t partner_v1 = (uint64_t)p_lo | ((uint64_t)p_hi << 32);
+    uint64_t h;
+    if (q & 1) {  // h[odd] from a3 = own v1+mul1, a2 = partner's, a1 = own v0+mul0
+        const uint64_t a3 = a_v1 & 0x3FFFFFFFFFFFFFFFull, a2 = partner_v1;
+        h = a_v0 ^ ((a3 << 1) | (a2 >> 63)) ^ ((a3 << 2) | (a2 >> 62));
+    } else {      // h[even] = a0 ^ (a2 << 1) ^ (a2 << 2), a2 = own v1+mul1
+        h = a_v0 ^ (a_v1 << 1) ^ (a_v1 << 2);
+    }
+#pragma unroll
+    for (int b = 0; b < 8; ++b) out[8 * q + b] = (uint8_t)(h >> (8 * b));  // any alignment
+}
+
+__device__ __forceinline__ uint64_t ld_u64_aligned(const uint8_t* p) {
+    const uint2 v = *(const uint2*)p;
+    return (uint64_t)v.x | ((uint64_t)v.y << 32);
+}
+
+// Plain / per-shard batch hash: quad j hashes message j (16 messages per wave).
+// Every lane issues its own 8-byte loads; 4 packets are fetched ahead.
+__global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
+    const uint64_t j = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 2;
+    const uint32_t q = threadIdx.x & 3u;
+    if (j >= p.n) return;  // whole quads exit together
     const uint64_t stripe = j / p.shards, shard = j - stripe * p.shards;
     const uint8_t* msg = p.data + stripe * p.stripe_stride + shard * p.shard_pitch;
-    HHState s;
-    hh_reset(p.key, s);
-    const uint64_t full = p.len & ~(uint64_t)31;
+    HHQuad s;
+    hhq_init(s, p.key, q);
+    const uint64_t packets = p.len >> 5;
+    uint64_t t = 0;
     if (p.aligned16) {
-#pragma unroll 1
-        for (uint64_t i = 0; i < full; i += 32) {
-            const uint4 a = *(const uint4*)(msg + i);
-            const uint4 b = *(const uint4*)(msg + i + 16);
-            const uint64_t lanes[4] = {(uint64_t)a.x | ((uint64_t)a.y << 32), (uint64_t)a.z | ((uint64_t)a.w << 32),
-                                       (uint64_t)b.x | ((uint64_t)b.y << 32), (uint64_t)b.z | ((uint64_t)b.w << 32)};
-            hh_update(lanes, s);
-        }
-    } else {
-#pragma unroll 1
-        for (uint64_t i = 0; i < full; i += 32) {
-            const uint64_t lanes[4] = {ld64_any(msg + i), ld64_any(msg + i + 8), ld64_any(msg + i + 16),
-                                       ld64_any(msg + i + 24)};
-            hh_update(lanes, s);
-        }
-    }
-    uint8_t digest[32];
-    hh_finish(msg + full, (uint32_t)(p.len & 31), s, digest);
-    uint8_t* o = p.out + j * 32u;
+        for (; t + 4 <= packets; t += 4) {
+            uint64_t w[4];
 #pragma unroll
-    for (int i = 0; i < 32; ++i) o[i] = digest[i];
+            for (int i = 0; i < 4; ++i) w[i] = ld_u64_aligned(msg + (t + i) * 32 + 8 * q);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) hhq_update(s, w[i]);
+        }
+        for (; t < packets; ++t) hhq_update(s, ld_u64_aligned(msg + t * 32 + 8 * q));
+    } else {
+        for (; t < packets; ++t) hhq_update(s, ld64_any(msg + t * 32 + 8 * q));
+    }
+    const uint32_t rem = (uint32_t)(p.len & 31);
+    if (rem) hhq_remainder(s, msg + packets * 32, rem, q);
+    hhq_finish(s, p.out + j * 32u, q);
+}
+
+// ---------------------------------------------------------------------------
+// Fused RS encode + per-shard HighwayHash-256 (BitrotWriter digests,
+// bitrot.rs:496-502) in one pass over HBM.  One 64-lane workgroup per stripe
+// walks the stripe in 512-byte column chunks: load the k data chunks (8 B per
+// lane per shard), compute and store the m parity chunks, stage all k+m chunks
+// in LDS, then 4-lane quads advance the k+m HighwayHash streams by 16 packets
+// each while the next chunk's loads are in flight.  HighwayHash is sequential
+// per shard, so its parallelism is (k+m) streams x 4 lanes per stripe; the
+// 4096-stripe batch keeps 4 such waves per SIMD.
+constexpr uint32_t kFusedChunk = 512;                 // bytes per shard per step
+constexpr uint32_t kFusedPitch = kFusedChunk + 32;    // LDS row pitch: conflict-free ds_read_b64
+
+template <int C, int R>
+__global__ __launch_bounds__(64) void k_encode_hash_fused(const GfApplyParams p, const HashParams h) {
+    // LDS: [C][R] coefficient tables (32 B each: T0 T0' T1 T1' | T2), then the
+    // (C+R) chunk rows.  The tables live in LDS rather than registers: kept in
+    // SGPR/VGPR across the chunk loop they cost 64+ VGPRs and dropped the
+    // kernel below the 4 waves per SIMD that keep a 4096-stripe batch resident.
+    extern __shared__ uint8_t lds_all[];
+    constexpr int T = C + R;
+    constexpr int NR = (T + 15) / 16;  // hash rounds of 16 streams
+    constexpr uint32_t kTabBytes = C * R * 32;
+    uint8_t* lds = lds_all + kTabBytes;
+    const uint32_t lane = threadIdx.x, q = lane & 3u;
+    const uint64_t stripe = blockIdx.x;
+    uint8_t* sb = p.out_base + stripe * p.stripe_stride;
+    const uint32_t chunks = p.units;  // S / kFusedChunk
+
+    if (lane == 0) {
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                uint8_t* d = lds_all + (c * R + r) * 32;
+                *(uint4*)d = make_uint4(p.tab[r][c][0], p.tab[r][c][1], p.tab[r][c][2], p.tab[r][c][3]);
+                *(uint32_t*)(d + 16) = p.tab[r][c][4];
+            }
+    }
+    __syncthreads();
+
+    HHQuad st[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) hhq_init(st[r], h.key, q);
+
+    uint2 x[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) x[c] = *(const uint2*)(sb + p.in_off[c] + lane * 8u);
+
+#pragma unroll 1
+    for (uint32_t ch = 0; ch < chunks; ++ch) {
+        const uint64_t off = (uint64_t)ch * kFusedChunk + lane * 8u;
+        uint32_t acc[R][2];
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = 0u;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const uint32_t s0a = x[c].x & 0x07070707u, s0b = x[c].y & 0x07070707u;
+            const uint32_t s1a = (x[c].x >> 3) & 0x07070707u, s1b = (x[c].y >> 3) & 0x07070707u;
+            const uint32_t s2a = (x[c].x >> 6) & 0x03030303u, s2b = (x[c].y >> 6) & 0x03030303u;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint8_t* tp = lds_all + (c * R + r) * 32;  // wave-uniform: broadcast read
+                const uint4 t4 = *(const uint4*)tp;
+                const uint32_t t2 = *(const uint32_t*)(tp + 16);
+                acc[r][0] ^= __builtin_amdgcn_perm(t4.y, t4.x, s0a) ^ __builtin_amdgcn_perm(t4.w, t4.z, s1a) ^
+                             __builtin_amdgcn_perm(t2, t2, s2a);
+                acc[r][1] ^= __builtin_amdgcn_perm(t4.y, t4.x, s0b) ^ __builtin_amdgcn_perm(t4.w, t4.z, s1b) ^
+                             __builtin_amdgcn_perm(t2, t2, s2b);
+            }
+            *(uint2*)(lds + c * kFusedPitch + lane * 8u) = x[c];
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint2 v = make_uint2(acc[r][0], acc[r][1]);
+            *(uint2*)(sb + p.out_off[r] + off) = v;
+            *(uint2*)(lds + (C + r) * kFusedPitch + lane * 8u) = v;
+        }
+        // next chunk's loads fly while the quads hash this one
+        if (ch + 1 < chunks) {
+#pragma unroll
+            for (int c = 0; c < C; ++c) x[c] = *(const uint2*)(sb + p.in_off[c] + off + kFusedChunk);
+        }
+        // The workgroup is one wave and a wave's LDS operations execute in
+        // order, so the rows written above are visible to the reads below and
+        // the next chunk's writes cannot overtake them: no s_barrier (which
+        // would also drain the prefetch loads with s_waitcnt vmcnt(0)).
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const uint32_t g = r * 16 + (lane >> 2);
+            if (g < (uint32_t)T) {
+                const uint8_t* row = lds + g * kFusedPitch + 8 * q;
+#pragma unroll 4
+                for (int t = 0; t < (int)(kFusedChunk / 32); ++t) {
+                    const uint2 v = *(const uint2*)(row + t * 32);
+                    hhq_update(st[r], (uint64_t)v.x | ((uint64_t)v.y << 32));
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const uint32_t g = r * 16 + (lane >> 2);
+        if (g < (uint32_t)T) hhq_finish(st[r], h.out + (stripe * T + g) * 32u, q);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -316,9 +427,7 @@ static GfKernel pick_byte(int R) {
 hipError_t launch_gf_apply_vec(GfApplyParams p, uint64_t n_stripes, hipStream_t stream) {
     GfKernel k = pick_vec((int)p.C, (int)p.R);
     if (!k || p.units == 0 || n_stripes == 0) return hipErrorInvalidValue;
-    if (p.units_per_thread == 0) p.units_per_thread = 1;
-    const uint32_t per_block = 256u * p.units_per_thread;
-    p.chunks_per_stripe = (p.units + per_block - 1) / per_block;
+    p.chunks_per_stripe = (p.units + 255u) / 256u;
     const uint64_t blocks = (uint64_t)p.chunks_per_stripe * n_stripes;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k, dim3((uint32_t)blocks), dim3(256), 0, stream, p);
@@ -338,8 +447,60 @@ hipError_t launch_gf_apply_byte(GfApplyParams p, uint64_t n_stripes, hipStream_t
 
 hipError_t launch_hh256(const HashParams& p, hipStream_t stream) {
     if (p.n == 0) return hipSuccess;
-    const uint64_t blocks = (p.n + 63u) / 64u;
-    hipLaunchKernelGGL(k_hh256_thread, dim3((uint32_t)blocks), dim3(64), 0, stream, p);
+    const uint64_t blocks = (p.n * 4u + 255u) / 256u;  // one quad per message
+    if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_hh256_quad, dim3((uint32_t)blocks), dim3(256), 0, stream, p);
+    return hipGetLastError();
+}
+
+using FusedKernel = void (*)(const GfApplyParams, const HashParams);
+
+template <int C>
+static FusedKernel pick_fused_r(int R) {
+    switch (R) {
+        case 1: return k_encode_hash_fused<C, 1>;
+        case 2: return k_encode_hash_fused<C, 2>;
+        case 3: return k_encode_hash_fused<C, 3>;
+        case 4: return k_encode_hash_fused<C, 4>;
+    }
+    return nullptr;
+}
+
+static FusedKernel pick_fused(int C, int R) {
+    switch (C) {
+        case 1: return pick_fused_r<1>(R);
+        case 2: return pick_fused_r<2>(R);
+        case 3: return pick_fused_r<3>(R);
+        case 4: return pick_fused_r<4>(R);
+        case 5: return pick_fused_r<5>(R);
+        case 6: return pick_fused_r<6>(R);
+        case 7: return pick_fused_r<7>(R);
+        case 8: return pick_fused_r<8>(R);
+        case 9: return pick_fused_r<9>(R);
+        case 10: return pick_fused_r<10>(R);
+        case 11: return pick_fused_r<11>(R);
+        case 12: return pick_fused_r<12>(R);
+        case 13: return pick_fused_r<13>(R);
+        case 14: return pick_fused_r<14>(R);
+        case 15: return pick_fused_r<15>(R);
+        case 16: return pick_fused_r<16>(R);
+    }
+    return nullptr;
+}
+
+bool fused_supported(int C, int R, uint64_t shard_len) {
+    return C >= 1 && C <= kMaxC && R >= 1 && R <= kMaxR && shard_len >= kFusedChunk &&
+           shard_len % kFusedChunk == 0 && shard_len / kFusedChunk <= 0xffffffffull;
+}
+
+hipError_t launch_encode_hash_fused(GfApplyParams p, const HashParams& h, uint64_t shard_len, uint64_t n_stripes,
+                                    hipStream_t stream) {
+    FusedKernel k = pick_fused((int)p.C, (int)p.R);
+    if (!k || !fused_supported((int)p.C, (int)p.R, shard_len) || n_stripes == 0 || n_stripes > 0x7fffffffull)
+        return hipErrorInvalidValue;
+    p.units = (uint32_t)(shard_len / kFusedChunk);
+    const size_t lds = (size_t)p.C * p.R * 32 + (size_t)(p.C + p.R) * kFusedPitch;
+    hipLaunchKernelGGL(k, dim3((uint32_t)n_stripes), dim3(64), lds, stream, p, h);
     return hipGetLastError();
 }
 

@@ -262,14 +262,34 @@ int hip_status(hipError_t e) {
     return RSG_ERR_DEVICE;
 }
 
-// Units per thread for the vector path (env RSG_UNITS_PER_THREAD overrides).
-uint32_t units_per_thread() {
-    static const uint32_t v = [] {
-        const char* s = std::getenv("RSG_UNITS_PER_THREAD");
-        long x = s ? std::strtol(s, nullptr, 10) : 1;
-        return (uint32_t)(x < 1 ? 1 : (x > 64 ? 64 : x));
+
+// Kernel parameter block for rows [r0, r0+4) x inputs [c0, c0+16) of rs.
+void fill_params(const RowSet& rs, int r0, int c0, const uint8_t* base, uint8_t* out_base, uint64_t stride,
+                 uint64_t out_stride, uint32_t mode, uint8_t* ok_flags, rsg::GfApplyParams& p) {
+    const int R = std::min(rsg::kMaxR, rs.R - r0);
+    const int C = std::min(rsg::kMaxC, rs.C - c0);
+    std::memset(&p, 0, sizeof(p));
+    p.base = base;
+    p.out_base = out_base;
+    p.stripe_stride = stride;
+    p.out_stripe_stride = out_stride;
+    for (int c = 0; c < C; ++c) p.in_off[c] = rs.in_off[c0 + c];
+    for (int r = 0; r < R; ++r) p.out_off[r] = rs.out_off[r0 + r];
+    for (int r = 0; r < R; ++r)
+        for (int c = 0; c < C; ++c) coef_tables(rs.coef[(size_t)(r0 + r) * rs.C + c0 + c], p.tab[r][c]);
+    p.ok_flags = ok_flags;
+    p.C = (uint32_t)C;
+    p.R = (uint32_t)R;
+    p.mode = mode;
+}
+
+// RSG_FUSED=0 disables the fused encode+hash kernel (A/B measurements).
+bool fused_enabled() {
+    static const bool on = [] {
+        const char* s = std::getenv("RSG_FUSED");
+        return !(s && s[0] == '0');
     }();
-    return v;
+    return on;
 }
 
 int apply_rows(const RowSet& rs, const uint8_t* base, uint8_t* out_base, uint64_t stride, uint64_t out_stride,
@@ -284,26 +304,13 @@ int apply_rows(const RowSet& rs, const uint8_t* base, uint8_t* out_base, uint64_
     if (units > 0xffffffffull) return RSG_ERR_UNSUPPORTED;
 
     for (int r0 = 0; r0 < rs.R; r0 += rsg::kMaxR) {
-        const int R = std::min(rsg::kMaxR, rs.R - r0);
         for (int c0 = 0; c0 < rs.C; c0 += rsg::kMaxC) {
-            const int C = std::min(rsg::kMaxC, rs.C - c0);
             rsg::GfApplyParams p;
-            std::memset(&p, 0, sizeof(p));
-            p.base = base;
-            p.out_base = out_base;
-            p.stripe_stride = stride;
-            p.out_stripe_stride = out_stride;
-            for (int c = 0; c < C; ++c) p.in_off[c] = rs.in_off[c0 + c];
-            for (int r = 0; r < R; ++r) p.out_off[r] = rs.out_off[r0 + r];
-            for (int r = 0; r < R; ++r)
-                for (int c = 0; c < C; ++c) coef_tables(rs.coef[(size_t)(r0 + r) * rs.C + c0 + c], p.tab[r][c]);
-            p.ok_flags = ok_flags;
-            p.C = (uint32_t)C;
-            p.R = (uint32_t)R;
-            p.mode = mode == rsg::GF_MODE_COMPARE ? mode : (c0 == 0 ? rsg::GF_MODE_STORE : rsg::GF_MODE_XOR);
+            fill_params(rs, r0, c0, base, out_base, stride, out_stride,
+                        mode == rsg::GF_MODE_COMPARE ? mode : (c0 == 0 ? rsg::GF_MODE_STORE : rsg::GF_MODE_XOR),
+                        ok_flags, p);
             if (units) {
                 p.units = (uint32_t)units;
-                p.units_per_thread = units_per_thread();
                 int st = hip_status(rsg::launch_gf_apply_vec(p, n, stream));
                 if (st) return st;
             }
@@ -474,6 +481,22 @@ int rsg_encode_batch_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
     if (n && !d_stripes) return RSG_ERR_INVALID_ARG;
     if (shard_pitch < shard_len) return RSG_ERR_INCONSISTENT_LENGTH;
     hipStream_t s = pick_stream(ctx, stream);
+    const bool want_hash = d_digests && algo != RSG_HASH_NONE;
+    if (want_hash && !hash_key(algo)) return RSG_ERR_INVALID_ARG;
+    const bool aligned = ((uintptr_t)d_stripes % 16 == 0) && shard_pitch % 16 == 0 && stripe_stride % 16 == 0;
+    if (want_hash && m > 0 && n > 0 && aligned && fused_enabled() && rsg::fused_supported(k, m, shard_len)) {
+        // one pass: parity + all k+m digests (rs_kernels.hip k_encode_hash_fused)
+        auto cd = get_codec(k, m);
+        if (!cd) return RSG_ERR_INVALID_ARG;
+        RowSet rs = encode_rows(*cd, shard_pitch);
+        rsg::GfApplyParams p;
+        fill_params(rs, 0, 0, d_stripes, d_stripes, stripe_stride, stripe_stride, rsg::GF_MODE_STORE, nullptr, p);
+        rsg::HashParams h;
+        std::memset(&h, 0, sizeof(h));
+        std::memcpy(h.key, hash_key(algo), sizeof(h.key));
+        h.out = d_digests;
+        return hip_status(rsg::launch_encode_hash_fused(p, h, shard_len, n, s));
+    }
     if (m > 0 && shard_len > 0) {
         auto cd = get_codec(k, m);
         if (!cd) return RSG_ERR_INVALID_ARG;
@@ -482,7 +505,7 @@ int rsg_encode_batch_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
                         nullptr, s);
         if (st) return st;
     }
-    if (d_digests && algo != RSG_HASH_NONE) {
+    if (want_hash) {
         st = hash_messages(algo, d_stripes, shard_len, n * (uint64_t)(k + m), (uint64_t)(k + m), shard_pitch,
                            stripe_stride, d_digests, s);
         if (st) return st;
