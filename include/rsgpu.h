@@ -142,6 +142,20 @@ int rsg_hash_batch_dev(rsg_ctx *ctx, int algo, const uint8_t *d_data, size_t len
 /* Block until all work queued on `stream` (NULL = the null stream) is done. */
 int rsg_sync(rsg_ctx *ctx, void *stream);
 
+/* ---- host-batch API: the PUT path starts and ends in host memory ----
+ * Encode n stripes held in HOST memory (same addressing as the device-batch
+ * API): sub-batches are pipelined over two streams (H2D data -> encode + fused
+ * digests -> D2H parity + digests) and the call returns when all are done.
+ * This is the batched replacement for encode_batched's per-block
+ * encode_data_block calls (encode.rs:795-919); pin the buffers (rsg_pin or a
+ * pinned allocation) for full PCIe bandwidth. */
+int rsg_encode_batch_host(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t n, uint8_t *h_stripes,
+                          size_t shard_pitch, size_t stripe_stride, uint8_t *h_digests, int algo);
+
+/* Page-lock / release host memory for DMA (hipHostRegister). */
+int rsg_pin(void *ptr, size_t bytes);
+int rsg_unpin(void *ptr);
+
 #ifdef __cplusplus
 }
 #endif

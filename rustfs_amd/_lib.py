@@ -50,7 +50,7 @@ EXPORTED = (
     "rsg_abi_version", "rsg_strerror", "rsg_device_count", "rsg_create", "rsg_destroy",
     "rsg_matrix", "rsg_check_geometry", "rsg_encode", "rsg_reconstruct", "rsg_verify",
     "rsg_hash", "rsg_encode_batch_dev", "rsg_reconstruct_batch_dev", "rsg_verify_batch_dev",
-    "rsg_hash_batch_dev", "rsg_sync",
+    "rsg_hash_batch_dev", "rsg_sync", "rsg_encode_batch_host", "rsg_pin", "rsg_unpin",
 )
 
 
@@ -100,6 +100,9 @@ def load():
         L.rsg_verify_batch_dev.argtypes = [P, I, I, S, S, P, S, S, P, P]
         L.rsg_hash_batch_dev.argtypes = [P, I, P, S, S, S, P, P]
         L.rsg_sync.argtypes = [P, P]
+        L.rsg_encode_batch_host.argtypes = [P, I, I, S, S, P, S, S, P, I]
+        L.rsg_pin.argtypes = [P, S]
+        L.rsg_unpin.argtypes = [P]
         _lib = L
         return L
 

@@ -154,13 +154,19 @@ __device__ __forceinline__ uint32_t quad_swap_halves(uint32_t x) {  // lane q <-
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
 }
 
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// Built as a 2-dword vector so the two v_perm results land in one register
+// pair and the following 64-bit add is a single v_lshl_add_u64 (building it
+// with shifts/ors cost an extra v_mov and add per zipper).
 __device__ __forceinline__ uint64_t hh_zip(uint64_t x, uint32_t sel_hi) {
-    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-    const uint32_t other_hi = quad_swap_pairs(hi);
-    const uint32_t t = __builtin_amdgcn_perm(hi, lo, 0x05020C03u);        // own.b3, 0, own.b2, own.b5
-    const uint32_t zlo = __builtin_amdgcn_perm(other_hi, t, 0x03020400u);  // t.b0, other.b4, t.b2, t.b3
-    const uint32_t zhi = __builtin_amdgcn_perm(other_hi, lo, sel_hi);
-    return (uint64_t)zlo | ((uint64_t)zhi << 32);
+    const u32x2 xv = __builtin_bit_cast(u32x2, x);
+    const uint32_t other_hi = quad_swap_pairs(xv.y);
+    const uint32_t t = __builtin_amdgcn_perm(xv.y, xv.x, 0x05020C03u);  // own.b3, 0, own.b2, own.b5
+    u32x2 z;
+    z.x = __builtin_amdgcn_perm(other_hi, t, 0x03020400u);  // t.b0, other.b4, t.b2, t.b3
+    z.y = __builtin_amdgcn_perm(other_hi, xv.x, sel_hi);
+    return __builtin_bit_cast(uint64_t, z);
 }
 
 __device__ __forceinline__ void hhq_init(HHQuad& s, const uint64_t* key, uint32_t q) {
@@ -270,33 +276,44 @@ __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
 
 // ---------------------------------------------------------------------------
 // Fused RS encode + per-shard HighwayHash-256 (BitrotWriter digests,
-// bitrot.rs:496-502) in one pass over HBM.  One 64-lane workgroup per stripe
-// walks the stripe in 512-byte column chunks: load the k data chunks (8 B per
-// lane per shard), compute and store the m parity chunks, stage all k+m chunks
-// in LDS, then 4-lane quads advance the k+m HighwayHash streams by 16 packets
-// each while the next chunk's loads are in flight.  HighwayHash is sequential
-// per shard, so its parallelism is (k+m) streams x 4 lanes per stripe; the
-// 4096-stripe batch keeps 4 such waves per SIMD.
+// bitrot.rs:496-502) in one pass over HBM.  One workgroup per stripe, two
+// waves with fixed roles, walking the stripe in 512-byte column chunks:
+//   wave 0 (encoder): loads the k data chunks (8 B per lane per shard),
+//     computes and stores the m parity chunks, and stages all k+m chunks in
+//     LDS; the next chunk's loads are issued before it waits for the hasher.
+//   wave 1 (hasher): 4-lane quads advance the k+m HighwayHash streams by 16
+//     packets per chunk (HighwayHash is sequential per shard, so a stripe
+//     offers only (k+m) x 4 lanes of hash parallelism).
+// Per chunk:  encoder  compute(i) | bar A | write rows(i) | bar B | loads(i+2)..
+//             hasher              | bar A |               | bar B | hash(i) ..
+// so the encoder's arithmetic for chunk i+1 overlaps the hashing of chunk i.
+// Barriers are raw s_barrier with an explicit lgkmcnt wait: __syncthreads()
+// would also drain the in-flight global loads (vmcnt(0)).
 constexpr uint32_t kFusedChunk = 512;                 // bytes per shard per step
 constexpr uint32_t kFusedPitch = kFusedChunk + 32;    // LDS row pitch: conflict-free ds_read_b64
 
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 template <int C, int R>
-__global__ __launch_bounds__(64) void k_encode_hash_fused(const GfApplyParams p, const HashParams h) {
+__global__ __launch_bounds__(128) void k_encode_hash_fused(const GfApplyParams p, const HashParams h) {
     // LDS: [C][R] coefficient tables (32 B each: T0 T0' T1 T1' | T2), then the
-    // (C+R) chunk rows.  The tables live in LDS rather than registers: kept in
-    // SGPR/VGPR across the chunk loop they cost 64+ VGPRs and dropped the
-    // kernel below the 4 waves per SIMD that keep a 4096-stripe batch resident.
+    // (C+R) chunk rows.  Tables are read from LDS (broadcast) at their use:
+    // held in registers across the chunk loop they cost 64+ VGPRs.
     extern __shared__ uint8_t lds_all[];
     constexpr int T = C + R;
     constexpr int NR = (T + 15) / 16;  // hash rounds of 16 streams
     constexpr uint32_t kTabBytes = C * R * 32;
-    uint8_t* lds = lds_all + kTabBytes;
-    const uint32_t lane = threadIdx.x, q = lane & 3u;
+    uint8_t* rows = lds_all + kTabBytes;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u, q = lane & 3u;
     const uint64_t stripe = blockIdx.x;
     uint8_t* sb = p.out_base + stripe * p.stripe_stride;
     const uint32_t chunks = p.units;  // S / kFusedChunk
 
-    if (lane == 0) {
+    if (threadIdx.x == 0) {
 #pragma unroll
         for (int c = 0; c < C; ++c)
 #pragma unroll
@@ -308,71 +325,79 @@ __global__ __launch_bounds__(64) void k_encode_hash_fused(const GfApplyParams p,
     }
     __syncthreads();
 
-    HHQuad st[NR];
+    if (__builtin_amdgcn_readfirstlane(wave) == 0) {
+        // ------------------------------ encoder ------------------------------
+        uint2 x[C];
 #pragma unroll
-    for (int r = 0; r < NR; ++r) hhq_init(st[r], h.key, q);
-
-    uint2 x[C];
-#pragma unroll
-    for (int c = 0; c < C; ++c) x[c] = *(const uint2*)(sb + p.in_off[c] + lane * 8u);
-
+        for (int c = 0; c < C; ++c) x[c] = *(const uint2*)(sb + p.in_off[c] + lane * 8u);
 #pragma unroll 1
-    for (uint32_t ch = 0; ch < chunks; ++ch) {
-        const uint64_t off = (uint64_t)ch * kFusedChunk + lane * 8u;
-        uint32_t acc[R][2];
+        for (uint32_t ch = 0; ch < chunks; ++ch) {
+            const uint64_t off = (uint64_t)ch * kFusedChunk + lane * 8u;
+            uint32_t acc[R][2];
 #pragma unroll
-        for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = 0u;
+            for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = 0u;
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
-            const uint32_t s0a = x[c].x & 0x07070707u, s0b = x[c].y & 0x07070707u;
-            const uint32_t s1a = (x[c].x >> 3) & 0x07070707u, s1b = (x[c].y >> 3) & 0x07070707u;
-            const uint32_t s2a = (x[c].x >> 6) & 0x03030303u, s2b = (x[c].y >> 6) & 0x03030303u;
+            for (int c = 0; c < C; ++c) {
+                const uint32_t s0a = x[c].x & 0x07070707u, s0b = x[c].y & 0x07070707u;
+                const uint32_t s1a = (x[c].x >> 3) & 0x07070707u, s1b = (x[c].y >> 3) & 0x07070707u;
+                const uint32_t s2a = (x[c].x >> 6) & 0x03030303u, s2b = (x[c].y >> 6) & 0x03030303u;
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const uint8_t* tp = lds_all + (c * R + r) * 32;  // wave-uniform: broadcast read
-                const uint4 t4 = *(const uint4*)tp;
-                const uint32_t t2 = *(const uint32_t*)(tp + 16);
-                acc[r][0] ^= __builtin_amdgcn_perm(t4.y, t4.x, s0a) ^ __builtin_amdgcn_perm(t4.w, t4.z, s1a) ^
-                             __builtin_amdgcn_perm(t2, t2, s2a);
-                acc[r][1] ^= __builtin_amdgcn_perm(t4.y, t4.x, s0b) ^ __builtin_amdgcn_perm(t4.w, t4.z, s1b) ^
-                             __builtin_amdgcn_perm(t2, t2, s2b);
+                for (int r = 0; r < R; ++r) {
+                    const uint8_t* tp = lds_all + (c * R + r) * 32;  // wave-uniform: broadcast read
+                    const uint4 t4 = *(const uint4*)tp;
+                    const uint32_t t2 = *(const uint32_t*)(tp + 16);
+                    acc[r][0] ^= __builtin_amdgcn_perm(t4.y, t4.x, s0a) ^ __builtin_amdgcn_perm(t4.w, t4.z, s1a) ^
+                                 __builtin_amdgcn_perm(t2, t2, s2a);
+                    acc[r][1] ^= __builtin_amdgcn_perm(t4.y, t4.x, s0b) ^ __builtin_amdgcn_perm(t4.w, t4.z, s1b) ^
+                                 __builtin_amdgcn_perm(t2, t2, s2b);
+                }
             }
-            *(uint2*)(lds + c * kFusedPitch + lane * 8u) = x[c];
-        }
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const uint2 v = make_uint2(acc[r][0], acc[r][1]);
-            *(uint2*)(sb + p.out_off[r] + off) = v;
-            *(uint2*)(lds + (C + r) * kFusedPitch + lane * 8u) = v;
-        }
-        // next chunk's loads fly while the quads hash this one
-        if (ch + 1 < chunks) {
+            for (int r = 0; r < R; ++r) *(uint2*)(sb + p.out_off[r] + off) = make_uint2(acc[r][0], acc[r][1]);
+            uint2 y[C];
+            if (ch + 1 < chunks) {
 #pragma unroll
-            for (int c = 0; c < C; ++c) x[c] = *(const uint2*)(sb + p.in_off[c] + off + kFusedChunk);
-        }
-        // The workgroup is one wave and a wave's LDS operations execute in
-        // order, so the rows written above are visible to the reads below and
-        // the next chunk's writes cannot overtake them: no s_barrier (which
-        // would also drain the prefetch loads with s_waitcnt vmcnt(0)).
-        __builtin_amdgcn_wave_barrier();
+                for (int c = 0; c < C; ++c) y[c] = *(const uint2*)(sb + p.in_off[c] + off + kFusedChunk);
+            }
+            lds_barrier();  // A: the hasher is done with chunk ch-1's rows
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            const uint32_t g = r * 16 + (lane >> 2);
-            if (g < (uint32_t)T) {
-                const uint8_t* row = lds + g * kFusedPitch + 8 * q;
+            for (int c = 0; c < C; ++c) *(uint2*)(rows + c * kFusedPitch + lane * 8u) = x[c];
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                *(uint2*)(rows + (C + r) * kFusedPitch + lane * 8u) = make_uint2(acc[r][0], acc[r][1]);
+            lds_barrier();  // B: rows of chunk ch are ready
+            if (ch + 1 < chunks) {
+#pragma unroll
+                for (int c = 0; c < C; ++c) x[c] = y[c];
+            }
+        }
+    } else {
+        // ------------------------------ hasher -------------------------------
+        HHQuad st[NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) hhq_init(st[r], h.key, q);
+#pragma unroll 1
+        for (uint32_t ch = 0; ch < chunks; ++ch) {
+            lds_barrier();  // A
+            lds_barrier();  // B
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const uint32_t g = r * 16 + (lane >> 2);
+                if (g < (uint32_t)T) {
+                    const uint8_t* row = rows + g * kFusedPitch + 8 * q;
 #pragma unroll 4
-                for (int t = 0; t < (int)(kFusedChunk / 32); ++t) {
-                    const uint2 v = *(const uint2*)(row + t * 32);
-                    hhq_update(st[r], (uint64_t)v.x | ((uint64_t)v.y << 32));
+                    for (int t = 0; t < (int)(kFusedChunk / 32); ++t) {
+                        const uint2 v = *(const uint2*)(row + t * 32);
+                        hhq_update(st[r], (uint64_t)v.x | ((uint64_t)v.y << 32));
+                    }
                 }
             }
         }
-        __builtin_amdgcn_wave_barrier();
-    }
 #pragma unroll
-    for (int r = 0; r < NR; ++r) {
-        const uint32_t g = r * 16 + (lane >> 2);
-        if (g < (uint32_t)T) hhq_finish(st[r], h.out + (stripe * T + g) * 32u, q);
+        for (int r = 0; r < NR; ++r) {
+            const uint32_t g = r * 16 + (lane >> 2);
+            if (g < (uint32_t)T) hhq_finish(st[r], h.out + (stripe * T + g) * 32u, q);
+        }
     }
 }
 
@@ -500,7 +525,7 @@ hipError_t launch_encode_hash_fused(GfApplyParams p, const HashParams& h, uint64
         return hipErrorInvalidValue;
     p.units = (uint32_t)(shard_len / kFusedChunk);
     const size_t lds = (size_t)p.C * p.R * 32 + (size_t)(p.C + p.R) * kFusedPitch;
-    hipLaunchKernelGGL(k, dim3((uint32_t)n_stripes), dim3(64), lds, stream, p, h);
+    hipLaunchKernelGGL(k, dim3((uint32_t)n_stripes), dim3(128), lds, stream, p, h);
     return hipGetLastError();
 }
 

@@ -367,6 +367,12 @@ struct rsg_ctx {
     uint8_t* d_scratch = nullptr;
     size_t scratch_cap = 0;
 
+    // host-batch pipeline (rsg_encode_batch_host): two stream/staging pairs
+    std::mutex pipe_mu;
+    hipStream_t pipe_stream[2] = {nullptr, nullptr};
+    uint8_t* d_stage[2] = {nullptr, nullptr};
+    size_t stage_cap = 0;
+
     int ensure_scratch(size_t bytes) {
         if (bytes <= scratch_cap) return RSG_OK;
         if (d_scratch) (void)hipFree(d_scratch);
@@ -376,6 +382,26 @@ struct rsg_ctx {
         hipError_t e = hipMalloc((void**)&d_scratch, cap);
         if (e != hipSuccess) return hip_status(e);
         scratch_cap = cap;
+        return RSG_OK;
+    }
+
+    int ensure_pipeline(size_t bytes) {
+        for (int i = 0; i < 2; ++i)
+            if (!pipe_stream[i]) {
+                hipError_t e = hipStreamCreateWithFlags(&pipe_stream[i], hipStreamNonBlocking);
+                if (e != hipSuccess) return hip_status(e);
+            }
+        if (bytes <= stage_cap) return RSG_OK;
+        for (int i = 0; i < 2; ++i) {
+            if (d_stage[i]) (void)hipFree(d_stage[i]);
+            d_stage[i] = nullptr;
+        }
+        stage_cap = 0;
+        for (int i = 0; i < 2; ++i) {
+            hipError_t e = hipMalloc((void**)&d_stage[i], bytes);
+            if (e != hipSuccess) return hip_status(e);
+        }
+        stage_cap = bytes;
         return RSG_OK;
     }
 };
@@ -449,10 +475,80 @@ void rsg_destroy(rsg_ctx* ctx) {
         (void)hipStreamDestroy(ctx->stream);
     }
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+    for (int i = 0; i < 2; ++i) {
+        if (ctx->pipe_stream[i]) {
+            (void)hipStreamSynchronize(ctx->pipe_stream[i]);
+            (void)hipStreamDestroy(ctx->pipe_stream[i]);
+        }
+        if (ctx->d_stage[i]) (void)hipFree(ctx->d_stage[i]);
+    }
     delete ctx;
 }
 
 int rsg_check_geometry(int k, int m) { return check_geometry(k, m); }
+
+int rsg_pin(void* ptr, size_t bytes) {
+    if (!ptr || !bytes) return RSG_ERR_INVALID_ARG;
+    return hip_status(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+}
+
+int rsg_unpin(void* ptr) {
+    if (!ptr) return RSG_ERR_INVALID_ARG;
+    return hip_status(hipHostUnregister(ptr));
+}
+
+// Host-memory batch encode: stripes in host memory (pinned for full PCIe rate),
+// a3 layout.  Sub-batches of `chunk` stripes alternate over two stream/staging
+// pairs: H2D of the data shards (one 2-D copy), encode (+ fused digests), D2H of
+// parity (+ digests); the copy engines overlap the kernel of the other pair.
+int rsg_encode_batch_host(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n, uint8_t* h_stripes,
+                          size_t shard_pitch, size_t stripe_stride, uint8_t* h_digests, int algo) {
+    int st = enter(ctx);
+    if (st) return st;
+    if ((st = check_geometry(k, m))) return st;
+    if (n && !h_stripes) return RSG_ERR_INVALID_ARG;
+    if (shard_pitch < shard_len) return RSG_ERR_INCONSISTENT_LENGTH;
+    if (stripe_stride < (size_t)(k + m) * shard_pitch) return RSG_ERR_INVALID_ARG;
+    if (n == 0 || m == 0 || shard_len == 0) return RSG_OK;
+    const bool want_hash = h_digests && algo != RSG_HASH_NONE;
+    std::lock_guard<std::mutex> g(ctx->pipe_mu);
+    // device layout: compact a3 stripes, 256-B aligned shards
+    const uint64_t dpitch = round_up(shard_len, 256);
+    const uint64_t dstride = dpitch * (k + m);
+    const uint64_t target = 96ull << 20;  // ~96 MiB per sub-batch
+    const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(n, target / dstride));
+    const uint64_t dig_bytes = want_hash ? chunk * (k + m) * 32 : 0;
+    if ((st = ctx->ensure_pipeline((size_t)(chunk * dstride + dig_bytes)))) return st;
+    const size_t dpitch_data = (shard_pitch == dpitch) ? (size_t)(k * dpitch) : 0;
+    for (uint64_t s0 = 0, it = 0; s0 < n; s0 += chunk, ++it) {
+        const int b = (int)(it & 1);
+        hipStream_t s = ctx->pipe_stream[b];
+        const uint64_t cnt = std::min<uint64_t>(chunk, n - s0);
+        uint8_t* hbase = h_stripes + s0 * stripe_stride;
+        uint8_t* d = ctx->d_stage[b];
+        if (dpitch_data) {  // data shards contiguous per stripe on both sides
+            st = hip_status(hipMemcpy2DAsync(d, dstride, hbase, stripe_stride, dpitch_data, cnt,
+                                             hipMemcpyHostToDevice, s));
+        } else {
+            for (int i = 0; i < k && !st; ++i)
+                st = hip_status(hipMemcpy2DAsync(d + i * dpitch, dstride, hbase + i * shard_pitch, stripe_stride,
+                                                 shard_len, cnt, hipMemcpyHostToDevice, s));
+        }
+        if (st) return st;
+        uint8_t* ddig = want_hash ? d + chunk * dstride : nullptr;
+        if ((st = rsg_encode_batch_dev(ctx, k, m, shard_len, cnt, d, dpitch, dstride, ddig, algo, s))) return st;
+        for (int p = 0; p < m && !st; ++p)
+            st = hip_status(hipMemcpy2DAsync(hbase + (k + p) * shard_pitch, stripe_stride, d + (k + p) * dpitch,
+                                             dstride, shard_len, cnt, hipMemcpyDeviceToHost, s));
+        if (!st && want_hash)
+            st = hip_status(hipMemcpyAsync(h_digests + s0 * (k + m) * 32, ddig, cnt * (k + m) * 32,
+                                           hipMemcpyDeviceToHost, s));
+        if (st) return st;
+    }
+    for (int i = 0; i < 2; ++i)
+        if ((st = hip_status(hipStreamSynchronize(ctx->pipe_stream[i])))) return st;
+    return RSG_OK;
+}
 
 int rsg_matrix(int k, int m, uint8_t* out) {
     if (!out) return RSG_ERR_INVALID_ARG;

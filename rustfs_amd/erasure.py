@@ -281,6 +281,24 @@ class Erasure:
             stripes.data_ptr(), S, t * S, d, algo if d else _lib.RSG_HASH_NONE, _stream_of(stripes, stream)),
             "Reed-Solomon encode failed")
 
+    def encode_batch_host(self, stripes: np.ndarray, digests: Optional[np.ndarray] = None,
+                          algo: int = _lib.RSG_HASH_HIGHWAY256S) -> None:
+        """Host-memory batch (n, k+m, S) uint8, parity written in place; pipelined
+        H2D -> encode(+digests) -> D2H inside librsgpu (rsg_encode_batch_host)."""
+        if stripes.dtype != np.uint8 or stripes.ndim != 3 or not stripes.flags.c_contiguous:
+            raise TypeError("stripes must be a C-contiguous uint8 array (n, k+m, S)")
+        n, t, S = stripes.shape
+        if t != self.total_shard_count():
+            raise RsgError(_lib.RSG_ERR_INVALID_SHARD_COUNT, f"invalid shard count: got {t}")
+        d = None
+        if digests is not None:
+            if digests.shape != (n, t, 32) or digests.dtype != np.uint8 or not digests.flags.c_contiguous:
+                raise TypeError("digests must be a C-contiguous uint8 array (n, k+m, 32)")
+            d = digests.ctypes.data
+        check(_lib.load().rsg_encode_batch_host(
+            _lib.context(self._device).handle, self.data_shards, self.parity_shards, S, n, stripes.ctypes.data,
+            S, t * S, d, algo if d else _lib.RSG_HASH_NONE), "Reed-Solomon encode failed")
+
     def reconstruct_batch(self, stripes, present: Sequence[bool], mode: int = _lib.RSG_RECONSTRUCT_MISSING,
                           stream=None) -> None:
         n, t, S = _check_batch(stripes, self.total_shard_count())

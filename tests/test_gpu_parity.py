@@ -277,3 +277,25 @@ def test_full_size_roundtrip_property(gpu):
     e.reconstruct_batch(a, [i not in (1, 4, 8, 11) for i in range(k + m)], RSG_RECONSTRUCT_MISSING)
     torch.cuda.synchronize()
     assert torch.equal(a, ref)
+
+
+@pytest.mark.parametrize("k,m,S,n,hashed", [(8, 4, 131072, 70, True), (2, 2, 4096, 9, False), (6, 3, 3001, 5, True),
+                                            (16, 4, 65536, 3, True)])
+def test_host_batch_pipeline_matches_oracle(gpu, oracle, k, m, S, n, hashed):
+    """rsg_encode_batch_host: pipelined H2D -> encode(+digests) -> D2H, host buffers."""
+    import torch
+    from rustfs_amd import Erasure
+    rng = np.random.default_rng(S + n)
+    st = torch.zeros((n, k + m, S), dtype=torch.uint8).pin_memory().numpy()
+    st[:, :k] = rng.integers(0, 256, (n, k, S), dtype=np.uint8)
+    st[:, k:] = 0x77
+    dig = np.zeros((n, k + m, 32), dtype=np.uint8) if hashed else None
+    Erasure(k, m, k * S).encode_batch_host(st, dig)
+    for s in (0, n // 2, n - 1):
+        ref = st[s].copy()
+        ref[k:] = 0
+        oracle.encode(k, m, ref)
+        assert (ref == st[s]).all(), s
+        if hashed:
+            for i in range(k + m):
+                assert dig[s, i].tobytes() == oracle.hh256s(ref[i]), (s, i)
