@@ -23,7 +23,9 @@ struct GfApplyParams {
     uint64_t out_stripe_stride;  // bytes between output stripes
     uint64_t in_off[kMaxC];      // byte offset of input c inside a stripe
     uint64_t out_off[kMaxR];     // byte offset of output r inside a stripe
-    uint32_t tab[kMaxR][kMaxC][5];  // v_perm tables per coefficient (see rs_kernels.hip)
+    // v_perm tables per coefficient (rs_kernels.hip): [0..4] 3/3/2-bit split,
+    // [5],[6] the extra 4-entry tables of the 2/2/2/2-bit split ([0], [4] shared)
+    uint32_t tab[kMaxR][kMaxC][8];
     uint8_t* ok_flags;           // GF_MODE_COMPARE target, one byte per stripe
     uint32_t C, R, mode;
     uint32_t units;              // 16-byte units per shard (vector path)

@@ -40,53 +40,72 @@ __device__ __forceinline__ uint32_t gf_mul_word(const uint32_t* t, uint32_t s0, 
 // SIMD).  A per-thread unit loop pushed it to 130 VGPRs (3 waves per SIMD) and
 // ran ~8 % slower; 2 or 4 units with all loads issued first ran 12-60 % slower
 // (tools/kbench/encode_variants.hip).
+//
+// acc[r] ^= sum over inputs c in [C0, C0+CN) of tab[r][c] * x[c - C0]  (4 words)
+template <int C0, int CN, int R>
+__device__ __forceinline__ void gf_accumulate(const GfApplyParams& p, const uint4* x, uint32_t (&acc)[R][4]) {
+#pragma unroll
+    for (int i = 0; i < CN; ++i) {
+        const int c = C0 + i;
+        const uint32_t w[4] = {x[i].x, x[i].y, x[i].z, x[i].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t s0 = w[q] & 0x07070707u;
+            const uint32_t s1 = (w[q] >> 3) & 0x07070707u;
+            const uint32_t s2 = (w[q] >> 6) & 0x03030303u;
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r][q] ^= gf_mul_word(p.tab[r][c], s0, s1, s2);
+        }
+    }
+}
+
+// 16-byte accesses with no alignment promise: gfx950 runs HSA code in
+// unaligned-access mode, so these stay single global_load/store_dwordx4 and let
+// shards of any length (S = ceil(1 MiB / 6) = 174763, ceil(1 MiB / 12) = 87382)
+// take the vector path; only the S % 16 tail goes to the byte kernel.
+__device__ __forceinline__ uint4 ld16(const uint8_t* p) {
+    uint4 v;
+    __builtin_memcpy(&v, p, 16);
+    return v;
+}
+__device__ __forceinline__ void st16(uint8_t* p, const uint4& v) { __builtin_memcpy(p, &v, 16); }
+
+template <int R>
+__device__ __forceinline__ void gf_store(const GfApplyParams& p, uint8_t* obase, uint64_t off,
+                                         const uint32_t (&acc)[R][4], uint32_t stripe) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        uint8_t* dst = obase + p.out_off[r] + off;
+        const uint4 v = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+        if (p.mode == GF_MODE_STORE) {
+            st16(dst, v);
+        } else if (p.mode == GF_MODE_XOR) {
+            const uint4 o = ld16(dst);
+            st16(dst, make_uint4(o.x ^ v.x, o.y ^ v.y, o.z ^ v.z, o.w ^ v.w));
+        } else {  // GF_MODE_COMPARE: clear the stripe's ok flag on mismatch
+            const uint4 o = ld16(dst);
+            if ((o.x ^ v.x) | (o.y ^ v.y) | (o.z ^ v.z) | (o.w ^ v.w)) p.ok_flags[stripe] = 0;
+        }
+    }
+}
+
 template <int C, int R>
 __global__ __launch_bounds__(256) void k_gf_apply_vec(const GfApplyParams p) {
     const uint32_t stripe = blockIdx.x / p.chunks_per_stripe;
     const uint32_t chunk = blockIdx.x - stripe * p.chunks_per_stripe;
     const uint8_t* sbase = p.base + (uint64_t)stripe * p.stripe_stride;
     uint8_t* obase = p.out_base + (uint64_t)stripe * p.out_stripe_stride;
-    {
-        const uint32_t u = chunk * 256u + threadIdx.x;
-        if (u >= p.units) return;
-        const uint64_t off = (uint64_t)u * 16u;
-
-        uint4 x[C];
+    const uint32_t u = chunk * 256u + threadIdx.x;
+    if (u >= p.units) return;
+    const uint64_t off = (uint64_t)u * 16u;
+    uint4 x[C];
 #pragma unroll
-        for (int c = 0; c < C; ++c) x[c] = *(const uint4*)(sbase + p.in_off[c] + off);
-
-        uint32_t acc[R][4];
+    for (int c = 0; c < C; ++c) x[c] = ld16(sbase + p.in_off[c] + off);
+    uint32_t acc[R][4];
 #pragma unroll
-        for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
-
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-            const uint32_t w[4] = {x[c].x, x[c].y, x[c].z, x[c].w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t s0 = w[q] & 0x07070707u;
-                const uint32_t s1 = (w[q] >> 3) & 0x07070707u;
-                const uint32_t s2 = (w[q] >> 6) & 0x03030303u;
-#pragma unroll
-                for (int r = 0; r < R; ++r) acc[r][q] ^= gf_mul_word(p.tab[r][c], s0, s1, s2);
-            }
-        }
-
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            uint4* dst = (uint4*)(obase + p.out_off[r] + off);
-            uint4 v = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
-            if (p.mode == GF_MODE_STORE) {
-                *dst = v;
-            } else if (p.mode == GF_MODE_XOR) {
-                uint4 o = *dst;
-                *dst = make_uint4(o.x ^ v.x, o.y ^ v.y, o.z ^ v.z, o.w ^ v.w);
-            } else {  // GF_MODE_COMPARE: clear the stripe's ok flag on mismatch
-                uint4 o = *dst;
-                if ((o.x ^ v.x) | (o.y ^ v.y) | (o.z ^ v.z) | (o.w ^ v.w)) p.ok_flags[stripe] = 0;
-            }
-        }
-    }
+    for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
+    gf_accumulate<0, C, R>(p, x, acc);
+    gf_store<R>(p, obase, off, acc, stripe);
 }
 
 // ---------------------------------------------------------------------------

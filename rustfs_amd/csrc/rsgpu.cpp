@@ -111,7 +111,9 @@ bool build_matrix(int k, int m, Mat& out) {
 }
 
 // v_perm_b32 tables of coefficient c (see rs_kernels.hip header).
-void coef_tables(uint8_t c, uint32_t t[5]) {
+// t[0..4]: the 3/3/2-bit split (T0 lo/hi, T1 lo/hi, T2);
+// t[4..7]: the 2/2/2/2-bit split (Q3 = T2, Q1, Q2, Q0 = t[0]); t[7] unused.
+void coef_tables(uint8_t c, uint32_t t[8]) {
     const Gf& g = gf();
     auto pack = [&](int shift, int first) {
         uint32_t v = 0;
@@ -123,6 +125,9 @@ void coef_tables(uint8_t c, uint32_t t[5]) {
     t[2] = pack(3, 0);
     t[3] = pack(3, 4);
     t[4] = pack(6, 0);
+    t[5] = pack(2, 0);
+    t[6] = pack(4, 0);
+    t[7] = 0;
 }
 
 // --------------------------------------------------------------------------
@@ -296,11 +301,9 @@ int apply_rows(const RowSet& rs, const uint8_t* base, uint8_t* out_base, uint64_
                uint64_t len, uint64_t n, uint32_t mode, uint8_t* ok_flags, hipStream_t stream) {
     if (rs.R == 0 || n == 0 || len == 0) return RSG_OK;
     if (mode == rsg::GF_MODE_COMPARE && rs.C > rsg::kMaxC) return RSG_ERR_UNSUPPORTED;
-    bool aligned = ((uintptr_t)base % 16 == 0) && ((uintptr_t)out_base % 16 == 0) && (stride % 16 == 0) &&
-                   (out_stride % 16 == 0);
-    for (uint64_t o : rs.in_off) aligned = aligned && (o % 16 == 0);
-    for (uint64_t o : rs.out_off) aligned = aligned && (o % 16 == 0);
-    const uint64_t units = aligned ? len / 16 : 0;
+    // The vector kernel's 16-byte accesses need no alignment (ld16/st16 in
+    // rs_kernels.hip); only the len % 16 tail of each shard takes the byte path.
+    const uint64_t units = len / 16;
     if (units > 0xffffffffull) return RSG_ERR_UNSUPPORTED;
 
     for (int r0 = 0; r0 < rs.R; r0 += rsg::kMaxR) {
