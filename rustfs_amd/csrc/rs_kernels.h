@@ -7,7 +7,7 @@
 namespace rsg {
 
 constexpr int kMaxC = 16;  // inputs per launch (more are chained with GF_MODE_XOR)
-constexpr int kMaxR = 4;   // outputs per launch (more are split over launches)
+constexpr int kMaxR = 8;   // outputs per launch (more are split over launches)
 
 enum GfMode : uint32_t {
     GF_MODE_STORE = 0,    // out = M * in
@@ -23,9 +23,7 @@ struct GfApplyParams {
     uint64_t out_stripe_stride;  // bytes between output stripes
     uint64_t in_off[kMaxC];      // byte offset of input c inside a stripe
     uint64_t out_off[kMaxR];     // byte offset of output r inside a stripe
-    // v_perm tables per coefficient (rs_kernels.hip): [0..4] 3/3/2-bit split,
-    // [5],[6] the extra 4-entry tables of the 2/2/2/2-bit split ([0], [4] shared)
-    uint32_t tab[kMaxR][kMaxC][8];
+    uint32_t tab[kMaxR][kMaxC][5];  // v_perm tables per coefficient (rs_kernels.hip)
     uint8_t* ok_flags;           // GF_MODE_COMPARE target, one byte per stripe
     uint32_t C, R, mode;
     uint32_t units;              // 16-byte units per shard (vector path)

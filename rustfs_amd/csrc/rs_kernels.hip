@@ -20,6 +20,7 @@
 // the HBM op budget).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "rs_kernels.h"
 
@@ -105,6 +106,57 @@ __global__ __launch_bounds__(256) void k_gf_apply_vec(const GfApplyParams p) {
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
     gf_accumulate<0, C, R>(p, x, acc);
+    gf_store<R>(p, obase, off, acc, stripe);
+}
+
+// Rolled over the inputs in groups of G=4 (any C <= 16, R <= 8): the next
+// group's loads are issued before the current group's arithmetic, and the
+// tables are indexed by the scalar loop counter.  The unrolled kernel above
+// keeps all C inputs and, for C > 8, parks all C*R coefficient tables in
+// VGPRs (~250 VGPRs at C=16, R=4: 2 waves per SIMD); rolled, RS(16,4) needs
+// 95 VGPRs and ran at 68 % of HBM peak against 49 % unrolled
+// (tools/kbench/geom_variants.hip).  For C <= 8, R <= 4 the unrolled kernel is
+// 1-2 % faster and stays the default there.
+template <int R>
+__global__ __launch_bounds__(256) void k_gf_apply_loop(const GfApplyParams p) {
+    constexpr int G = 4;
+    const uint32_t stripe = blockIdx.x / p.chunks_per_stripe;
+    const uint32_t chunk = blockIdx.x - stripe * p.chunks_per_stripe;
+    const uint8_t* sbase = p.base + (uint64_t)stripe * p.stripe_stride;
+    uint8_t* obase = p.out_base + (uint64_t)stripe * p.out_stripe_stride;
+    const uint32_t u = chunk * 256u + threadIdx.x;
+    if (u >= p.units) return;
+    const uint64_t off = (uint64_t)u * 16u;
+    const uint32_t C = p.C;
+    uint32_t acc[R][4];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
+    uint4 x[G], y[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+        if ((uint32_t)g < C) x[g] = ld16(sbase + p.in_off[g] + off);
+#pragma unroll 1
+    for (uint32_t c0 = 0; c0 < C; c0 += G) {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+            if (c0 + G + g < C) y[g] = ld16(sbase + p.in_off[c0 + G + g] + off);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const uint32_t c = c0 + g;
+            if (c >= C) break;  // wave-uniform
+            const uint32_t w[4] = {x[g].x, x[g].y, x[g].z, x[g].w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t s0 = w[q] & 0x07070707u;
+                const uint32_t s1 = (w[q] >> 3) & 0x07070707u;
+                const uint32_t s2 = (w[q] >> 6) & 0x03030303u;
+#pragma unroll
+                for (int r = 0; r < R; ++r) acc[r][q] ^= gf_mul_word(p.tab[r][c], s0, s1, s2);
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) x[g] = y[g];
+    }
     gf_store<R>(p, obase, off, acc, stripe);
 }
 
@@ -436,24 +488,36 @@ static GfKernel pick_vec_r(int R) {
     return nullptr;
 }
 
+// Unrolled kernel for C <= 8 inputs and R <= 4 outputs, the rolled one above
+// (k_gf_apply_loop); RSG_ROLLED=1 forces the rolled kernel for A/B runs.
 static GfKernel pick_vec(int C, int R) {
-    switch (C) {
-        case 1: return pick_vec_r<1>(R);
-        case 2: return pick_vec_r<2>(R);
-        case 3: return pick_vec_r<3>(R);
-        case 4: return pick_vec_r<4>(R);
-        case 5: return pick_vec_r<5>(R);
-        case 6: return pick_vec_r<6>(R);
-        case 7: return pick_vec_r<7>(R);
-        case 8: return pick_vec_r<8>(R);
-        case 9: return pick_vec_r<9>(R);
-        case 10: return pick_vec_r<10>(R);
-        case 11: return pick_vec_r<11>(R);
-        case 12: return pick_vec_r<12>(R);
-        case 13: return pick_vec_r<13>(R);
-        case 14: return pick_vec_r<14>(R);
-        case 15: return pick_vec_r<15>(R);
-        case 16: return pick_vec_r<16>(R);
+    static const bool force_rolled = [] {
+        const char* s = std::getenv("RSG_ROLLED");
+        return s && s[0] == '1';
+    }();
+    if (C <= 8 && R <= 4 && !force_rolled) {
+        switch (C) {
+            case 1: return pick_vec_r<1>(R);
+            case 2: return pick_vec_r<2>(R);
+            case 3: return pick_vec_r<3>(R);
+            case 4: return pick_vec_r<4>(R);
+            case 5: return pick_vec_r<5>(R);
+            case 6: return pick_vec_r<6>(R);
+            case 7: return pick_vec_r<7>(R);
+            case 8: return pick_vec_r<8>(R);
+        }
+        return nullptr;
+    }
+    if (C < 1 || C > kMaxC) return nullptr;
+    switch (R) {
+        case 1: return k_gf_apply_loop<1>;
+        case 2: return k_gf_apply_loop<2>;
+        case 3: return k_gf_apply_loop<3>;
+        case 4: return k_gf_apply_loop<4>;
+        case 5: return k_gf_apply_loop<5>;
+        case 6: return k_gf_apply_loop<6>;
+        case 7: return k_gf_apply_loop<7>;
+        case 8: return k_gf_apply_loop<8>;
     }
     return nullptr;
 }
@@ -464,6 +528,10 @@ static GfKernel pick_byte(int R) {
         case 2: return k_gf_apply_byte<2>;
         case 3: return k_gf_apply_byte<3>;
         case 4: return k_gf_apply_byte<4>;
+        case 5: return k_gf_apply_byte<5>;
+        case 6: return k_gf_apply_byte<6>;
+        case 7: return k_gf_apply_byte<7>;
+        case 8: return k_gf_apply_byte<8>;
     }
     return nullptr;
 }
@@ -533,7 +601,7 @@ static FusedKernel pick_fused(int C, int R) {
 }
 
 bool fused_supported(int C, int R, uint64_t shard_len) {
-    return C >= 1 && C <= kMaxC && R >= 1 && R <= kMaxR && shard_len >= kFusedChunk &&
+    return C >= 1 && C <= kMaxC && R >= 1 && R <= 4 && shard_len >= kFusedChunk &&
            shard_len % kFusedChunk == 0 && shard_len / kFusedChunk <= 0xffffffffull;
 }
 

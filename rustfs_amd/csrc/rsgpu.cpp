@@ -110,10 +110,9 @@ bool build_matrix(int k, int m, Mat& out) {
     return true;
 }
 
-// v_perm_b32 tables of coefficient c (see rs_kernels.hip header).
-// t[0..4]: the 3/3/2-bit split (T0 lo/hi, T1 lo/hi, T2);
-// t[4..7]: the 2/2/2/2-bit split (Q3 = T2, Q1, Q2, Q0 = t[0]); t[7] unused.
-void coef_tables(uint8_t c, uint32_t t[8]) {
+// v_perm_b32 tables of coefficient c: T0 lo/hi, T1 lo/hi, T2 of the 3/3/2-bit
+// split (rs_kernels.hip header).
+void coef_tables(uint8_t c, uint32_t t[5]) {
     const Gf& g = gf();
     auto pack = [&](int shift, int first) {
         uint32_t v = 0;
@@ -125,9 +124,6 @@ void coef_tables(uint8_t c, uint32_t t[8]) {
     t[2] = pack(3, 0);
     t[3] = pack(3, 4);
     t[4] = pack(6, 0);
-    t[5] = pack(2, 0);
-    t[6] = pack(4, 0);
-    t[7] = 0;
 }
 
 // --------------------------------------------------------------------------

@@ -188,7 +188,8 @@ def _device_batch(torch, n, k, m, S, seed):
 
 
 @pytest.mark.parametrize("k,m,S,n", [(8, 4, 4096, 7), (2, 2, 1000, 5), (16, 4, 2048, 3), (6, 3, 3001, 4),
-                                     (20, 5, 512, 2), (8, 4, 131072, 3)])
+                                     (20, 5, 512, 2), (8, 4, 131072, 3), (6, 6, 4096, 3), (10, 6, 1000, 2),
+                                     (12, 4, 87382, 2), (6, 2, 174763, 2), (9, 7, 2064, 2), (4, 8, 512, 3)])
 def test_batch_encode_and_digests_match_oracle(gpu, oracle, k, m, S, n):
     import torch
     from rustfs_amd import Erasure
@@ -224,6 +225,25 @@ def test_batch_derived_fixtures(gpu, derived_vectors):
         h = st.cpu().numpy()[0]
         assert hashlib.sha256(h[k:].tobytes()).hexdigest() == v["parity_sha256"]
         assert [bytes(d).hex() for d in dig.cpu().numpy()[0]] == v["hh256s"]
+
+
+@pytest.mark.parametrize("k,m,missing", [(10, 6, (0, 1, 2, 3, 4, 5)), (10, 6, (3, 7, 9, 10, 12)),
+                                         (12, 4, (0, 5, 11, 13)), (6, 6, (0, 1, 2, 6, 7, 8))])
+def test_batch_reconstruct_wide(gpu, k, m, missing):
+    """More than 4 rebuilt shards in one launch (R up to 8) and unaligned S."""
+    import torch
+    from rustfs_amd import Erasure, RSG_RECONSTRUCT_MISSING
+    S = -(-(1 << 20) // k)
+    n = 5
+    e = Erasure(k, m, 1 << 20)
+    st = _device_batch(torch, n, k, m, S, seed=k * m)
+    e.encode_batch(st)
+    ref = st.clone()
+    for i in missing:
+        st[:, i] = 0xC3
+    e.reconstruct_batch(st, [i not in missing for i in range(k + m)], RSG_RECONSTRUCT_MISSING)
+    torch.cuda.synchronize()
+    assert torch.equal(st, ref)
 
 
 @pytest.mark.parametrize("missing", [(0,), (0, 3), (0, 3, 5), (0, 3, 5, 7), (1, 9), (8, 9, 10, 11), (2, 11)])
