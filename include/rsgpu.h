@@ -139,6 +139,23 @@ int rsg_verify_batch_dev(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t n,
 int rsg_hash_batch_dev(rsg_ctx *ctx, int algo, const uint8_t *d_data, size_t len, size_t stride,
                        size_t n, uint8_t *d_out, void *stream);
 
+/* GET-side engine, batched (RustfsCodecDecodeEngine::reconstruct_into,
+ * bridge.rs:274-307, with BitrotReader's verify-before-use, bitrot.rs:227-247).
+ * Shard i of n stripes is resident on the device in BitrotWriter layout:
+ * record s at d_files[i] + s*(32+shard_len) = [32-byte digest][shard_len bytes]
+ * (d_files[i] == NULL: shard unavailable).  Every available record is hashed
+ * and compared with its digest; a mismatching record counts as missing for
+ * that stripe only.  The k data shards of stripe s are written contiguously to
+ * d_out + s*k*shard_len (present ones copied, missing ones rebuilt from the
+ * first k valid shards).  With verify_surplus, stripes that rebuilt data while
+ * holding more than k valid shards re-derive the surplus parity and compare
+ * (decode_data_with_reconstruction_verification, erasure.rs:935-973).
+ * h_status[s] (host array): RSG_OK, RSG_ERR_TOO_FEW_SHARDS or
+ * RSG_ERR_INCONSISTENT_SOURCES.  Synchronous. */
+int rsg_decode_records_dev(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t n,
+                           const uint8_t *const *d_files, int algo, int verify_surplus,
+                           uint8_t *d_out, int *h_status, void *stream);
+
 /* Block until all work queued on `stream` (NULL = the null stream) is done. */
 int rsg_sync(rsg_ctx *ctx, void *stream);
 

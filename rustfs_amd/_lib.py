@@ -51,6 +51,7 @@ EXPORTED = (
     "rsg_matrix", "rsg_check_geometry", "rsg_encode", "rsg_reconstruct", "rsg_verify",
     "rsg_hash", "rsg_encode_batch_dev", "rsg_reconstruct_batch_dev", "rsg_verify_batch_dev",
     "rsg_hash_batch_dev", "rsg_sync", "rsg_encode_batch_host", "rsg_pin", "rsg_unpin",
+    "rsg_decode_records_dev",
 )
 
 
@@ -101,6 +102,7 @@ def load():
         L.rsg_hash_batch_dev.argtypes = [P, I, P, S, S, S, P, P]
         L.rsg_sync.argtypes = [P, P]
         L.rsg_encode_batch_host.argtypes = [P, I, I, S, S, P, S, S, P, I]
+        L.rsg_decode_records_dev.argtypes = [P, I, I, S, S, P, I, I, P, P, P]
         L.rsg_pin.argtypes = [P, S]
         L.rsg_unpin.argtypes = [P]
         _lib = L

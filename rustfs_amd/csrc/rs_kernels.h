@@ -39,8 +39,13 @@ struct HashParams {
     uint64_t shard_pitch;    // bytes between messages of one stripe
     uint64_t stripe_stride;  // bytes between stripes
     uint64_t key[4];
-    uint8_t* out;            // n x 32 digests
+    uint8_t* out;            // n x 32 digests (may be null in verify mode)
     uint32_t aligned16;      // every message 16-B aligned: vector loads
+    // verify mode (expect != null): compare with the stored digest of message j
+    // at expect + j*expect_stride and clear flags[j] on mismatch
+    const uint8_t* expect;
+    uint64_t expect_stride;
+    uint8_t* flags;
 };
 
 hipError_t launch_gf_apply_vec(GfApplyParams p, uint64_t n_stripes, hipStream_t stream);

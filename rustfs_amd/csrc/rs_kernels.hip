@@ -291,7 +291,8 @@ __device__ __forceinline__ void hhq_remainder(HHQuad& s, const uint8_t* tail, ui
 }
 
 // 10 x PermuteAndUpdate, ModularReduction; lane q writes digest bytes [8q, 8q+8).
-__device__ __forceinline__ void hhq_finish(HHQuad& s, uint8_t* out, uint32_t q) {
+// Finalize; returns lane q's digest word (bytes [8q, 8q+8) little-endian).
+__device__ __forceinline__ uint64_t hhq_digest(HHQuad& s, uint32_t q) {
 #pragma unroll 1
     for (int it = 0; it < 10; ++it) {
         const uint32_t lo = quad_swap_halves((uint32_t)s.v0), hi = quad_swap_halves((uint32_t)(s.v0 >> 32));
@@ -307,6 +308,11 @@ __device__ __forceinline__ void hhq_finish(HHQuad& s, uint8_t* out, uint32_t q) 
     } else {      // h[even] = a0 ^ (a2 << 1) ^ (a2 << 2), a2 = own v1+mul1
         h = a_v0 ^ (a_v1 << 1) ^ (a_v1 << 2);
     }
+    return h;
+}
+
+__device__ __forceinline__ void hhq_finish(HHQuad& s, uint8_t* out, uint32_t q) {
+    const uint64_t h = hhq_digest(s, q);
 #pragma unroll
     for (int b = 0; b < 8; ++b) out[8 * q + b] = (uint8_t)(h >> (8 * b));  // any alignment
 }
@@ -342,7 +348,12 @@ __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
     }
     const uint32_t rem = (uint32_t)(p.len & 31);
     if (rem) hhq_remainder(s, msg + packets * 32, rem, q);
-    hhq_finish(s, p.out + j * 32u, q);
+    if (p.expect) {  // verify before use (split_and_verify, bitrot.rs:227-247)
+        const uint64_t h = hhq_digest(s, q);
+        if (h != ld64_any(p.expect + j * p.expect_stride + 8 * q)) p.flags[j] = 0;
+    } else {
+        hhq_finish(s, p.out + j * 32u, q);
+    }
 }
 
 // ---------------------------------------------------------------------------

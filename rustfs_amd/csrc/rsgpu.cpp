@@ -656,6 +656,133 @@ int rsg_hash_batch_dev(rsg_ctx* ctx, int algo, const uint8_t* d_data, size_t len
     return hash_messages(algo, d_data, len, n, 1, 0, stride, d_out, pick_stream(ctx, stream));
 }
 
+// GET-side engine: verify every [digest][block] record, then copy or rebuild
+// the data shards of each stripe, runs of stripes with one erasure pattern at
+// a time (normally one run: whole shard files present or absent).
+int rsg_decode_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n, const uint8_t* const* d_files,
+                           int algo, int verify_surplus, uint8_t* d_out, int* h_status, void* stream) {
+    int st = enter(ctx);
+    if (st) return st;
+    if ((st = check_geometry(k, m))) return st;
+    if (!d_files || (n && (!d_out || !h_status))) return RSG_ERR_INVALID_ARG;
+    const uint64_t* key = hash_key(algo);
+    if (!key) return RSG_ERR_INVALID_ARG;
+    if (n == 0 || shard_len == 0) {
+        for (size_t s = 0; s < n; ++s) h_status[s] = RSG_OK;
+        return RSG_OK;
+    }
+    const int t = k + m;
+    const uint64_t rec = 32 + shard_len;  // BitrotWriter record: [hash][block]
+    hipStream_t s = pick_stream(ctx, stream);
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if ((st = ctx->ensure_scratch((size_t)(t + 1) * n))) return st;
+    uint8_t* d_flags = ctx->d_scratch;  // [shard][stripe] 1 = record verified
+    uint8_t* d_ok = d_flags + (size_t)t * n;  // surplus-parity verdict per stripe
+    if ((st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
+    // 1. verify every available record
+    for (int i = 0; i < t; ++i) {
+        if ((st = hip_status(hipMemsetAsync(d_flags + (size_t)i * n, d_files[i] ? 1 : 0, n, s)))) return st;
+        if (!d_files[i]) continue;
+        rsg::HashParams h;
+        std::memset(&h, 0, sizeof(h));
+        h.data = d_files[i] + 32;
+        h.len = shard_len;
+        h.n = n;
+        h.shards = 1;
+        h.stripe_stride = rec;
+        std::memcpy(h.key, key, sizeof(h.key));
+        h.aligned16 = false;
+        h.expect = d_files[i];
+        h.expect_stride = rec;
+        h.flags = d_flags + (size_t)i * n;
+        if ((st = hip_status(rsg::launch_hh256(h, s)))) return st;
+    }
+    std::vector<uint8_t> flags((size_t)t * n);
+    if ((st = hip_status(hipMemcpyAsync(flags.data(), d_flags, flags.size(), hipMemcpyDeviceToHost, s)))) return st;
+    if ((st = hip_status(hipStreamSynchronize(s)))) return st;
+    auto cd = m > 0 ? get_codec(k, m) : nullptr;
+    if (m > 0 && !cd) return RSG_ERR_INVALID_ARG;
+    // 2. runs of stripes with the same verified-shard pattern
+    std::vector<uint8_t> present(t);
+    bool any_verify = false;
+    for (size_t s0 = 0; s0 < n;) {
+        for (int i = 0; i < t; ++i) present[i] = flags[(size_t)i * n + s0];
+        size_t s1 = s0 + 1;
+        for (; s1 < n; ++s1) {
+            bool same = true;
+            for (int i = 0; i < t && same; ++i) same = flags[(size_t)i * n + s1] == present[i];
+            if (!same) break;
+        }
+        const uint64_t cnt = s1 - s0;
+        int valid = 0, missing_data = 0;
+        for (int i = 0; i < t; ++i) valid += present[i];
+        for (int i = 0; i < k; ++i) missing_data += present[i] ? 0 : 1;
+        int run_status = RSG_OK;
+        if (valid < k) {
+            run_status = RSG_ERR_TOO_FEW_SHARDS;
+        } else {
+            uint8_t* out = d_out + s0 * (uint64_t)k * shard_len;
+            for (int i = 0; i < k; ++i)  // present data shards: strided copy out of the records
+                if (present[i] && (st = hip_status(hipMemcpy2DAsync(out + i * shard_len, (size_t)k * shard_len,
+                                                                    d_files[i] + s0 * rec + 32, rec, shard_len, cnt,
+                                                                    hipMemcpyDeviceToDevice, s))))
+                    return st;
+            if (missing_data) {
+                auto plan = cd->plan(present.data());
+                if (!plan) return RSG_ERR_TOO_FEW_SHARDS;
+                // survivors read in place from the records; base = first survivor
+                const uint8_t* base = d_files[plan->survivors[0]] + s0 * rec + 32;
+                RowSet rs;
+                rs.C = k;
+                for (int sv : plan->survivors)
+                    rs.in_off.push_back((uint64_t)(uintptr_t)(d_files[sv] + s0 * rec + 32) - (uint64_t)(uintptr_t)base);
+                for (int i = 0; i < k; ++i) {
+                    if (present[i]) continue;
+                    rs.coef.resize((size_t)(rs.R + 1) * k);
+                    plan_row(*cd, *plan, i, &rs.coef[(size_t)rs.R * k]);
+                    rs.out_off.push_back((uint64_t)i * shard_len);
+                    ++rs.R;
+                }
+                if ((st = apply_rows(rs, base, out, rec, (uint64_t)k * shard_len, shard_len, cnt,
+                                     rsg::GF_MODE_STORE, nullptr, s)))
+                    return st;
+                // 3. surplus parity must agree with the rebuilt data (erasure.rs:935-973)
+                if (verify_surplus && valid > k) {
+                    RowSet vs;
+                    vs.C = k;
+                    vs.in_off = rs.in_off;
+                    for (int p = k; p < t; ++p) {
+                        if (!present[p]) continue;
+                        if (std::find(plan->survivors.begin(), plan->survivors.end(), p) != plan->survivors.end())
+                            continue;  // a survivor re-derives to itself
+                        vs.coef.resize((size_t)(vs.R + 1) * k);
+                        plan_row(*cd, *plan, p, &vs.coef[(size_t)vs.R * k]);
+                        vs.out_off.push_back((uint64_t)(uintptr_t)(d_files[p] + s0 * rec + 32) -
+                                             (uint64_t)(uintptr_t)base);
+                        ++vs.R;
+                    }
+                    if (vs.R) {
+                        if ((st = apply_rows(vs, base, const_cast<uint8_t*>(base), rec, rec, shard_len, cnt,
+                                             rsg::GF_MODE_COMPARE, d_ok + s0, s)))
+                            return st;
+                        any_verify = true;
+                    }
+                }
+            }
+        }
+        for (size_t x = s0; x < s1; ++x) h_status[x] = run_status;
+        s0 = s1;
+    }
+    if (any_verify) {
+        std::vector<uint8_t> ok(n, 1);
+        if ((st = hip_status(hipMemcpyAsync(ok.data(), d_ok, n, hipMemcpyDeviceToHost, s)))) return st;
+        if ((st = hip_status(hipStreamSynchronize(s)))) return st;
+        for (size_t x = 0; x < n; ++x)
+            if (h_status[x] == RSG_OK && !ok[x]) h_status[x] = RSG_ERR_INCONSISTENT_SOURCES;
+    }
+    return hip_status(hipStreamSynchronize(s));
+}
+
 // ---- host-buffer API ----
 
 int rsg_encode(rsg_ctx* ctx, int k, int m, size_t shard_len, uint8_t* const* shards) {

@@ -299,6 +299,34 @@ class Erasure:
             _lib.context(self._device).handle, self.data_shards, self.parity_shards, S, n, stripes.ctypes.data,
             S, t * S, d, algo if d else _lib.RSG_HASH_NONE), "Reed-Solomon encode failed")
 
+    def decode_records_batch(self, files: Sequence, shard_len: int, n: int, verify_surplus: bool = True,
+                             algo: int = _lib.RSG_HASH_HIGHWAY256S, out=None, stream=None):
+        """GET engine (rsg_decode_records_dev): `files[i]` is a cuda uint8 tensor
+        holding shard i's n BitrotWriter records ([32-byte digest][shard_len]) or
+        None.  Returns (data (n, k*shard_len) tensor, per-stripe status list)."""
+        import torch
+        t = self.total_shard_count()
+        if len(files) != t:
+            raise RsgError(_lib.RSG_ERR_INVALID_SHARD_COUNT, f"invalid shard count: got {len(files)}")
+        rec = 32 + shard_len
+        dev = None
+        for f in files:
+            if f is not None:
+                if f.dtype != torch.uint8 or not f.is_cuda or not f.is_contiguous() or f.numel() < n * rec:
+                    raise TypeError("each file must be a contiguous cuda uint8 tensor of n records")
+                dev = f.device
+        if dev is None:
+            raise RsgError(_lib.RSG_ERR_TOO_FEW_SHARDS, "no shard available")
+        if out is None:
+            out = torch.empty((n, self.data_shards * shard_len), dtype=torch.uint8, device=dev)
+        ptrs = (ctypes.c_void_p * t)(*[f.data_ptr() if f is not None else None for f in files])
+        status = (ctypes.c_int * max(n, 1))()
+        s = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+        check(_lib.load().rsg_decode_records_dev(
+            _lib.context(dev.index or 0).handle, self.data_shards, self.parity_shards, shard_len, n, ptrs, algo,
+            1 if verify_surplus else 0, out.data_ptr(), status, s), "RustFS codec reconstruct failed")
+        return out, [int(status[i]) for i in range(n)]
+
     def reconstruct_batch(self, stripes, present: Sequence[bool], mode: int = _lib.RSG_RECONSTRUCT_MISSING,
                           stream=None) -> None:
         n, t, S = _check_batch(stripes, self.total_shard_count())
