@@ -380,7 +380,9 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("" ::: "memory");
 }
 
-template <int C, int R>
+// ABLATE (measurement builds only, tools/kbench/fused_variants.hip): bit 0
+// skips the GF arithmetic, bit 1 the hash updates; production uses 0.
+template <int C, int R, int ABLATE = 0>
 __global__ __launch_bounds__(128) void k_encode_hash_fused(const GfApplyParams p, const HashParams h) {
     // LDS: [C][R] coefficient tables (32 B each: T0 T0' T1 T1' | T2), then the
     // (C+R) chunk rows.  Tables are read from LDS (broadcast) at their use:
@@ -420,6 +422,11 @@ __global__ __launch_bounds__(128) void k_encode_hash_fused(const GfApplyParams p
             for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = 0u;
 #pragma unroll
             for (int c = 0; c < C; ++c) {
+                if constexpr (ABLATE & 1) {
+                    acc[c % R][0] ^= x[c].x;
+                    acc[c % R][1] ^= x[c].y;
+                    continue;
+                }
                 const uint32_t s0a = x[c].x & 0x07070707u, s0b = x[c].y & 0x07070707u;
                 const uint32_t s1a = (x[c].x >> 3) & 0x07070707u, s1b = (x[c].y >> 3) & 0x07070707u;
                 const uint32_t s2a = (x[c].x >> 6) & 0x03030303u, s2b = (x[c].y >> 6) & 0x03030303u;
@@ -469,8 +476,12 @@ __global__ __launch_bounds__(128) void k_encode_hash_fused(const GfApplyParams p
                     const uint8_t* row = rows + g * kFusedPitch + 8 * q;
 #pragma unroll 4
                     for (int t = 0; t < (int)(kFusedChunk / 32); ++t) {
-                        const uint2 v = *(const uint2*)(row + t * 32);
-                        hhq_update(st[r], (uint64_t)v.x | ((uint64_t)v.y << 32));
+                        const u32x2 v = *(const u32x2*)(row + t * 32);
+                        if constexpr (ABLATE & 2) {
+                            st[r].v0 ^= __builtin_bit_cast(uint64_t, v);
+                        } else {
+                            hhq_update(st[r], __builtin_bit_cast(uint64_t, v));
+                        }
                     }
                 }
             }

@@ -1,0 +1,64 @@
+// op_rates.hip — issue cost of the VALU ops the HighwayHash update uses, on
+// gfx950: 8 independent chains per lane, 8 waves per SIMD, reported as SIMD
+// cycles per wave-instruction (2.0 = full rate for a wave64 op on SIMD32).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s\n", hipGetErrorString(e_)); return 1; } } while (0)
+constexpr int ITERS = 4096;
+
+template <int OP>
+__global__ __launch_bounds__(256) void k(uint64_t* out, uint64_t seed) {
+    uint64_t a[8];
+    uint32_t b[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { a[i] = seed * (threadIdx.x + i + 1); b[i] = (uint32_t)(a[i] >> 7) | 1u; }
+    for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if constexpr (OP == 0) asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(a[i]) : "v"(a[(i + 1) & 7]));
+            if constexpr (OP == 1) asm volatile("v_mad_u64_u32 %0, vcc, %1, %1, %0" : "+v"(a[i]) : "v"(b[i]) : "vcc");
+            if constexpr (OP == 2) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(b[i]) : "v"(b[(i + 1) & 7]), "v"(0x05020C03u));
+            if constexpr (OP == 3) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(b[i]) : "v"(b[(i + 1) & 7]));
+            if constexpr (OP == 4) asm volatile("v_add_co_u32 %0, vcc, %0, %1\n\tv_addc_co_u32 %2, vcc, %2, %1, vcc" : "+v"(b[i]), "+v"(b[(i + 4) & 7]) ,"+v"(b[(i+2)&7]) : : "vcc");
+            if constexpr (OP == 5) asm volatile("v_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=v"(b[i]) : "v"(b[(i + 1) & 7]));
+            if constexpr (OP == 6) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(b[i]) : "v"(b[(i + 1) & 7]));
+            if constexpr (OP == 7) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(b[i]) : "v"(b[(i + 1) & 7]));
+        }
+    }
+    uint64_t r = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r ^= a[i] ^ b[i];
+    out[blockIdx.x * 256 + threadIdx.x] = r;
+}
+
+template <int OP>
+float run(uint64_t* d, int blocks) {
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    k<OP><<<blocks, 256>>>(d, 3);
+    hipEventRecord(a);
+    k<OP><<<blocks, 256>>>(d, 5);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    return ms;
+}
+
+int main() {
+    const int blocks = 256 * 8;  // 8 blocks of 4 waves per CU = 8 waves per SIMD
+    uint64_t* d;
+    CK(hipMalloc(&d, (size_t)blocks * 256 * 8));
+    const char* names[] = {"v_lshl_add_u64", "v_mad_u64_u32", "v_perm_b32", "v_xor_b32", "add_co+addc (2 ops)", "v_mov_b32_dpp", "v_mul_lo_u32", "v_mul_hi_u32"};
+    float ms[8] = {run<0>(d, blocks), run<1>(d, blocks), run<2>(d, blocks), run<3>(d, blocks), run<4>(d, blocks), run<5>(d, blocks), run<6>(d, blocks), run<7>(d, blocks)};
+    const double waves_per_simd = 8, clk = 2.1e9;
+    for (int i = 0; i < 8; ++i) {
+        const double ops = waves_per_simd * ITERS * 8;  // wave-ops per SIMD
+        printf("%-22s %.3f ms  ~%.2f SIMD cycles per wave-op (at %.1f GHz)\n", names[i], ms[i], ms[i] * 1e-3 * clk / ops,
+               clk / 1e9);
+    }
+    return 0;
+}
