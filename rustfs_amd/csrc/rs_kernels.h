@@ -57,7 +57,7 @@ hipError_t launch_hh256(const HashParams& p, hipStream_t stream);
 // digest output [n][C+R][32].  Requires shard_len % 512 == 0, C <= 16, R <= 4
 // and 16-B aligned shards.
 bool fused_supported(int C, int R, uint64_t shard_len);
-hipError_t launch_encode_hash_fused(GfApplyParams p, const HashParams& h, uint64_t shard_len, uint64_t n_stripes,
+hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                     hipStream_t stream);
 
 }  // namespace rsg

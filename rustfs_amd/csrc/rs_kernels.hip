@@ -358,19 +358,23 @@ __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
 
 // ---------------------------------------------------------------------------
 // Fused RS encode + per-shard HighwayHash-256 (BitrotWriter digests,
-// bitrot.rs:496-502) in one pass over HBM.  One workgroup per stripe, two
-// waves with fixed roles, walking the stripe in 512-byte column chunks:
-//   wave 0 (encoder): loads the k data chunks (8 B per lane per shard),
-//     computes and stores the m parity chunks, and stages all k+m chunks in
-//     LDS; the next chunk's loads are issued before it waits for the hasher.
-//   wave 1 (hasher): 4-lane quads advance the k+m HighwayHash streams by 16
-//     packets per chunk (HighwayHash is sequential per shard, so a stripe
-//     offers only (k+m) x 4 lanes of hash parallelism).
-// Per chunk:  encoder  compute(i) | bar A | write rows(i) | bar B | loads(i+2)..
-//             hasher              | bar A |               | bar B | hash(i) ..
-// so the encoder's arithmetic for chunk i+1 overlaps the hashing of chunk i.
+// bitrot.rs:496-502) in one pass over HBM.  One workgroup owns SPW stripes and
+// walks them in 512-byte column chunks with fixed wave roles:
+//   waves 0..SPW-1 (encoders, one per stripe): load the k data chunks (8 B per
+//     lane per shard), compute and store the m parity chunks, and stage all
+//     k+m chunks in LDS; the next chunk's loads are issued before the barrier.
+//   waves SPW.. (hashers): the SPW*(k+m) HighwayHash streams of the workgroup,
+//     one 4-lane quad per stream, 16 streams per wave, each advanced by 16
+//     packets per chunk.  HighwayHash is sequential per shard, so a stripe has
+//     only (k+m) x 4 lanes of hash parallelism; packing the streams of several
+//     stripes into full hasher waves (SPW = 4 for RS(8,4): 48 streams = 3 waves)
+//     keeps every hasher lane busy.
+// Per chunk:  encoders compute(i) | bar A | write rows(i) | bar B | loads(i+2)..
+//             hashers             | bar A |               | bar B | hash(i) ..
+// so the encoders' arithmetic for chunk i+1 overlaps the hashing of chunk i.
 // Barriers are raw s_barrier with an explicit lgkmcnt wait: __syncthreads()
-// would also drain the in-flight global loads (vmcnt(0)).
+// would also drain the in-flight global loads (vmcnt(0)).  Stripes past the end
+// of the batch keep their waves in the barrier sequence with memory ops masked.
 constexpr uint32_t kFusedChunk = 512;                 // bytes per shard per step
 constexpr uint32_t kFusedPitch = kFusedChunk + 32;    // LDS row pitch: conflict-free ds_read_b64
 
@@ -380,43 +384,71 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("" ::: "memory");
 }
 
+// A constant in a VGPR: VOP2 v_and with two VGPR operands issues at full rate
+// on gfx950, with a literal (constant bus) at half rate (tools/kbench/op_rates.hip).
+__device__ __forceinline__ uint32_t vgpr_const(uint32_t v) {
+    uint32_t r;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "i"(v));
+    return r;
+}
+
+template <int T>
+constexpr int fused_spw() {  // stripes per workgroup: fill hasher waves, cap LDS
+    return (T % 16 == 0) ? 1 : (T % 8 == 0) ? 2 : (T % 4 == 0 || T <= 6) ? 4 : 2;
+}
+
 // ABLATE (measurement builds only, tools/kbench/fused_variants.hip): bit 0
-// skips the GF arithmetic, bit 1 the hash updates; production uses 0.
-template <int C, int R, int ABLATE = 0>
-__global__ __launch_bounds__(128) void k_encode_hash_fused(const GfApplyParams p, const HashParams h) {
-    // LDS: [C][R] coefficient tables (32 B each: T0 T0' T1 T1' | T2), then the
-    // (C+R) chunk rows.  Tables are read from LDS (broadcast) at their use:
-    // held in registers across the chunk loop they cost 64+ VGPRs.
+// skips the GF arithmetic, bit 1 the hash updates, bit 3 records each wave's
+// HW_ID in its stripe's first digest words; production uses 0.
+template <int C, int R, int SPW, int ABLATE = 0>
+__global__ __launch_bounds__(64 * (SPW + (SPW * (C + R) + 15) / 16))
+__attribute__((amdgpu_waves_per_eu(R == 1 ? 4 : C <= 8 ? 7 : C <= 12 ? 5 : 4)))
+void k_encode_hash_fused(const GfApplyParams p,
+                                                                                              const HashParams h) {
+    // LDS: [C][R] coefficient tables (32 B each: T0 T0' T1 T1' | T2), then
+    // SPW x (C+R) chunk rows.  Tables are read from LDS (broadcast) at their
+    // use: held in registers across the chunk loop they cost 64+ VGPRs.
     extern __shared__ uint8_t lds_all[];
     constexpr int T = C + R;
-    constexpr int NR = (T + 15) / 16;  // hash rounds of 16 streams
     constexpr uint32_t kTabBytes = C * R * 32;
+    constexpr uint32_t kStripeRows = T * kFusedPitch;
     uint8_t* rows = lds_all + kTabBytes;
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u, q = lane & 3u;
-    const uint64_t stripe = blockIdx.x;
-    uint8_t* sb = p.out_base + stripe * p.stripe_stride;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u, q = lane & 3u;
+    const uint64_t n = h.n;
     const uint32_t chunks = p.units;  // S / kFusedChunk
 
-    if (threadIdx.x == 0) {
-#pragma unroll
-        for (int c = 0; c < C; ++c)
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                uint8_t* d = lds_all + (c * R + r) * 32;
-                *(uint4*)d = make_uint4(p.tab[r][c][0], p.tab[r][c][1], p.tab[r][c][2], p.tab[r][c][3]);
-                *(uint32_t*)(d + 16) = p.tab[r][c][4];
-            }
+    for (uint32_t i = threadIdx.x; i < (uint32_t)(C * R); i += blockDim.x) {
+        const int c = i / R, r = i % R;
+        uint8_t* d = lds_all + i * 32;
+        *(uint4*)d = make_uint4(p.tab[r][c][0], p.tab[r][c][1], p.tab[r][c][2], p.tab[r][c][3]);
+        *(uint32_t*)(d + 16) = p.tab[r][c][4];
     }
     __syncthreads();
+    if constexpr (ABLATE & 8) {
+        const uint64_t stripe = (uint64_t)blockIdx.x * SPW + (wave < SPW ? wave : 0);
+        if (lane == 0 && stripe < n) ((uint32_t*)(h.out + stripe * T * 32u))[wave < SPW ? 0 : 1 + (wave - SPW)] =
+            __builtin_amdgcn_s_getreg(0xF804);
+        return;
+    }
 
-    if (__builtin_amdgcn_readfirstlane(wave) == 0) {
+    if (wave < (uint32_t)SPW) {
         // ------------------------------ encoder ------------------------------
+        const uint64_t stripe = (uint64_t)blockIdx.x * SPW + wave;
+        const bool live = stripe < n;  // a dead stripe re-reads stripe 0 and stores nothing
+        uint8_t* sb = p.out_base + (live ? stripe : 0) * p.stripe_stride;
+        uint8_t* my_rows = rows + wave * kStripeRows;
+        const uint32_t m7 = vgpr_const(0x07070707u), m3 = vgpr_const(0x03030303u);
         uint2 x[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) x[c] = *(const uint2*)(sb + p.in_off[c] + lane * 8u);
 #pragma unroll 1
         for (uint32_t ch = 0; ch < chunks; ++ch) {
             const uint64_t off = (uint64_t)ch * kFusedChunk + lane * 8u;
+            // opaque per-iteration zero: keeps the table reads at their use
+            // instead of hoisted out of the loop into (spilled) registers
+            uint32_t tz;
+            asm volatile("s_mov_b32 %0, 0" : "=s"(tz));
+            const uint8_t* tabs = lds_all + tz;
             uint32_t acc[R][2];
 #pragma unroll
             for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = 0u;
@@ -427,12 +459,12 @@ __global__ __launch_bounds__(128) void k_encode_hash_fused(const GfApplyParams p
                     acc[c % R][1] ^= x[c].y;
                     continue;
                 }
-                const uint32_t s0a = x[c].x & 0x07070707u, s0b = x[c].y & 0x07070707u;
-                const uint32_t s1a = (x[c].x >> 3) & 0x07070707u, s1b = (x[c].y >> 3) & 0x07070707u;
-                const uint32_t s2a = (x[c].x >> 6) & 0x03030303u, s2b = (x[c].y >> 6) & 0x03030303u;
+                const uint32_t s0a = x[c].x & m7, s0b = x[c].y & m7;
+                const uint32_t s1a = (x[c].x >> 3) & m7, s1b = (x[c].y >> 3) & m7;
+                const uint32_t s2a = (x[c].x >> 6) & m3, s2b = (x[c].y >> 6) & m3;
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    const uint8_t* tp = lds_all + (c * R + r) * 32;  // wave-uniform: broadcast read
+                    const uint8_t* tp = tabs + (c * R + r) * 32;  // wave-uniform: broadcast read
                     const uint4 t4 = *(const uint4*)tp;
                     const uint32_t t2 = *(const uint32_t*)(tp + 16);
                     acc[r][0] ^= __builtin_amdgcn_perm(t4.y, t4.x, s0a) ^ __builtin_amdgcn_perm(t4.w, t4.z, s1a) ^
@@ -441,19 +473,21 @@ __global__ __launch_bounds__(128) void k_encode_hash_fused(const GfApplyParams p
                                  __builtin_amdgcn_perm(t2, t2, s2b);
                 }
             }
+            if (live) {
 #pragma unroll
-            for (int r = 0; r < R; ++r) *(uint2*)(sb + p.out_off[r] + off) = make_uint2(acc[r][0], acc[r][1]);
+                for (int r = 0; r < R; ++r) *(uint2*)(sb + p.out_off[r] + off) = make_uint2(acc[r][0], acc[r][1]);
+            }
             uint2 y[C];
             if (ch + 1 < chunks) {
 #pragma unroll
                 for (int c = 0; c < C; ++c) y[c] = *(const uint2*)(sb + p.in_off[c] + off + kFusedChunk);
             }
-            lds_barrier();  // A: the hasher is done with chunk ch-1's rows
+            lds_barrier();  // A: the hashers are done with chunk ch-1's rows
 #pragma unroll
-            for (int c = 0; c < C; ++c) *(uint2*)(rows + c * kFusedPitch + lane * 8u) = x[c];
+            for (int c = 0; c < C; ++c) *(uint2*)(my_rows + c * kFusedPitch + lane * 8u) = x[c];
 #pragma unroll
             for (int r = 0; r < R; ++r)
-                *(uint2*)(rows + (C + r) * kFusedPitch + lane * 8u) = make_uint2(acc[r][0], acc[r][1]);
+                *(uint2*)(my_rows + (C + r) * kFusedPitch + lane * 8u) = make_uint2(acc[r][0], acc[r][1]);
             lds_barrier();  // B: rows of chunk ch are ready
             if (ch + 1 < chunks) {
 #pragma unroll
@@ -462,35 +496,30 @@ __global__ __launch_bounds__(128) void k_encode_hash_fused(const GfApplyParams p
         }
     } else {
         // ------------------------------ hasher -------------------------------
-        HHQuad st[NR];
-#pragma unroll
-        for (int r = 0; r < NR; ++r) hhq_init(st[r], h.key, q);
+        const uint32_t g = (wave - SPW) * 16u + (lane >> 2);  // stream of this quad
+        const uint32_t ls = g / T, shard = g - ls * T;        // local stripe, shard
+        const uint64_t stripe = (uint64_t)blockIdx.x * SPW + ls;
+        const bool live = g < (uint32_t)(SPW * T) && stripe < n;
+        const uint8_t* row = rows + (live ? ls * kStripeRows + shard * kFusedPitch : 0) + 8 * q;
+        HHQuad st;
+        hhq_init(st, h.key, q);
 #pragma unroll 1
         for (uint32_t ch = 0; ch < chunks; ++ch) {
             lds_barrier();  // A
             lds_barrier();  // B
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                const uint32_t g = r * 16 + (lane >> 2);
-                if (g < (uint32_t)T) {
-                    const uint8_t* row = rows + g * kFusedPitch + 8 * q;
+            if (live) {
 #pragma unroll 4
-                    for (int t = 0; t < (int)(kFusedChunk / 32); ++t) {
-                        const u32x2 v = *(const u32x2*)(row + t * 32);
-                        if constexpr (ABLATE & 2) {
-                            st[r].v0 ^= __builtin_bit_cast(uint64_t, v);
-                        } else {
-                            hhq_update(st[r], __builtin_bit_cast(uint64_t, v));
-                        }
+                for (int t = 0; t < (int)(kFusedChunk / 32); ++t) {
+                    const u32x2 v = *(const u32x2*)(row + t * 32);
+                    if constexpr (ABLATE & 2) {
+                        st.v0 ^= __builtin_bit_cast(uint64_t, v);
+                    } else {
+                        hhq_update(st, __builtin_bit_cast(uint64_t, v));
                     }
                 }
             }
         }
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            const uint32_t g = r * 16 + (lane >> 2);
-            if (g < (uint32_t)T) hhq_finish(st[r], h.out + (stripe * T + g) * 32u, q);
-        }
+        if (live) hhq_finish(st, h.out + (stripe * T + shard) * 32u, q);
     }
 }
 
@@ -589,18 +618,29 @@ hipError_t launch_hh256(const HashParams& p, hipStream_t stream) {
 
 using FusedKernel = void (*)(const GfApplyParams, const HashParams);
 
-template <int C>
-static FusedKernel pick_fused_r(int R) {
-    switch (R) {
-        case 1: return k_encode_hash_fused<C, 1>;
-        case 2: return k_encode_hash_fused<C, 2>;
-        case 3: return k_encode_hash_fused<C, 3>;
-        case 4: return k_encode_hash_fused<C, 4>;
-    }
-    return nullptr;
+struct FusedPick {
+    FusedKernel k;
+    int spw, waves;
+};
+
+template <int C, int R>
+static FusedPick fused_entry() {
+    constexpr int spw = fused_spw<C + R>();
+    return {k_encode_hash_fused<C, R, spw>, spw, spw + (spw * (C + R) + 15) / 16};
 }
 
-static FusedKernel pick_fused(int C, int R) {
+template <int C>
+static FusedPick pick_fused_r(int R) {
+    switch (R) {
+        case 1: return fused_entry<C, 1>();
+        case 2: return fused_entry<C, 2>();
+        case 3: return fused_entry<C, 3>();
+        case 4: return fused_entry<C, 4>();
+    }
+    return {nullptr, 0, 0};
+}
+
+static FusedPick pick_fused(int C, int R) {
     switch (C) {
         case 1: return pick_fused_r<1>(R);
         case 2: return pick_fused_r<2>(R);
@@ -619,7 +659,7 @@ static FusedKernel pick_fused(int C, int R) {
         case 15: return pick_fused_r<15>(R);
         case 16: return pick_fused_r<16>(R);
     }
-    return nullptr;
+    return {nullptr, 0, 0};
 }
 
 bool fused_supported(int C, int R, uint64_t shard_len) {
@@ -627,14 +667,16 @@ bool fused_supported(int C, int R, uint64_t shard_len) {
            shard_len % kFusedChunk == 0 && shard_len / kFusedChunk <= 0xffffffffull;
 }
 
-hipError_t launch_encode_hash_fused(GfApplyParams p, const HashParams& h, uint64_t shard_len, uint64_t n_stripes,
+hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                     hipStream_t stream) {
-    FusedKernel k = pick_fused((int)p.C, (int)p.R);
-    if (!k || !fused_supported((int)p.C, (int)p.R, shard_len) || n_stripes == 0 || n_stripes > 0x7fffffffull)
+    const FusedPick f = pick_fused((int)p.C, (int)p.R);
+    if (!f.k || !fused_supported((int)p.C, (int)p.R, shard_len) || n_stripes == 0 || n_stripes > 0x7fffffffull)
         return hipErrorInvalidValue;
     p.units = (uint32_t)(shard_len / kFusedChunk);
-    const size_t lds = (size_t)p.C * p.R * 32 + (size_t)(p.C + p.R) * kFusedPitch;
-    hipLaunchKernelGGL(k, dim3((uint32_t)n_stripes), dim3(128), lds, stream, p, h);
+    h.n = n_stripes;
+    const size_t lds = (size_t)p.C * p.R * 32 + (size_t)f.spw * (p.C + p.R) * kFusedPitch;
+    const uint64_t blocks = (n_stripes + f.spw - 1) / f.spw;
+    hipLaunchKernelGGL(f.k, dim3((uint32_t)blocks), dim3(64 * f.waves), lds, stream, p, h);
     return hipGetLastError();
 }
 

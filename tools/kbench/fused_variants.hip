@@ -58,7 +58,10 @@ int main(int argc, char** argv) {
     const uint64_t key[4] = {0xcd8a238efa34e74bull, 0x528596bbe6833e26ull, 0x14449fa35d930f04ull, 0xa036de22139de097ull};
     memcpy(h.key, key, sizeof(key));
     h.out = dig;
-    const size_t lds = (size_t)K * M * 32 + (size_t)(K + M) * kFusedPitch;
+    h.n = n;
+    const size_t lds1 = (size_t)K * M * 32 + (size_t)(K + M) * kFusedPitch;
+    const size_t lds4 = (size_t)K * M * 32 + (size_t)4 * (K + M) * kFusedPitch;
+    const uint32_t g4 = (uint32_t)((n + 3) / 4);
     HashParams hq;
     memset(&hq, 0, sizeof(hq));
     hq.data = d; hq.len = S; hq.n = n * (K + M); hq.shards = K + M; hq.shard_pitch = S; hq.stripe_stride = STRIDE;
@@ -68,10 +71,12 @@ int main(int argc, char** argv) {
     pe.units = S / 16;
     struct V { const char* name; std::function<void()> f; };
     std::vector<V> vs = {
-        {"fused", [&] { k_encode_hash_fused<K, M, 0><<<n, 128, lds>>>(p, h); }},
-        {"fused no-GF", [&] { k_encode_hash_fused<K, M, 1><<<n, 128, lds>>>(p, h); }},
-        {"fused no-hash", [&] { k_encode_hash_fused<K, M, 2><<<n, 128, lds>>>(p, h); }},
-        {"fused neither", [&] { k_encode_hash_fused<K, M, 3><<<n, 128, lds>>>(p, h); }},
+        {"fused spw4 (prod)", [&] { CK(launch_encode_hash_fused(p, h, S, n, 0)); }},
+        {"fused spw1", [&] { k_encode_hash_fused<K, M, 1, 0><<<n, 128, lds1>>>(p, h); }},
+        {"fused spw2", [&] { k_encode_hash_fused<K, M, 2, 0><<<(n + 1) / 2, 64 * 4, lds1 * 2 - K * M * 32>>>(p, h); }},
+        {"spw4 no-GF", [&] { k_encode_hash_fused<K, M, 4, 1><<<g4, 448, lds4>>>(p, h); }},
+        {"spw4 no-hash", [&] { k_encode_hash_fused<K, M, 4, 2><<<g4, 448, lds4>>>(p, h); }},
+        {"spw4 neither", [&] { k_encode_hash_fused<K, M, 4, 3><<<g4, 448, lds4>>>(p, h); }},
         {"encode only", [&] { CK(launch_gf_apply_vec(pe, n, 0)); }},
         {"quad hash only", [&] { CK(launch_hh256(hq, 0)); }},
     };
@@ -89,6 +94,18 @@ int main(int argc, char** argv) {
             CK(hipEventElapsedTime(&ms, a, b));
             if (it) t[v].push_back(ms);
         }
+    // where do the two waves of a workgroup run?  HW_ID bits [5:4] = SIMD, [11:8] = CU
+    k_encode_hash_fused<K, M, 1, 8><<<n, 128, lds1>>>(p, h);
+    CK(hipDeviceSynchronize());
+    std::vector<uint8_t> hd(n * (K + M) * 32);
+    CK(hipMemcpy(hd.data(), dig, hd.size(), hipMemcpyDeviceToHost));
+    int pairs[4][4] = {};
+    for (uint64_t s = 0; s < n; ++s) {
+        const uint32_t* w = (const uint32_t*)(hd.data() + s * (K + M) * 32);
+        pairs[(w[0] >> 4) & 3][(w[1] >> 4) & 3]++;
+    }
+    printf("encoder SIMD x hasher SIMD histogram (rows: encoder simd)\n");
+    for (int a = 0; a < 4; ++a) printf("  %6d %6d %6d %6d\n", pairs[a][0], pairs[a][1], pairs[a][2], pairs[a][3]);
     const double alg = (double)n * STRIDE;
     for (size_t v = 0; v < vs.size(); ++v) {
         auto& x = t[v];

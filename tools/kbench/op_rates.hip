@@ -10,6 +10,7 @@ constexpr int ITERS = 4096;
 
 template <int OP>
 __global__ __launch_bounds__(256) void k(uint64_t* out, uint64_t seed) {
+    const uint32_t seed_s = (uint32_t)seed;
     uint64_t a[8];
     uint32_t b[8];
 #pragma unroll
@@ -25,6 +26,17 @@ __global__ __launch_bounds__(256) void k(uint64_t* out, uint64_t seed) {
             if constexpr (OP == 5) asm volatile("v_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=v"(b[i]) : "v"(b[(i + 1) & 7]));
             if constexpr (OP == 6) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(b[i]) : "v"(b[(i + 1) & 7]));
             if constexpr (OP == 7) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(b[i]) : "v"(b[(i + 1) & 7]));
+            if constexpr (OP == 8) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(b[i]) : "v"(b[(i + 1) & 7]), "s"(seed_s));
+            if constexpr (OP == 9) asm volatile("v_perm_b32 %0, %1, %1, %0" : "+v"(b[i]) : "v"(b[(i + 1) & 7]));
+            if constexpr (OP == 10) asm volatile("v_perm_b32 %0, %1, %1, %0" : "+v"(b[i]) : "s"(seed_s));
+            if constexpr (OP == 11) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(b[i]) : "v"(b[(i + 1) & 7]), "v"(b[(i + 3) & 7]));
+            if constexpr (OP == 12) asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(b[i]) : "v"(b[(i + 1) & 7]), "s"(seed_s));
+            if constexpr (OP == 13) asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(b[i]));
+            if constexpr (OP == 14) asm volatile("v_bfe_u32 %0, %0, 3, %1" : "+v"(b[i]) : "v"(b[(i + 1) & 7]));
+            if constexpr (OP == 15) asm volatile("v_xad_u32 %0, %0, %1, %2" : "+v"(b[i]) : "v"(b[(i + 1) & 7]), "v"(b[(i + 3) & 7]));
+            if constexpr (OP == 16) asm volatile("v_lshl_add_u64 %0, %1, 0, %0" : "+v"(a[i]) : "s"(seed));
+            if constexpr (OP == 17) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(b[i]) : "s"(seed_s));
+            if constexpr (OP == 18) asm volatile("v_perm_b32 %0, %0, %0, %1" : "+v"(b[i]) : "v"(b[(i + 1) & 7]));
         }
     }
     uint64_t r = 0;
@@ -52,10 +64,16 @@ int main() {
     const int blocks = 256 * 8;  // 8 blocks of 4 waves per CU = 8 waves per SIMD
     uint64_t* d;
     CK(hipMalloc(&d, (size_t)blocks * 256 * 8));
-    const char* names[] = {"v_lshl_add_u64", "v_mad_u64_u32", "v_perm_b32", "v_xor_b32", "add_co+addc (2 ops)", "v_mov_b32_dpp", "v_mul_lo_u32", "v_mul_hi_u32"};
-    float ms[8] = {run<0>(d, blocks), run<1>(d, blocks), run<2>(d, blocks), run<3>(d, blocks), run<4>(d, blocks), run<5>(d, blocks), run<6>(d, blocks), run<7>(d, blocks)};
+    const char* names[] = {"v_lshl_add_u64 v,v", "v_mad_u64_u32", "v_perm_b32 v,v,v", "v_xor_b32 v,v", "add_co+addc (2 ops)",
+                           "v_mov_b32_dpp", "v_mul_lo_u32", "v_mul_hi_u32", "v_perm_b32 v,v,s", "v_perm_b32 x,x,v",
+                           "v_perm_b32 s,s,v", "v_add3_u32 v,v,v", "v_and_or_b32 v,v,s", "v_lshrrev_b32 imm", "v_bfe_u32",
+                           "v_xad_u32 v,v,v", "v_lshl_add_u64 s,v", "v_xor_b32 s,v", "v_perm_b32 v0,v0,v"};
+    float ms[19] = {run<0>(d, blocks), run<1>(d, blocks), run<2>(d, blocks), run<3>(d, blocks), run<4>(d, blocks),
+                    run<5>(d, blocks), run<6>(d, blocks), run<7>(d, blocks), run<8>(d, blocks), run<9>(d, blocks),
+                    run<10>(d, blocks), run<11>(d, blocks), run<12>(d, blocks), run<13>(d, blocks), run<14>(d, blocks),
+                    run<15>(d, blocks), run<16>(d, blocks), run<17>(d, blocks), run<18>(d, blocks)};
     const double waves_per_simd = 8, clk = 2.1e9;
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 19; ++i) {
         const double ops = waves_per_simd * ITERS * 8;  // wave-ops per SIMD
         printf("%-22s %.3f ms  ~%.2f SIMD cycles per wave-op (at %.1f GHz)\n", names[i], ms[i], ms[i] * 1e-3 * clk / ops,
                clk / 1e9);
