@@ -392,9 +392,12 @@ __device__ __forceinline__ uint32_t vgpr_const(uint32_t v) {
     return r;
 }
 
-template <int T>
-constexpr int fused_spw() {  // stripes per workgroup: fill hasher waves, cap LDS
+constexpr int fused_spw_for(int T) {  // stripes per workgroup: fill hasher waves, cap LDS
     return (T % 16 == 0) ? 1 : (T % 8 == 0) ? 2 : (T % 4 == 0 || T <= 6) ? 4 : 2;
+}
+template <int T>
+constexpr int fused_spw() {
+    return fused_spw_for(T);
 }
 
 // ABLATE (measurement builds only, tools/kbench/fused_variants.hip): bit 0
@@ -623,41 +626,44 @@ struct FusedPick {
     int spw, waves;
 };
 
+// packed: SPW = fused_spw (full hasher waves); !packed: one stripe per
+// workgroup (A/B only).
 template <int C, int R>
-static FusedPick fused_entry() {
+static FusedPick fused_entry(bool packed) {
     constexpr int spw = fused_spw<C + R>();
+    if (!packed || spw == 1) return {k_encode_hash_fused<C, R, 1>, 1, 1 + (C + R + 15) / 16};
     return {k_encode_hash_fused<C, R, spw>, spw, spw + (spw * (C + R) + 15) / 16};
 }
 
 template <int C>
-static FusedPick pick_fused_r(int R) {
+static FusedPick pick_fused_r(int R, bool packed) {
     switch (R) {
-        case 1: return fused_entry<C, 1>();
-        case 2: return fused_entry<C, 2>();
-        case 3: return fused_entry<C, 3>();
-        case 4: return fused_entry<C, 4>();
+        case 1: return fused_entry<C, 1>(packed);
+        case 2: return fused_entry<C, 2>(packed);
+        case 3: return fused_entry<C, 3>(packed);
+        case 4: return fused_entry<C, 4>(packed);
     }
     return {nullptr, 0, 0};
 }
 
-static FusedPick pick_fused(int C, int R) {
+static FusedPick pick_fused(int C, int R, bool packed) {
     switch (C) {
-        case 1: return pick_fused_r<1>(R);
-        case 2: return pick_fused_r<2>(R);
-        case 3: return pick_fused_r<3>(R);
-        case 4: return pick_fused_r<4>(R);
-        case 5: return pick_fused_r<5>(R);
-        case 6: return pick_fused_r<6>(R);
-        case 7: return pick_fused_r<7>(R);
-        case 8: return pick_fused_r<8>(R);
-        case 9: return pick_fused_r<9>(R);
-        case 10: return pick_fused_r<10>(R);
-        case 11: return pick_fused_r<11>(R);
-        case 12: return pick_fused_r<12>(R);
-        case 13: return pick_fused_r<13>(R);
-        case 14: return pick_fused_r<14>(R);
-        case 15: return pick_fused_r<15>(R);
-        case 16: return pick_fused_r<16>(R);
+        case 1: return pick_fused_r<1>(R, packed);
+        case 2: return pick_fused_r<2>(R, packed);
+        case 3: return pick_fused_r<3>(R, packed);
+        case 4: return pick_fused_r<4>(R, packed);
+        case 5: return pick_fused_r<5>(R, packed);
+        case 6: return pick_fused_r<6>(R, packed);
+        case 7: return pick_fused_r<7>(R, packed);
+        case 8: return pick_fused_r<8>(R, packed);
+        case 9: return pick_fused_r<9>(R, packed);
+        case 10: return pick_fused_r<10>(R, packed);
+        case 11: return pick_fused_r<11>(R, packed);
+        case 12: return pick_fused_r<12>(R, packed);
+        case 13: return pick_fused_r<13>(R, packed);
+        case 14: return pick_fused_r<14>(R, packed);
+        case 15: return pick_fused_r<15>(R, packed);
+        case 16: return pick_fused_r<16>(R, packed);
     }
     return {nullptr, 0, 0};
 }
@@ -669,7 +675,14 @@ bool fused_supported(int C, int R, uint64_t shard_len) {
 
 hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                     hipStream_t stream) {
-    const FusedPick f = pick_fused((int)p.C, (int)p.R);
+    // Packed workgroups measured as fast or faster than one stripe per
+    // workgroup at every batch size tried (n = 256..65536; tools/sweep_small_batch.sh);
+    // RSG_FUSED_SPW1=1 selects the unpacked variant for A/B runs.
+    static const bool unpacked = [] {
+        const char* e = getenv("RSG_FUSED_SPW1");
+        return e && e[0] == '1';
+    }();
+    const FusedPick f = pick_fused((int)p.C, (int)p.R, !unpacked);
     if (!f.k || !fused_supported((int)p.C, (int)p.R, shard_len) || n_stripes == 0 || n_stripes > 0x7fffffffull)
         return hipErrorInvalidValue;
     p.units = (uint32_t)(shard_len / kFusedChunk);
