@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RSG_ABI_VERSION 1
+#define RSG_ABI_VERSION 2
 #define RSG_MAX_TOTAL_SHARDS 256 /* galois_8::Field::ORDER, erasure.rs:72 */
 #define RSG_DIGEST_BYTES 32      /* HighwayHash-256 */
 
@@ -51,7 +51,10 @@ typedef enum rsg_status {
     RSG_ERR_NO_DEVICE = 12,            /* no HIP device / bad ordinal */
     RSG_ERR_DEVICE = 13,               /* HIP runtime failure */
     RSG_ERR_OUT_OF_MEMORY = 14,
-    RSG_ERR_UNSUPPORTED = 15
+    RSG_ERR_UNSUPPORTED = 15,
+    RSG_ERR_FILE_SIZE_MISMATCH = 16,   /* "bitrot shard file size mismatch", bitrot.rs:627 */
+    RSG_ERR_UNEXPECTED_EOF = 17,       /* io::ErrorKind::UnexpectedEof from read_exact, bitrot.rs:631,639 */
+    RSG_ERR_TRAILING_DATA = 18         /* "bitrot shard file has trailing data", bitrot.rs:651 */
 } rsg_status;
 
 /* Bitrot hash selector (crates/utils/src/hash.rs:52-68). */
@@ -155,6 +158,37 @@ int rsg_hash_batch_dev(rsg_ctx *ctx, int algo, const uint8_t *d_data, size_t len
 int rsg_decode_records_dev(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t n,
                            const uint8_t *const *d_files, int algo, int verify_surplus,
                            uint8_t *d_out, int *h_status, void *stream);
+
+/* Heal, batched (Erasure::heal, heal.rs:112-206, which calls
+ * decode_data_and_parity, erasure.rs:917, per block).  Sources as in
+ * rsg_decode_records_dev (d_files[i] == NULL: no reader; every record is
+ * verified before use).  d_targets[i] != NULL marks shard i as a heal target
+ * (a writer): it receives n BitrotWriter records [HH256S][shard_len bytes]
+ * (stride 32+shard_len) of the rebuilt shard i (data shards as read/rebuilt,
+ * parity re-encoded).  Every verified source parity is compared with the
+ * parity re-encoded from the data (heal.rs:180-196).  d_work: device
+ * workspace of n*k*shard_len bytes (receives the data of every stripe).
+ * h_status[s]: RSG_OK, RSG_ERR_TOO_FEW_SHARDS (ErasureReadQuorum) or
+ * RSG_ERR_INCONSISTENT_SOURCES ("inconsistent heal source shards"); target
+ * records of a failed stripe are unspecified.  Synchronous. */
+int rsg_heal_records_dev(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t n,
+                         const uint8_t *const *d_files, uint8_t *const *d_targets, int algo,
+                         uint8_t *d_work, int *h_status, void *stream);
+
+/* Whole-shard-file bitrot verification (bitrot_verify, bitrot.rs:616-655) of
+ * n_files device-resident shard files of one part (file f: file_lens[f]
+ * bytes at d_files[f]).  want_size must equal
+ * bitrot_shard_file_size(part_size, shard_size, algo) (else every file gets
+ * RSG_ERR_FILE_SIZE_MISMATCH); then records are checked in order like the
+ * reference's read loop: h_status[f] = RSG_ERR_BITROT_MISMATCH at the first
+ * bad digest, RSG_ERR_UNEXPECTED_EOF if the file ends early,
+ * RSG_ERR_TRAILING_DATA if it is longer than want_size, else RSG_OK.
+ * algo: HIGHWAY256S / LEGACY (streaming records) or NONE (sizes only);
+ * whole-file algorithms are RSG_ERR_UNSUPPORTED, as in the reference.
+ * Synchronous. */
+int rsg_bitrot_verify_dev(rsg_ctx *ctx, int algo, size_t n_files, const uint8_t *const *d_files,
+                          const size_t *file_lens, size_t want_size, size_t part_size, size_t shard_size,
+                          int *h_status, void *stream);
 
 /* Block until all work queued on `stream` (NULL = the null stream) is done. */
 int rsg_sync(rsg_ctx *ctx, void *stream);

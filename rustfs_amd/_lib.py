@@ -36,6 +36,9 @@ RSG_ERR_NO_DEVICE = 12
 RSG_ERR_DEVICE = 13
 RSG_ERR_OUT_OF_MEMORY = 14
 RSG_ERR_UNSUPPORTED = 15
+RSG_ERR_FILE_SIZE_MISMATCH = 16
+RSG_ERR_UNEXPECTED_EOF = 17
+RSG_ERR_TRAILING_DATA = 18
 
 RSG_HASH_NONE = 0
 RSG_HASH_HIGHWAY256S = 1
@@ -51,7 +54,7 @@ EXPORTED = (
     "rsg_matrix", "rsg_check_geometry", "rsg_encode", "rsg_reconstruct", "rsg_verify",
     "rsg_hash", "rsg_encode_batch_dev", "rsg_reconstruct_batch_dev", "rsg_verify_batch_dev",
     "rsg_hash_batch_dev", "rsg_sync", "rsg_encode_batch_host", "rsg_pin", "rsg_unpin",
-    "rsg_decode_records_dev",
+    "rsg_decode_records_dev", "rsg_heal_records_dev", "rsg_bitrot_verify_dev",
 )
 
 
@@ -103,6 +106,8 @@ def load():
         L.rsg_sync.argtypes = [P, P]
         L.rsg_encode_batch_host.argtypes = [P, I, I, S, S, P, S, S, P, I]
         L.rsg_decode_records_dev.argtypes = [P, I, I, S, S, P, I, I, P, P, P]
+        L.rsg_heal_records_dev.argtypes = [P, I, I, S, S, P, P, I, P, P, P]
+        L.rsg_bitrot_verify_dev.argtypes = [P, I, S, P, P, S, S, S, P, P]
         L.rsg_pin.argtypes = [P, S]
         L.rsg_unpin.argtypes = [P]
         _lib = L

@@ -121,6 +121,41 @@ def bitrot_verify(r, want_size: int, part_size: int, algo: HashAlgorithm, shard_
         raise IOError("bitrot shard file has trailing data")
 
 
+def bitrot_verify_batch(files, want_size: int, part_size: int, algo: HashAlgorithm, shard_size: int,
+                        stream=None) -> list:
+    """Device-batch whole-shard-file verification (rsg_bitrot_verify_dev):
+    `files` are cuda uint8 tensors holding complete shard files of one part.
+    Returns one rsg_status per file with bitrot_verify's decision order
+    (bitrot.rs:616-655): size mismatch, first bad record, early EOF, trailing
+    data.  `raise_for_status` turns a status into the reference's error."""
+    import torch
+    n = len(files)
+    dev = None
+    for f in files:
+        if f.dtype != torch.uint8 or not f.is_cuda or not f.is_contiguous():
+            raise TypeError("files must be contiguous cuda uint8 tensors")
+        dev = f.device
+    if n == 0:
+        return []
+    ptrs = (ctypes.c_void_p * n)(*[f.data_ptr() if f.numel() else None for f in files])
+    lens = (ctypes.c_size_t * n)(*[f.numel() for f in files])
+    status = (ctypes.c_int * n)()
+    s = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    _lib.check(_lib.load().rsg_bitrot_verify_dev(
+        _lib.context(dev.index or 0).handle, algo.value, n, ptrs, lens, want_size, part_size, shard_size, status,
+        s), "bitrot_verify")
+    return [int(status[i]) for i in range(n)]
+
+
+def raise_for_status(code: int) -> None:
+    """bitrot_verify's error for an rsg_bitrot_verify_dev status."""
+    if code == _lib.RSG_OK:
+        return
+    if code == _lib.RSG_ERR_UNEXPECTED_EOF:
+        raise EOFError("unexpected eof")
+    raise IOError(_lib.strerror(code))
+
+
 def frame_shards(shards, digests) -> list:
     """encode_inline_shards layout: one ``[hash][shard]`` bytes object per shard
     (encode.rs:601-628), from shard bytes and their 32-byte digests."""
@@ -128,4 +163,4 @@ def frame_shards(shards, digests) -> list:
 
 
 __all__ = ["HashAlgorithm", "bitrot_shard_file_size", "BitrotWriter", "BitrotReader", "split_and_verify",
-           "bitrot_verify", "frame_shards", "io"]
+           "bitrot_verify", "bitrot_verify_batch", "raise_for_status", "frame_shards", "io"]

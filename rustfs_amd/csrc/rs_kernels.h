@@ -39,7 +39,8 @@ struct HashParams {
     uint64_t shard_pitch;    // bytes between messages of one stripe
     uint64_t stripe_stride;  // bytes between stripes
     uint64_t key[4];
-    uint8_t* out;            // n x 32 digests (may be null in verify mode)
+    uint8_t* out;            // digests (may be null in verify mode)
+    uint64_t out_stride;     // bytes between digests j and j+1 (0 = 32: packed)
     uint32_t aligned16;      // every message 16-B aligned: vector loads
     // verify mode (expect != null): compare with the stored digest of message j
     // at expect + j*expect_stride and clear flags[j] on mismatch

@@ -352,7 +352,7 @@ __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
         const uint64_t h = hhq_digest(s, q);
         if (h != ld64_any(p.expect + j * p.expect_stride + 8 * q)) p.flags[j] = 0;
     } else {
-        hhq_finish(s, p.out + j * 32u, q);
+        hhq_finish(s, p.out + j * (p.out_stride ? p.out_stride : 32u), q);
     }
 }
 

@@ -437,6 +437,9 @@ const char* rsg_strerror(int status) {
         case RSG_ERR_DEVICE: return "HIP runtime error";
         case RSG_ERR_OUT_OF_MEMORY: return "out of device memory";
         case RSG_ERR_UNSUPPORTED: return "unsupported configuration";
+        case RSG_ERR_FILE_SIZE_MISMATCH: return "bitrot shard file size mismatch";
+        case RSG_ERR_UNEXPECTED_EOF: return "unexpected end of file";
+        case RSG_ERR_TRAILING_DATA: return "bitrot shard file has trailing data";
     }
     return "unknown rsgpu status";
 }
@@ -659,27 +662,19 @@ int rsg_hash_batch_dev(rsg_ctx* ctx, int algo, const uint8_t* d_data, size_t len
 // GET-side engine: verify every [digest][block] record, then copy or rebuild
 // the data shards of each stripe, runs of stripes with one erasure pattern at
 // a time (normally one run: whole shard files present or absent).
-int rsg_decode_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n, const uint8_t* const* d_files,
-                           int algo, int verify_surplus, uint8_t* d_out, int* h_status, void* stream) {
-    int st = enter(ctx);
-    if (st) return st;
-    if ((st = check_geometry(k, m))) return st;
-    if (!d_files || (n && (!d_out || !h_status))) return RSG_ERR_INVALID_ARG;
-    const uint64_t* key = hash_key(algo);
-    if (!key) return RSG_ERR_INVALID_ARG;
-    if (n == 0 || shard_len == 0) {
-        for (size_t s = 0; s < n; ++s) h_status[s] = RSG_OK;
-        return RSG_OK;
-    }
-    const int t = k + m;
-    const uint64_t rec = 32 + shard_len;  // BitrotWriter record: [hash][block]
-    hipStream_t s = pick_stream(ctx, stream);
-    std::lock_guard<std::mutex> g(ctx->mu);
-    if ((st = ctx->ensure_scratch((size_t)(t + 1) * n))) return st;
-    uint8_t* d_flags = ctx->d_scratch;  // [shard][stripe] 1 = record verified
-    uint8_t* d_ok = d_flags + (size_t)t * n;  // surplus-parity verdict per stripe
-    if ((st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
-    // 1. verify every available record
+}  // extern "C"
+
+namespace {
+
+// Verify-before-use of n BitrotWriter records ([hash][S bytes]) of every
+// available shard file: on return flags[i*n + s] = 1 iff shard i's record s is
+// present and its stored digest matches (split_and_verify, bitrot.rs:227-247).
+// Needs ctx->mu held; uses ctx->d_scratch[0, t*n).
+int verify_records(rsg_ctx* ctx, int t, uint64_t shard_len, uint64_t n, const uint8_t* const* d_files,
+                   const uint64_t* key, std::vector<uint8_t>& flags, hipStream_t s) {
+    const uint64_t rec = 32 + shard_len;
+    uint8_t* d_flags = ctx->d_scratch;
+    int st;
     for (int i = 0; i < t; ++i) {
         if ((st = hip_status(hipMemsetAsync(d_flags + (size_t)i * n, d_files[i] ? 1 : 0, n, s)))) return st;
         if (!d_files[i]) continue;
@@ -697,90 +692,301 @@ int rsg_decode_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t 
         h.flags = d_flags + (size_t)i * n;
         if ((st = hip_status(rsg::launch_hh256(h, s)))) return st;
     }
-    std::vector<uint8_t> flags((size_t)t * n);
+    flags.assign((size_t)t * n, 0);
     if ((st = hip_status(hipMemcpyAsync(flags.data(), d_flags, flags.size(), hipMemcpyDeviceToHost, s)))) return st;
-    if ((st = hip_status(hipStreamSynchronize(s)))) return st;
-    auto cd = m > 0 ? get_codec(k, m) : nullptr;
-    if (m > 0 && !cd) return RSG_ERR_INVALID_ARG;
-    // 2. runs of stripes with the same verified-shard pattern
+    return hip_status(hipStreamSynchronize(s));
+}
+
+// Calls f(s0, s1, present) for each maximal run of stripes sharing one
+// verified-shard pattern (degraded stripes come in long runs: a lost disk).
+template <class F>
+int for_each_pattern_run(int t, uint64_t n, const std::vector<uint8_t>& flags, F&& f) {
     std::vector<uint8_t> present(t);
-    bool any_verify = false;
-    for (size_t s0 = 0; s0 < n;) {
+    for (uint64_t s0 = 0; s0 < n;) {
         for (int i = 0; i < t; ++i) present[i] = flags[(size_t)i * n + s0];
-        size_t s1 = s0 + 1;
+        uint64_t s1 = s0 + 1;
         for (; s1 < n; ++s1) {
             bool same = true;
             for (int i = 0; i < t && same; ++i) same = flags[(size_t)i * n + s1] == present[i];
             if (!same) break;
         }
+        int st = f(s0, s1, present);
+        if (st) return st;
+        s0 = s1;
+    }
+    return RSG_OK;
+}
+
+// GET engine body (ctx->mu held): verify records, copy/rebuild the k data
+// shards of every stripe into d_out (n x k*S), optional surplus-parity check.
+// Uses ctx->d_scratch[0, (t+1)*n).  `flags` returns the verified-shard map.
+int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64_t n, const uint8_t* const* d_files,
+                          const uint64_t* key, bool verify_surplus, uint8_t* d_out, int* h_status,
+                          std::vector<uint8_t>& flags, hipStream_t s) {
+    const int t = k + m;
+    const uint64_t rec = 32 + shard_len;  // BitrotWriter record: [hash][block]
+    int st;
+    if ((st = ctx->ensure_scratch((size_t)(t + 1) * n))) return st;
+    uint8_t* d_ok = ctx->d_scratch + (size_t)t * n;  // surplus-parity verdict per stripe
+    if ((st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
+    // 1. verify every available record
+    if ((st = verify_records(ctx, t, shard_len, n, d_files, key, flags, s))) return st;
+    auto cd = m > 0 ? get_codec(k, m) : nullptr;
+    if (m > 0 && !cd) return RSG_ERR_INVALID_ARG;
+    bool any_verify = false;
+    // 2. per run of stripes with one pattern: copy present data, rebuild the rest
+    st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) -> int {
         const uint64_t cnt = s1 - s0;
-        int valid = 0, missing_data = 0;
+        int valid = 0, missing_data = 0, e;
         for (int i = 0; i < t; ++i) valid += present[i];
         for (int i = 0; i < k; ++i) missing_data += present[i] ? 0 : 1;
-        int run_status = RSG_OK;
-        if (valid < k) {
-            run_status = RSG_ERR_TOO_FEW_SHARDS;
-        } else {
-            uint8_t* out = d_out + s0 * (uint64_t)k * shard_len;
-            for (int i = 0; i < k; ++i)  // present data shards: strided copy out of the records
-                if (present[i] && (st = hip_status(hipMemcpy2DAsync(out + i * shard_len, (size_t)k * shard_len,
-                                                                    d_files[i] + s0 * rec + 32, rec, shard_len, cnt,
-                                                                    hipMemcpyDeviceToDevice, s))))
-                    return st;
-            if (missing_data) {
-                auto plan = cd->plan(present.data());
-                if (!plan) return RSG_ERR_TOO_FEW_SHARDS;
-                // survivors read in place from the records; base = first survivor
-                const uint8_t* base = d_files[plan->survivors[0]] + s0 * rec + 32;
-                RowSet rs;
-                rs.C = k;
-                for (int sv : plan->survivors)
-                    rs.in_off.push_back((uint64_t)(uintptr_t)(d_files[sv] + s0 * rec + 32) - (uint64_t)(uintptr_t)base);
-                for (int i = 0; i < k; ++i) {
-                    if (present[i]) continue;
-                    rs.coef.resize((size_t)(rs.R + 1) * k);
-                    plan_row(*cd, *plan, i, &rs.coef[(size_t)rs.R * k]);
-                    rs.out_off.push_back((uint64_t)i * shard_len);
-                    ++rs.R;
-                }
-                if ((st = apply_rows(rs, base, out, rec, (uint64_t)k * shard_len, shard_len, cnt,
-                                     rsg::GF_MODE_STORE, nullptr, s)))
-                    return st;
-                // 3. surplus parity must agree with the rebuilt data (erasure.rs:935-973)
-                if (verify_surplus && valid > k) {
-                    RowSet vs;
-                    vs.C = k;
-                    vs.in_off = rs.in_off;
-                    for (int p = k; p < t; ++p) {
-                        if (!present[p]) continue;
-                        if (std::find(plan->survivors.begin(), plan->survivors.end(), p) != plan->survivors.end())
-                            continue;  // a survivor re-derives to itself
-                        vs.coef.resize((size_t)(vs.R + 1) * k);
-                        plan_row(*cd, *plan, p, &vs.coef[(size_t)vs.R * k]);
-                        vs.out_off.push_back((uint64_t)(uintptr_t)(d_files[p] + s0 * rec + 32) -
-                                             (uint64_t)(uintptr_t)base);
-                        ++vs.R;
-                    }
-                    if (vs.R) {
-                        if ((st = apply_rows(vs, base, const_cast<uint8_t*>(base), rec, rec, shard_len, cnt,
-                                             rsg::GF_MODE_COMPARE, d_ok + s0, s)))
-                            return st;
-                        any_verify = true;
-                    }
-                }
-            }
+        const int run_status = valid < k ? RSG_ERR_TOO_FEW_SHARDS : RSG_OK;
+        for (uint64_t x = s0; x < s1; ++x) h_status[x] = run_status;
+        if (run_status != RSG_OK) return RSG_OK;
+        uint8_t* out = d_out + s0 * (uint64_t)k * shard_len;
+        for (int i = 0; i < k; ++i)  // present data shards: strided copy out of the records
+            if (present[i] && (e = hip_status(hipMemcpy2DAsync(out + i * shard_len, (size_t)k * shard_len,
+                                                               d_files[i] + s0 * rec + 32, rec, shard_len, cnt,
+                                                               hipMemcpyDeviceToDevice, s))))
+                return e;
+        if (!missing_data) return RSG_OK;
+        auto plan = cd->plan(present.data());
+        if (!plan) return RSG_ERR_TOO_FEW_SHARDS;
+        // survivors read in place from the records; base = first survivor
+        const uint8_t* base = d_files[plan->survivors[0]] + s0 * rec + 32;
+        RowSet rs;
+        rs.C = k;
+        for (int sv : plan->survivors)
+            rs.in_off.push_back((uint64_t)(uintptr_t)(d_files[sv] + s0 * rec + 32) - (uint64_t)(uintptr_t)base);
+        for (int i = 0; i < k; ++i) {
+            if (present[i]) continue;
+            rs.coef.resize((size_t)(rs.R + 1) * k);
+            plan_row(*cd, *plan, i, &rs.coef[(size_t)rs.R * k]);
+            rs.out_off.push_back((uint64_t)i * shard_len);
+            ++rs.R;
         }
-        for (size_t x = s0; x < s1; ++x) h_status[x] = run_status;
-        s0 = s1;
+        if ((e = apply_rows(rs, base, out, rec, (uint64_t)k * shard_len, shard_len, cnt, rsg::GF_MODE_STORE,
+                            nullptr, s)))
+            return e;
+        // 3. surplus parity must agree with the rebuilt data (erasure.rs:935-973)
+        if (!verify_surplus || valid <= k) return RSG_OK;
+        RowSet vs;
+        vs.C = k;
+        vs.in_off = rs.in_off;
+        for (int p = k; p < t; ++p) {
+            if (!present[p]) continue;
+            if (std::find(plan->survivors.begin(), plan->survivors.end(), p) != plan->survivors.end())
+                continue;  // a survivor re-derives to itself
+            vs.coef.resize((size_t)(vs.R + 1) * k);
+            plan_row(*cd, *plan, p, &vs.coef[(size_t)vs.R * k]);
+            vs.out_off.push_back((uint64_t)(uintptr_t)(d_files[p] + s0 * rec + 32) - (uint64_t)(uintptr_t)base);
+            ++vs.R;
+        }
+        if (!vs.R) return RSG_OK;
+        any_verify = true;
+        return apply_rows(vs, base, const_cast<uint8_t*>(base), rec, rec, shard_len, cnt, rsg::GF_MODE_COMPARE,
+                          d_ok + s0, s);
+    });
+    if (st) return st;
+    if (any_verify) {
+        std::vector<uint8_t> ok(n, 1);
+        if ((st = hip_status(hipMemcpyAsync(ok.data(), d_ok, n, hipMemcpyDeviceToHost, s)))) return st;
+        if ((st = hip_status(hipStreamSynchronize(s)))) return st;
+        for (uint64_t x = 0; x < n; ++x)
+            if (h_status[x] == RSG_OK && !ok[x]) h_status[x] = RSG_ERR_INCONSISTENT_SOURCES;
+    }
+    return hip_status(hipStreamSynchronize(s));
+}
+
+}  // namespace
+
+extern "C" {
+
+int rsg_decode_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n, const uint8_t* const* d_files,
+                           int algo, int verify_surplus, uint8_t* d_out, int* h_status, void* stream) {
+    int st = enter(ctx);
+    if (st) return st;
+    if ((st = check_geometry(k, m))) return st;
+    if (!d_files || (n && (!d_out || !h_status))) return RSG_ERR_INVALID_ARG;
+    const uint64_t* key = hash_key(algo);
+    if (!key) return RSG_ERR_INVALID_ARG;
+    if (n == 0 || shard_len == 0) {
+        for (size_t s = 0; s < n; ++s) h_status[s] = RSG_OK;
+        return RSG_OK;
+    }
+    hipStream_t s = pick_stream(ctx, stream);
+    std::lock_guard<std::mutex> g(ctx->mu);
+    std::vector<uint8_t> flags;
+    return decode_records_locked(ctx, k, m, shard_len, n, d_files, key, verify_surplus != 0, d_out, h_status, flags,
+                                 s);
+}
+
+// Heal (Erasure::heal, heal.rs:112-206) over n stripes of bitrot records.
+int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n, const uint8_t* const* d_files,
+                         uint8_t* const* d_targets, int algo, uint8_t* d_work, int* h_status, void* stream) {
+    int st = enter(ctx);
+    if (st) return st;
+    if ((st = check_geometry(k, m))) return st;
+    if (m == 0) return RSG_ERR_ZERO_PARITY_SHARDS;
+    if (!d_files || !d_targets || (n && (!d_work || !h_status))) return RSG_ERR_INVALID_ARG;
+    const uint64_t* key = hash_key(algo);
+    if (!key) return RSG_ERR_INVALID_ARG;
+    if (n == 0 || shard_len == 0) {
+        for (size_t x = 0; x < n; ++x) h_status[x] = RSG_OK;
+        return RSG_OK;
+    }
+    const int t = k + m;
+    const uint64_t rec = 32 + shard_len, ks = (uint64_t)k * shard_len;
+    hipStream_t s = pick_stream(ctx, stream);
+    std::lock_guard<std::mutex> g(ctx->mu);
+    // 1. verified sources -> full data of every stripe (read quorum: k verified shards)
+    std::vector<uint8_t> flags;
+    if ((st = decode_records_locked(ctx, k, m, shard_len, n, d_files, key, false, d_work, h_status, flags, s)))
+        return st;
+    auto cd = get_codec(k, m);
+    if (!cd) return RSG_ERR_INVALID_ARG;
+    // 2. every verified source parity must equal the parity re-encoded from the
+    //    (rebuilt) data: "inconsistent heal source shards" (heal.rs:180-196)
+    uint8_t* d_ok = ctx->d_scratch + (size_t)t * n;
+    if ((st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
+    bool any_verify = false;
+    st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) -> int {
+        if (h_status[s0] != RSG_OK) return RSG_OK;
+        RowSet vs;
+        vs.C = k;
+        for (int c = 0; c < k; ++c) vs.in_off.push_back((uint64_t)c * shard_len);
+        const uint8_t* base = d_work + s0 * ks;
+        for (int p = k; p < t; ++p) {
+            if (!present[p]) continue;
+            vs.coef.insert(vs.coef.end(), cd->matrix.begin() + (size_t)p * k, cd->matrix.begin() + (size_t)(p + 1) * k);
+            vs.out_off.push_back((uint64_t)(uintptr_t)(d_files[p] + s0 * rec + 32) - (uint64_t)(uintptr_t)base);
+            ++vs.R;
+        }
+        if (!vs.R) return RSG_OK;
+        any_verify = true;
+        return apply_rows(vs, base, const_cast<uint8_t*>(base), ks, rec, shard_len, s1 - s0, rsg::GF_MODE_COMPARE,
+                          d_ok + s0, s);
+    });
+    if (st) return st;
+    // 3. targets: [HH256S][shard] records of the rebuilt shards (BitrotWriter::write)
+    RowSet ps;
+    ps.C = k;
+    for (int c = 0; c < k; ++c) ps.in_off.push_back((uint64_t)c * shard_len);
+    for (int i = 0; i < t; ++i) {
+        if (!d_targets[i]) continue;
+        if (i < k) {
+            if ((st = hip_status(hipMemcpy2DAsync(d_targets[i] + 32, rec, d_work + (uint64_t)i * shard_len, ks,
+                                                  shard_len, n, hipMemcpyDeviceToDevice, s))))
+                return st;
+        } else {
+            ps.coef.insert(ps.coef.end(), cd->matrix.begin() + (size_t)i * k, cd->matrix.begin() + (size_t)(i + 1) * k);
+            ps.out_off.push_back((uint64_t)(uintptr_t)(d_targets[i] + 32) - (uint64_t)(uintptr_t)d_work);
+            ++ps.R;
+        }
+    }
+    if ((st = apply_rows(ps, d_work, d_work, ks, rec, shard_len, n, rsg::GF_MODE_STORE, nullptr, s))) return st;
+    for (int i = 0; i < t; ++i) {
+        if (!d_targets[i]) continue;
+        rsg::HashParams h;
+        std::memset(&h, 0, sizeof(h));
+        h.data = d_targets[i] + 32;
+        h.len = shard_len;
+        h.n = n;
+        h.shards = 1;
+        h.stripe_stride = rec;
+        std::memcpy(h.key, key, sizeof(h.key));
+        h.out = d_targets[i];
+        h.out_stride = rec;
+        if ((st = hip_status(rsg::launch_hh256(h, s)))) return st;
     }
     if (any_verify) {
         std::vector<uint8_t> ok(n, 1);
         if ((st = hip_status(hipMemcpyAsync(ok.data(), d_ok, n, hipMemcpyDeviceToHost, s)))) return st;
         if ((st = hip_status(hipStreamSynchronize(s)))) return st;
-        for (size_t x = 0; x < n; ++x)
+        for (uint64_t x = 0; x < n; ++x)
             if (h_status[x] == RSG_OK && !ok[x]) h_status[x] = RSG_ERR_INCONSISTENT_SOURCES;
     }
     return hip_status(hipStreamSynchronize(s));
+}
+
+// Whole-shard-file verification (bitrot_verify, bitrot.rs:616-655) of n files.
+int rsg_bitrot_verify_dev(rsg_ctx* ctx, int algo, size_t n_files, const uint8_t* const* d_files,
+                          const size_t* file_lens, size_t want_size, size_t part_size, size_t shard_size,
+                          int* h_status, void* stream) {
+    int st = enter(ctx);
+    if (st) return st;
+    if (n_files && (!d_files || !file_lens || !h_status)) return RSG_ERR_INVALID_ARG;
+    const bool streaming = algo == RSG_HASH_HIGHWAY256S || algo == RSG_HASH_HIGHWAY256S_LEGACY;
+    if (!streaming && algo != RSG_HASH_NONE) return RSG_ERR_UNSUPPORTED;
+    if (shard_size == 0 && part_size > 0) return RSG_ERR_INVALID_ARG;
+    const uint64_t hs = streaming ? 32 : 0;
+    // bitrot_shard_file_size (bitrot.rs:593-601)
+    const uint64_t expect =
+        (streaming && part_size) ? (part_size + shard_size - 1) / shard_size * hs + part_size : part_size;
+    if (want_size != expect) {
+        for (size_t f = 0; f < n_files; ++f) h_status[f] = RSG_ERR_FILE_SIZE_MISMATCH;
+        return RSG_OK;
+    }
+    const uint64_t* key = streaming ? hash_key(algo) : nullptr;
+    const uint64_t full = part_size ? part_size / shard_size : 0, tail = part_size - full * shard_size;
+    const uint64_t recs = full + (tail ? 1 : 0);  // records in a complete file
+    const uint64_t rec = hs + shard_size;
+    hipStream_t s = pick_stream(ctx, stream);
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (streaming && recs && (st = ctx->ensure_scratch((size_t)recs * n_files))) return st;
+    // records wholly inside each file are verified on the GPU (flags per record)
+    std::vector<uint64_t> avail(n_files, 0);
+    for (size_t f = 0; f < n_files; ++f) {
+        if (!d_files[f] && file_lens[f]) return RSG_ERR_INVALID_ARG;
+        const uint64_t len = std::min<uint64_t>(file_lens[f], want_size);
+        uint64_t a = std::min<uint64_t>(len / rec, full);
+        if (a == full && tail && len - full * rec >= hs + tail) a = recs;
+        avail[f] = a;
+        if (!streaming || !a) continue;
+        uint8_t* flags = ctx->d_scratch + (size_t)f * recs;
+        if ((st = hip_status(hipMemsetAsync(flags, 1, a, s)))) return st;
+        rsg::HashParams h;
+        std::memset(&h, 0, sizeof(h));
+        std::memcpy(h.key, key, sizeof(h.key));
+        h.shards = 1;
+        h.stripe_stride = rec;
+        h.expect_stride = rec;
+        const uint64_t nf = std::min(a, full);
+        if (nf) {
+            h.data = d_files[f] + hs;
+            h.len = shard_size;
+            h.n = nf;
+            h.expect = d_files[f];
+            h.flags = flags;
+            if ((st = hip_status(rsg::launch_hh256(h, s)))) return st;
+        }
+        if (a > full) {  // short last record
+            h.data = d_files[f] + full * rec + hs;
+            h.len = tail;
+            h.n = 1;
+            h.expect = d_files[f] + full * rec;
+            h.flags = flags + full;
+            if ((st = hip_status(rsg::launch_hh256(h, s)))) return st;
+        }
+    }
+    std::vector<uint8_t> flags(streaming ? (size_t)recs * n_files : 0);
+    if (!flags.empty() &&
+        (st = hip_status(hipMemcpyAsync(flags.data(), ctx->d_scratch, flags.size(), hipMemcpyDeviceToHost, s))))
+        return st;
+    if ((st = hip_status(hipStreamSynchronize(s)))) return st;
+    // the reference reads records in order: the first bad or missing one decides
+    for (size_t f = 0; f < n_files; ++f) {
+        int res = RSG_OK;
+        for (uint64_t r = 0; r < avail[f] && streaming; ++r)
+            if (!flags[(size_t)f * recs + r]) {
+                res = RSG_ERR_BITROT_MISMATCH;
+                break;
+            }
+        if (res == RSG_OK && file_lens[f] < want_size) res = RSG_ERR_UNEXPECTED_EOF;
+        if (res == RSG_OK && file_lens[f] > want_size) res = RSG_ERR_TRAILING_DATA;
+        h_status[f] = res;
+    }
+    return RSG_OK;
 }
 
 // ---- host-buffer API ----

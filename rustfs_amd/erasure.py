@@ -327,6 +327,40 @@ class Erasure:
             1 if verify_surplus else 0, out.data_ptr(), status, s), "RustFS codec reconstruct failed")
         return out, [int(status[i]) for i in range(n)]
 
+    def heal_records_batch(self, files: Sequence, targets: Sequence, shard_len: int, n: int,
+                           algo: int = _lib.RSG_HASH_HIGHWAY256S, work=None, stream=None):
+        """Batched heal (rsg_heal_records_dev; Erasure::heal, heal.rs:112-206).
+
+        `files[i]`: cuda uint8 tensor with shard i's n BitrotWriter records, or
+        None (no reader).  `targets[i]`: cuda uint8 tensor of n*(32+shard_len)
+        bytes that receives the rebuilt records of shard i, or None (no
+        writer).  Returns the per-stripe status list (RSG_OK,
+        RSG_ERR_TOO_FEW_SHARDS = read quorum, RSG_ERR_INCONSISTENT_SOURCES)."""
+        import torch
+        t = self.total_shard_count()
+        if len(files) != t or len(targets) != t:
+            raise RsgError(_lib.RSG_ERR_INVALID_SHARD_COUNT,
+                           f"invalid shard count: got {len(files)}/{len(targets)}, expected {t}")
+        rec = 32 + shard_len
+        dev = None
+        for f in list(files) + list(targets):
+            if f is not None:
+                if f.dtype != torch.uint8 or not f.is_cuda or not f.is_contiguous() or f.numel() < n * rec:
+                    raise TypeError("files/targets must be contiguous cuda uint8 tensors of n records")
+                dev = f.device
+        if dev is None:
+            raise RsgError(_lib.RSG_ERR_INVALID_ARG, "invalid argument")
+        if work is None:
+            work = torch.empty((n, self.data_shards * shard_len), dtype=torch.uint8, device=dev)
+        src = (ctypes.c_void_p * t)(*[f.data_ptr() if f is not None else None for f in files])
+        dst = (ctypes.c_void_p * t)(*[f.data_ptr() if f is not None else None for f in targets])
+        status = (ctypes.c_int * max(n, 1))()
+        s = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+        check(_lib.load().rsg_heal_records_dev(
+            _lib.context(dev.index or 0).handle, self.data_shards, self.parity_shards, shard_len, n, src, dst,
+            algo, work.data_ptr(), status, s), "erasure heal")
+        return [int(status[i]) for i in range(n)]
+
     def reconstruct_batch(self, stripes, present: Sequence[bool], mode: int = _lib.RSG_RECONSTRUCT_MISSING,
                           stream=None) -> None:
         n, t, S = _check_batch(stripes, self.total_shard_count())
