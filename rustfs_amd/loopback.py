@@ -15,7 +15,13 @@ what exercises the codec path:
   (split_and_verify, bitrot.rs:227-247; a mismatching record marks that shard
   missing for the block), reconstruct missing data shards
   (decode_data_with_reconstruction_verification, erasure.rs:935-973), and
-  return the first `size` bytes.
+  return the first `size` bytes.  Full blocks go through the GPU GET engine
+  (rsg_decode_records_dev).
+* HEAL: rebuild the shard files of replaced disks (Erasure::heal,
+  heal.rs:112-206) — full blocks in one rsg_heal_records_dev call, the tail
+  block through decode_data_and_parity — byte-identical to what PUT wrote.
+* VERIFY: deep-scan every shard file (bitrot_verify, bitrot.rs:616-655) with
+  one rsg_bitrot_verify_dev call.
 
 Shard placement is identity (shard i on disk i); the reference's key-hash
 distribution, xl.meta, quorum and locking are out of scope.
@@ -88,17 +94,17 @@ class LocalErasureSet:
         return meta
 
     # ------------------------------------------------------------------ GET
-    def get_object(self, name: str) -> bytes:
-        meta = None
+    def _meta(self, name: str) -> dict:
         for i in range(self.k + self.m):
             try:
                 with open(os.path.join(self.dirs[i], name, "meta.json")) as f:
-                    meta = json.load(f)
-                break
+                    return json.load(f)
             except OSError:
                 continue
-        if meta is None:
-            raise FileNotFoundError(name)
+        raise FileNotFoundError(name)
+
+    def get_object(self, name: str) -> bytes:
+        meta = self._meta(name)
         e, k, t = self.erasure, self.k, self.k + self.m
         size, bs = meta["size"], meta["block_size"]
         S = e.shard_size()
@@ -173,3 +179,89 @@ class LocalErasureSet:
         if bad:
             _lib.check(bad[0], "erasure decode")
         return data[:, :bs].contiguous().cpu().numpy().tobytes()
+
+    # ----------------------------------------------------------------- HEAL
+    def heal_object(self, name: str, targets: List[int]) -> None:
+        """Rewrite the part files of the disks in `targets` from the others."""
+        import torch
+        meta = self._meta(name)
+        e, k, t = self.erasure, self.k, self.k + self.m
+        size, bs = meta["size"], meta["block_size"]
+        S = e.shard_size()
+        want = bitrot_shard_file_size(e.shard_file_size(size), S, self.algo)
+        raws: List[Optional[bytes]] = []
+        for i in range(t):
+            raw = None
+            if i not in targets:
+                try:
+                    with open(self._path(i, name), "rb") as f:
+                        raw = f.read()
+                except OSError:
+                    raw = None
+                if raw is not None and len(raw) != want:
+                    raw = None
+            raws.append(raw)
+        nfull = size // bs
+        rec = 32 + S
+        out = {i: bytearray() for i in targets}
+        if nfull:
+            src = [torch.frombuffer(bytearray(r[: nfull * rec]), dtype=torch.uint8).to("cuda") if r else None
+                   for r in raws]
+            dst = [torch.empty(nfull * rec, dtype=torch.uint8, device="cuda") if i in targets else None
+                   for i in range(t)]
+            status = e.heal_records_batch(src, dst, S, nfull, algo=self.algo.value)
+            bad = [x for x in status if x != _lib.RSG_OK]
+            if bad:
+                _lib.check(bad[0], f"heal {name}")
+            for i in targets:
+                out[i] += dst[i].cpu().numpy().tobytes()
+        tail = size - nfull * bs
+        if tail:  # the short last block: host path, verify-before-use per record
+            s_blk = calc_shard_size(tail, k)
+            hs = self.algo.size()
+            shards: List[Optional[bytes]] = [None] * t
+            for i, r in enumerate(raws):
+                if r is None:
+                    continue
+                h, body = r[nfull * rec: nfull * rec + hs], r[nfull * rec + hs: nfull * rec + hs + s_blk]
+                if len(body) == s_blk and self.algo.hash_encode(body) == h:
+                    shards[i] = body
+            if sum(x is not None for x in shards) < k:
+                raise _lib.RsgError(_lib.RSG_ERR_TOO_FEW_SHARDS, f"heal {name}: read quorum")
+            source_parity = {i: shards[i] for i in range(k, t) if shards[i] is not None}
+            e.decode_data_and_parity(shards)
+            for i, src_p in source_parity.items():
+                if bytes(shards[i]) != bytes(src_p):
+                    raise _lib.InvalidDataError(_lib.RSG_ERR_INCONSISTENT_SOURCES, f"heal {name}")
+            for i in targets:
+                out[i] += self.algo.hash_encode(bytes(shards[i])) + bytes(shards[i])
+        for i in targets:
+            os.makedirs(os.path.dirname(self._path(i, name)), exist_ok=True)
+            with open(self._path(i, name), "wb") as f:
+                f.write(bytes(out[i]))
+            with open(os.path.join(self.dirs[i], name, "meta.json"), "w") as f:
+                json.dump(meta, f)
+
+    # --------------------------------------------------------------- VERIFY
+    def verify_object(self, name: str) -> List[int]:
+        """Deep scan: rsg_status of every shard file (RSG_OK = healthy)."""
+        import torch
+        from .bitrot import bitrot_verify_batch
+        meta = self._meta(name)
+        e, t = self.erasure, self.k + self.m
+        S = e.shard_size()
+        part = e.shard_file_size(meta["size"])
+        want = bitrot_shard_file_size(part, S, self.algo)
+        files = []
+        for i in range(t):
+            try:
+                with open(self._path(i, name), "rb") as f:
+                    raw = f.read()
+                files.append(torch.frombuffer(bytearray(raw), dtype=torch.uint8).to("cuda") if raw
+                             else torch.empty(0, dtype=torch.uint8, device="cuda"))
+            except OSError:
+                files.append(None)
+        present = [f for f in files if f is not None]
+        status = bitrot_verify_batch(present, want, part, self.algo, S) if present else []
+        it = iter(status)
+        return [_lib.RSG_ERR_UNEXPECTED_EOF if f is None else next(it) for f in files]
