@@ -31,6 +31,8 @@ struct GfApplyParams {
     uint64_t byte_begin, byte_end;  // byte path column range
 };
 
+constexpr int kMaxHashBases = 32;
+
 struct HashParams {
     const uint8_t* data;
     uint64_t len;            // message length
@@ -41,12 +43,20 @@ struct HashParams {
     uint64_t key[4];
     uint8_t* out;            // digests (may be null in verify mode)
     uint64_t out_stride;     // bytes between digests j and j+1 (0 = 32: packed)
-    uint32_t aligned16;      // every message 16-B aligned: vector loads
     // verify mode (expect != null): compare with the stored digest of message j
     // at expect + j*expect_stride and clear flags[j] on mismatch
     const uint8_t* expect;
     uint64_t expect_stride;
     uint8_t* flags;
+    // multi-file mode (nbases > 0): message j is record r = j % per_base of
+    // file b = j / per_base, at base[b] + r*stripe_stride; its digest (stored
+    // or written) sits at message + digest_off (BitrotWriter records: -32).
+    // One launch then covers every shard file of a set.
+    uint32_t nbases;
+    uint64_t per_base;
+    int64_t digest_off;
+    const uint8_t* base[kMaxHashBases];
+    uint8_t* flag_base[kMaxHashBases];  // verify mode with per-file flag arrays (else flags + j)
 };
 
 hipError_t launch_gf_apply_vec(GfApplyParams p, uint64_t n_stripes, hipStream_t stream);

@@ -195,10 +195,11 @@ __global__ __launch_bounds__(256) void k_gf_apply_byte(const GfApplyParams p) {
 // HighwayHash-256 (public spec; the `highway` crate 1.3.0 behind
 // crates/utils/src/hash.rs:123-127).
 
+// 8-byte little-endian load at any alignment: one global_load_dwordx2 in
+// gfx950's unaligned-access mode (as ld16 below).
 __device__ __forceinline__ uint64_t ld64_any(const uint8_t* p) {
-    uint64_t v = 0;
-#pragma unroll
-    for (int i = 7; i >= 0; --i) v = (v << 8) | p[i];
+    uint64_t v;
+    __builtin_memcpy(&v, p, 8);
     return v;
 }
 
@@ -317,42 +318,45 @@ __device__ __forceinline__ void hhq_finish(HHQuad& s, uint8_t* out, uint32_t q) 
     for (int b = 0; b < 8; ++b) out[8 * q + b] = (uint8_t)(h >> (8 * b));  // any alignment
 }
 
-__device__ __forceinline__ uint64_t ld_u64_aligned(const uint8_t* p) {
-    const uint2 v = *(const uint2*)p;
-    return (uint64_t)v.x | ((uint64_t)v.y << 32);
-}
-
 // Plain / per-shard batch hash: quad j hashes message j (16 messages per wave).
-// Every lane issues its own 8-byte loads; 4 packets are fetched ahead.
+// Every lane issues its own 8-byte loads; 8 packets are fetched ahead.
 __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
     const uint64_t j = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 2;
     const uint32_t q = threadIdx.x & 3u;
     if (j >= p.n) return;  // whole quads exit together
-    const uint64_t stripe = j / p.shards, shard = j - stripe * p.shards;
-    const uint8_t* msg = p.data + stripe * p.stripe_stride + shard * p.shard_pitch;
+    const uint8_t* msg;
+    uint8_t* flag = p.flags ? p.flags + j : nullptr;
+    if (p.nbases) {
+        const uint64_t b = j / p.per_base, r = j - b * p.per_base;
+        msg = p.base[b] + r * p.stripe_stride;
+        if (p.flag_base[b]) flag = p.flag_base[b] + r;
+    } else {
+        const uint64_t stripe = j / p.shards, shard = j - stripe * p.shards;
+        msg = p.data + stripe * p.stripe_stride + shard * p.shard_pitch;
+    }
     HHQuad s;
     hhq_init(s, p.key, q);
     const uint64_t packets = p.len >> 5;
     uint64_t t = 0;
-    if (p.aligned16) {
-        for (; t + 4 <= packets; t += 4) {
-            uint64_t w[4];
+    // 8-byte loads at any alignment (records put data 32 B after the digest,
+    // shards of unaligned length are common); 8 packets fetched ahead
+    for (; t + 8 <= packets; t += 8) {
+        uint64_t w[8];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) w[i] = ld_u64_aligned(msg + (t + i) * 32 + 8 * q);
+        for (int i = 0; i < 8; ++i) w[i] = ld64_any(msg + (t + i) * 32 + 8 * q);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) hhq_update(s, w[i]);
-        }
-        for (; t < packets; ++t) hhq_update(s, ld_u64_aligned(msg + t * 32 + 8 * q));
-    } else {
-        for (; t < packets; ++t) hhq_update(s, ld64_any(msg + t * 32 + 8 * q));
+        for (int i = 0; i < 8; ++i) hhq_update(s, w[i]);
     }
+    for (; t < packets; ++t) hhq_update(s, ld64_any(msg + t * 32 + 8 * q));
     const uint32_t rem = (uint32_t)(p.len & 31);
     if (rem) hhq_remainder(s, msg + packets * 32, rem, q);
-    if (p.expect) {  // verify before use (split_and_verify, bitrot.rs:227-247)
+    if (flag) {  // verify before use (split_and_verify, bitrot.rs:227-247)
+        const uint8_t* want = p.nbases ? msg + p.digest_off : p.expect + j * p.expect_stride;
         const uint64_t h = hhq_digest(s, q);
-        if (h != ld64_any(p.expect + j * p.expect_stride + 8 * q)) p.flags[j] = 0;
+        if (h != ld64_any(want + 8 * q)) *flag = 0;
     } else {
-        hhq_finish(s, p.out + j * (p.out_stride ? p.out_stride : 32u), q);
+        hhq_finish(s, p.nbases ? const_cast<uint8_t*>(msg) + p.digest_off : p.out + j * (p.out_stride ? p.out_stride : 32u),
+                   q);
     }
 }
 

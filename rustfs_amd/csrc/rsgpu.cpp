@@ -348,7 +348,6 @@ int hash_messages(int algo, const uint8_t* d_data, uint64_t len, uint64_t n, uin
     h.stripe_stride = stride;
     std::memcpy(h.key, key, sizeof(h.key));
     h.out = d_out;
-    h.aligned16 = ((uintptr_t)d_data % 16 == 0) && (pitch % 16 == 0) && (stride % 16 == 0);
     return hip_status(rsg::launch_hh256(h, stream));
 }
 
@@ -673,28 +672,62 @@ namespace {
 int verify_records(rsg_ctx* ctx, int t, uint64_t shard_len, uint64_t n, const uint8_t* const* d_files,
                    const uint64_t* key, std::vector<uint8_t>& flags, hipStream_t s) {
     const uint64_t rec = 32 + shard_len;
-    uint8_t* d_flags = ctx->d_scratch;
+    uint8_t* d_flags = ctx->d_scratch;  // compact: [present file][stripe]
+    std::vector<int> avail;
+    for (int i = 0; i < t; ++i)
+        if (d_files[i]) avail.push_back(i);
+    flags.assign((size_t)t * n, 0);
     int st;
-    for (int i = 0; i < t; ++i) {
-        if ((st = hip_status(hipMemsetAsync(d_flags + (size_t)i * n, d_files[i] ? 1 : 0, n, s)))) return st;
-        if (!d_files[i]) continue;
+    if (avail.empty()) return RSG_OK;
+    if ((st = hip_status(hipMemsetAsync(d_flags, 1, avail.size() * n, s)))) return st;
+    // all available shard files in one launch (up to kMaxHashBases per launch)
+    for (size_t g0 = 0; g0 < avail.size(); g0 += rsg::kMaxHashBases) {
+        const size_t g1 = std::min(avail.size(), g0 + (size_t)rsg::kMaxHashBases);
         rsg::HashParams h;
         std::memset(&h, 0, sizeof(h));
-        h.data = d_files[i] + 32;
         h.len = shard_len;
-        h.n = n;
-        h.shards = 1;
+        h.n = (g1 - g0) * n;
         h.stripe_stride = rec;
         std::memcpy(h.key, key, sizeof(h.key));
-        h.aligned16 = false;
-        h.expect = d_files[i];
-        h.expect_stride = rec;
-        h.flags = d_flags + (size_t)i * n;
+        h.flags = d_flags + g0 * n;
+        h.nbases = (uint32_t)(g1 - g0);
+        h.per_base = n;
+        h.digest_off = -32;
+        for (size_t x = g0; x < g1; ++x) h.base[x - g0] = d_files[avail[x]] + 32;
         if ((st = hip_status(rsg::launch_hh256(h, s)))) return st;
     }
-    flags.assign((size_t)t * n, 0);
-    if ((st = hip_status(hipMemcpyAsync(flags.data(), d_flags, flags.size(), hipMemcpyDeviceToHost, s)))) return st;
-    return hip_status(hipStreamSynchronize(s));
+    std::vector<uint8_t> compact(avail.size() * n);
+    if ((st = hip_status(hipMemcpyAsync(compact.data(), d_flags, compact.size(), hipMemcpyDeviceToHost, s))))
+        return st;
+    if ((st = hip_status(hipStreamSynchronize(s)))) return st;
+    for (size_t x = 0; x < avail.size(); ++x)
+        std::memcpy(&flags[(size_t)avail[x] * n], &compact[x * n], n);
+    return RSG_OK;
+}
+
+// Hash `count` record files' n records in place: digest written into each
+// record's 32-byte header (BitrotWriter::write framing).
+int hash_records_inplace(uint8_t* const* files, int count, uint64_t shard_len, uint64_t n, const uint64_t* key,
+                         hipStream_t s) {
+    std::vector<uint8_t*> f;
+    for (int i = 0; i < count; ++i)
+        if (files[i]) f.push_back(files[i]);
+    for (size_t g0 = 0; g0 < f.size(); g0 += rsg::kMaxHashBases) {
+        const size_t g1 = std::min(f.size(), g0 + (size_t)rsg::kMaxHashBases);
+        rsg::HashParams h;
+        std::memset(&h, 0, sizeof(h));
+        h.len = shard_len;
+        h.n = (g1 - g0) * n;
+        h.stripe_stride = 32 + shard_len;
+        std::memcpy(h.key, key, sizeof(h.key));
+        h.nbases = (uint32_t)(g1 - g0);
+        h.per_base = n;
+        h.digest_off = -32;
+        for (size_t x = g0; x < g1; ++x) h.base[x - g0] = f[x] + 32;
+        int st = hip_status(rsg::launch_hh256(h, s));
+        if (st) return st;
+    }
+    return RSG_OK;
 }
 
 // Calls f(s0, s1, present) for each maximal run of stripes sharing one
@@ -885,20 +918,7 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
         }
     }
     if ((st = apply_rows(ps, d_work, d_work, ks, rec, shard_len, n, rsg::GF_MODE_STORE, nullptr, s))) return st;
-    for (int i = 0; i < t; ++i) {
-        if (!d_targets[i]) continue;
-        rsg::HashParams h;
-        std::memset(&h, 0, sizeof(h));
-        h.data = d_targets[i] + 32;
-        h.len = shard_len;
-        h.n = n;
-        h.shards = 1;
-        h.stripe_stride = rec;
-        std::memcpy(h.key, key, sizeof(h.key));
-        h.out = d_targets[i];
-        h.out_stride = rec;
-        if ((st = hip_status(rsg::launch_hh256(h, s)))) return st;
-    }
+    if ((st = hash_records_inplace(d_targets, t, shard_len, n, key, s))) return st;
     if (any_verify) {
         std::vector<uint8_t> ok(n, 1);
         if ((st = hip_status(hipMemcpyAsync(ok.data(), d_ok, n, hipMemcpyDeviceToHost, s)))) return st;
@@ -934,8 +954,11 @@ int rsg_bitrot_verify_dev(rsg_ctx* ctx, int algo, size_t n_files, const uint8_t*
     hipStream_t s = pick_stream(ctx, stream);
     std::lock_guard<std::mutex> g(ctx->mu);
     if (streaming && recs && (st = ctx->ensure_scratch((size_t)recs * n_files))) return st;
-    // records wholly inside each file are verified on the GPU (flags per record)
+    // records wholly inside each file are verified on the GPU (flags per
+    // record, [file][record]); full records of up to kMaxHashBases files per
+    // launch, then the short last records likewise
     std::vector<uint64_t> avail(n_files, 0);
+    std::vector<size_t> bulk_full, bulk_tail;
     for (size_t f = 0; f < n_files; ++f) {
         if (!d_files[f] && file_lens[f]) return RSG_ERR_INVALID_ARG;
         const uint64_t len = std::min<uint64_t>(file_lens[f], want_size);
@@ -943,29 +966,42 @@ int rsg_bitrot_verify_dev(rsg_ctx* ctx, int algo, size_t n_files, const uint8_t*
         if (a == full && tail && len - full * rec >= hs + tail) a = recs;
         avail[f] = a;
         if (!streaming || !a) continue;
-        uint8_t* flags = ctx->d_scratch + (size_t)f * recs;
-        if ((st = hip_status(hipMemsetAsync(flags, 1, a, s)))) return st;
-        rsg::HashParams h;
-        std::memset(&h, 0, sizeof(h));
-        std::memcpy(h.key, key, sizeof(h.key));
-        h.shards = 1;
-        h.stripe_stride = rec;
-        h.expect_stride = rec;
-        const uint64_t nf = std::min(a, full);
-        if (nf) {
-            h.data = d_files[f] + hs;
+        if ((st = hip_status(hipMemsetAsync(ctx->d_scratch + (size_t)f * recs, 1, a, s)))) return st;
+        if (a >= full && full) bulk_full.push_back(f);
+        if (a > full) bulk_tail.push_back(f);
+        if (a < full) {  // a short file: its complete records alone
+            rsg::HashParams h;
+            std::memset(&h, 0, sizeof(h));
+            std::memcpy(h.key, key, sizeof(h.key));
             h.len = shard_size;
-            h.n = nf;
-            h.expect = d_files[f];
-            h.flags = flags;
+            h.n = a;
+            h.stripe_stride = rec;
+            h.nbases = 1;
+            h.per_base = a;
+            h.digest_off = -(int64_t)hs;
+            h.base[0] = d_files[f] + hs;
+            h.flag_base[0] = ctx->d_scratch + (size_t)f * recs;
             if ((st = hip_status(rsg::launch_hh256(h, s)))) return st;
         }
-        if (a > full) {  // short last record
-            h.data = d_files[f] + full * rec + hs;
-            h.len = tail;
-            h.n = 1;
-            h.expect = d_files[f] + full * rec;
-            h.flags = flags + full;
+    }
+    for (int pass = 0; pass < 2; ++pass) {
+        const std::vector<size_t>& list = pass == 0 ? bulk_full : bulk_tail;
+        for (size_t g0 = 0; g0 < list.size(); g0 += rsg::kMaxHashBases) {
+            const size_t g1 = std::min(list.size(), g0 + (size_t)rsg::kMaxHashBases);
+            rsg::HashParams h;
+            std::memset(&h, 0, sizeof(h));
+            std::memcpy(h.key, key, sizeof(h.key));
+            h.len = pass == 0 ? shard_size : tail;
+            h.per_base = pass == 0 ? full : 1;
+            h.n = (g1 - g0) * h.per_base;
+            h.stripe_stride = rec;
+            h.nbases = (uint32_t)(g1 - g0);
+            h.digest_off = -(int64_t)hs;
+            for (size_t x = g0; x < g1; ++x) {
+                const size_t f = list[x];
+                h.base[x - g0] = d_files[f] + (pass == 0 ? 0 : full * rec) + hs;
+                h.flag_base[x - g0] = ctx->d_scratch + (size_t)f * recs + (pass == 0 ? 0 : full);
+            }
             if ((st = hip_status(rsg::launch_hh256(h, s)))) return st;
         }
     }

@@ -66,7 +66,7 @@ int main(int argc, char** argv) {
     memset(&hq, 0, sizeof(hq));
     hq.data = d; hq.len = S; hq.n = n * (K + M); hq.shards = K + M; hq.shard_pitch = S; hq.stripe_stride = STRIDE;
     memcpy(hq.key, key, sizeof(key));
-    hq.out = dig; hq.aligned16 = 1;
+    hq.out = dig;
     GfApplyParams pe = p;
     pe.units = S / 16;
     struct V { const char* name; std::function<void()> f; };
