@@ -57,6 +57,10 @@ struct HashParams {
     int64_t digest_off;
     const uint8_t* base[kMaxHashBases];
     uint8_t* flag_base[kMaxHashBases];  // verify mode with per-file flag arrays (else flags + j)
+    // multi-file mode, optional: copy each message to copy_base[b] + r*copy_stride
+    // while hashing it (GET: verify-before-use and gather in one pass)
+    uint8_t* copy_base[kMaxHashBases];
+    uint64_t copy_stride;
 };
 
 hipError_t launch_gf_apply_vec(GfApplyParams p, uint64_t n_stripes, hipStream_t stream);

@@ -318,18 +318,24 @@ __device__ __forceinline__ void hhq_finish(HHQuad& s, uint8_t* out, uint32_t q) 
     for (int b = 0; b < 8; ++b) out[8 * q + b] = (uint8_t)(h >> (8 * b));  // any alignment
 }
 
+__device__ __forceinline__ void st64_any(uint8_t* p, uint64_t v) { __builtin_memcpy(p, &v, 8); }
+
 // Plain / per-shard batch hash: quad j hashes message j (16 messages per wave).
-// Every lane issues its own 8-byte loads; 8 packets are fetched ahead.
+// Every lane issues its own 8-byte loads; 8 packets are fetched ahead.  COPY:
+// also store the message bytes to copy_base[b] + r*copy_stride (multi-file).
+template <bool COPY>
 __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
     const uint64_t j = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 2;
     const uint32_t q = threadIdx.x & 3u;
     if (j >= p.n) return;  // whole quads exit together
     const uint8_t* msg;
+    uint8_t* dst = nullptr;
     uint8_t* flag = p.flags ? p.flags + j : nullptr;
     if (p.nbases) {
         const uint64_t b = j / p.per_base, r = j - b * p.per_base;
         msg = p.base[b] + r * p.stripe_stride;
         if (p.flag_base[b]) flag = p.flag_base[b] + r;
+        if constexpr (COPY) dst = p.copy_base[b] + r * p.copy_stride;
     } else {
         const uint64_t stripe = j / p.shards, shard = j - stripe * p.shards;
         msg = p.data + stripe * p.stripe_stride + shard * p.shard_pitch;
@@ -346,10 +352,22 @@ __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
         for (int i = 0; i < 8; ++i) w[i] = ld64_any(msg + (t + i) * 32 + 8 * q);
 #pragma unroll
         for (int i = 0; i < 8; ++i) hhq_update(s, w[i]);
+        if constexpr (COPY) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) st64_any(dst + (t + i) * 32 + 8 * q, w[i]);
+        }
     }
-    for (; t < packets; ++t) hhq_update(s, ld64_any(msg + t * 32 + 8 * q));
+    for (; t < packets; ++t) {
+        const uint64_t w = ld64_any(msg + t * 32 + 8 * q);
+        hhq_update(s, w);
+        if constexpr (COPY) st64_any(dst + t * 32 + 8 * q, w);
+    }
     const uint32_t rem = (uint32_t)(p.len & 31);
-    if (rem) hhq_remainder(s, msg + packets * 32, rem, q);
+    if (rem) {
+        hhq_remainder(s, msg + packets * 32, rem, q);
+        if constexpr (COPY)
+            for (uint32_t b = 8 * q; b < rem && b < 8 * q + 8; ++b) dst[packets * 32 + b] = msg[packets * 32 + b];
+    }
     if (flag) {  // verify before use (split_and_verify, bitrot.rs:227-247)
         const uint8_t* want = p.nbases ? msg + p.digest_off : p.expect + j * p.expect_stride;
         const uint64_t h = hhq_digest(s, q);
@@ -619,7 +637,9 @@ hipError_t launch_hh256(const HashParams& p, hipStream_t stream) {
     if (p.n == 0) return hipSuccess;
     const uint64_t blocks = (p.n * 4u + 255u) / 256u;  // one quad per message
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_hh256_quad, dim3((uint32_t)blocks), dim3(256), 0, stream, p);
+    const bool copy = p.nbases && p.copy_base[0];
+    hipLaunchKernelGGL(copy ? k_hh256_quad<true> : k_hh256_quad<false>, dim3((uint32_t)blocks), dim3(256), 0,
+                       stream, p);
     return hipGetLastError();
 }
 

@@ -665,46 +665,6 @@ int rsg_hash_batch_dev(rsg_ctx* ctx, int algo, const uint8_t* d_data, size_t len
 
 namespace {
 
-// Verify-before-use of n BitrotWriter records ([hash][S bytes]) of every
-// available shard file: on return flags[i*n + s] = 1 iff shard i's record s is
-// present and its stored digest matches (split_and_verify, bitrot.rs:227-247).
-// Needs ctx->mu held; uses ctx->d_scratch[0, t*n).
-int verify_records(rsg_ctx* ctx, int t, uint64_t shard_len, uint64_t n, const uint8_t* const* d_files,
-                   const uint64_t* key, std::vector<uint8_t>& flags, hipStream_t s) {
-    const uint64_t rec = 32 + shard_len;
-    uint8_t* d_flags = ctx->d_scratch;  // compact: [present file][stripe]
-    std::vector<int> avail;
-    for (int i = 0; i < t; ++i)
-        if (d_files[i]) avail.push_back(i);
-    flags.assign((size_t)t * n, 0);
-    int st;
-    if (avail.empty()) return RSG_OK;
-    if ((st = hip_status(hipMemsetAsync(d_flags, 1, avail.size() * n, s)))) return st;
-    // all available shard files in one launch (up to kMaxHashBases per launch)
-    for (size_t g0 = 0; g0 < avail.size(); g0 += rsg::kMaxHashBases) {
-        const size_t g1 = std::min(avail.size(), g0 + (size_t)rsg::kMaxHashBases);
-        rsg::HashParams h;
-        std::memset(&h, 0, sizeof(h));
-        h.len = shard_len;
-        h.n = (g1 - g0) * n;
-        h.stripe_stride = rec;
-        std::memcpy(h.key, key, sizeof(h.key));
-        h.flags = d_flags + g0 * n;
-        h.nbases = (uint32_t)(g1 - g0);
-        h.per_base = n;
-        h.digest_off = -32;
-        for (size_t x = g0; x < g1; ++x) h.base[x - g0] = d_files[avail[x]] + 32;
-        if ((st = hip_status(rsg::launch_hh256(h, s)))) return st;
-    }
-    std::vector<uint8_t> compact(avail.size() * n);
-    if ((st = hip_status(hipMemcpyAsync(compact.data(), d_flags, compact.size(), hipMemcpyDeviceToHost, s))))
-        return st;
-    if ((st = hip_status(hipStreamSynchronize(s)))) return st;
-    for (size_t x = 0; x < avail.size(); ++x)
-        std::memcpy(&flags[(size_t)avail[x] * n], &compact[x * n], n);
-    return RSG_OK;
-}
-
 // Hash `count` record files' n records in place: digest written into each
 // record's 32-byte header (BitrotWriter::write framing).
 int hash_records_inplace(uint8_t* const* files, int count, uint64_t shard_len, uint64_t n, const uint64_t* key,
@@ -750,11 +710,85 @@ int for_each_pattern_run(int t, uint64_t n, const std::vector<uint8_t>& flags, F
     return RSG_OK;
 }
 
+// Verify (and optionally gather) records of the shard files listed in `idx`
+// for stripes [lo, hi): flags[i*n + s] in device scratch is set to 1 for a
+// present shard and cleared by the kernel on a digest mismatch.  With d_out,
+// data shard i's record bodies are also copied to d_out + s*k*S + i*S.
+int launch_verify_group(const std::vector<int>& idx, const uint8_t* const* d_files, uint8_t* d_flags, int k,
+                        uint64_t shard_len, uint64_t n, uint64_t lo, uint64_t hi, const uint64_t* key,
+                        uint8_t* d_out, hipStream_t s) {
+    const uint64_t rec = 32 + shard_len;
+    int st;
+    for (int i : idx)
+        if ((st = hip_status(hipMemsetAsync(d_flags + (size_t)i * n + lo, 1, hi - lo, s)))) return st;
+    for (size_t g0 = 0; g0 < idx.size(); g0 += rsg::kMaxHashBases) {
+        const size_t g1 = std::min(idx.size(), g0 + (size_t)rsg::kMaxHashBases);
+        rsg::HashParams h;
+        std::memset(&h, 0, sizeof(h));
+        h.len = shard_len;
+        h.per_base = hi - lo;
+        h.n = (g1 - g0) * h.per_base;
+        h.stripe_stride = rec;
+        std::memcpy(h.key, key, sizeof(h.key));
+        h.nbases = (uint32_t)(g1 - g0);
+        h.digest_off = -32;
+        h.copy_stride = (uint64_t)k * shard_len;
+        for (size_t x = g0; x < g1; ++x) {
+            const int i = idx[x];
+            h.base[x - g0] = d_files[i] + lo * rec + 32;
+            h.flag_base[x - g0] = d_flags + (size_t)i * n + lo;
+            if (d_out) h.copy_base[x - g0] = d_out + lo * h.copy_stride + (uint64_t)i * shard_len;
+        }
+        if ((st = hip_status(rsg::launch_hh256(h, s)))) return st;
+    }
+    return RSG_OK;
+}
+
+// GET-side verify-before-use: the data records are verified and gathered into
+// d_out in one pass; parity records are read only for stripes that need them
+// (a data record missing or rotten), or for all stripes with all_parity (heal).
+// flags (host) returns the verified map [shard][stripe]; an unread parity
+// record counts as absent.  Uses ctx->d_scratch[0, t*n).
+int verify_gather(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64_t n, const uint8_t* const* d_files,
+                  const uint64_t* key, uint8_t* d_out, bool all_parity, std::vector<uint8_t>& flags, hipStream_t s) {
+    const int t = k + m;
+    uint8_t* d_flags = ctx->d_scratch;
+    int st;
+    if ((st = hip_status(hipMemsetAsync(d_flags, 0, (size_t)t * n, s)))) return st;
+    std::vector<int> data_idx, par_idx;
+    for (int i = 0; i < t; ++i)
+        if (d_files[i]) (i < k ? data_idx : par_idx).push_back(i);
+    if ((st = launch_verify_group(data_idx, d_files, d_flags, k, shard_len, n, 0, n, key, d_out, s))) return st;
+    flags.assign((size_t)t * n, 0);
+    if ((st = hip_status(hipMemcpyAsync(flags.data(), d_flags, (size_t)k * n, hipMemcpyDeviceToHost, s)))) return st;
+    if ((st = hip_status(hipStreamSynchronize(s)))) return st;
+    uint64_t lo = n, hi = 0;
+    if (all_parity) {
+        lo = 0;
+        hi = n;
+    } else {
+        for (uint64_t x = 0; x < n; ++x) {
+            bool whole = true;
+            for (int i = 0; i < k && whole; ++i) whole = flags[(size_t)i * n + x] != 0;
+            if (!whole) {
+                lo = std::min(lo, x);
+                hi = x + 1;
+            }
+        }
+    }
+    if (lo >= hi || par_idx.empty()) return RSG_OK;
+    if ((st = launch_verify_group(par_idx, d_files, d_flags, k, shard_len, n, lo, hi, key, nullptr, s))) return st;
+    if ((st = hip_status(hipMemcpyAsync(flags.data() + (size_t)k * n, d_flags + (size_t)k * n, (size_t)m * n,
+                                        hipMemcpyDeviceToHost, s))))
+        return st;
+    return hip_status(hipStreamSynchronize(s));
+}
+
 // GET engine body (ctx->mu held): verify records, copy/rebuild the k data
 // shards of every stripe into d_out (n x k*S), optional surplus-parity check.
 // Uses ctx->d_scratch[0, (t+1)*n).  `flags` returns the verified-shard map.
 int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64_t n, const uint8_t* const* d_files,
-                          const uint64_t* key, bool verify_surplus, uint8_t* d_out, int* h_status,
+                          const uint64_t* key, bool verify_surplus, bool all_parity, uint8_t* d_out, int* h_status,
                           std::vector<uint8_t>& flags, hipStream_t s) {
     const int t = k + m;
     const uint64_t rec = 32 + shard_len;  // BitrotWriter record: [hash][block]
@@ -762,12 +796,12 @@ int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64
     if ((st = ctx->ensure_scratch((size_t)(t + 1) * n))) return st;
     uint8_t* d_ok = ctx->d_scratch + (size_t)t * n;  // surplus-parity verdict per stripe
     if ((st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
-    // 1. verify every available record
-    if ((st = verify_records(ctx, t, shard_len, n, d_files, key, flags, s))) return st;
+    // 1. verify the data records and gather them into d_out; parity where needed
+    if ((st = verify_gather(ctx, k, m, shard_len, n, d_files, key, d_out, all_parity, flags, s))) return st;
     auto cd = m > 0 ? get_codec(k, m) : nullptr;
     if (m > 0 && !cd) return RSG_ERR_INVALID_ARG;
     bool any_verify = false;
-    // 2. per run of stripes with one pattern: copy present data, rebuild the rest
+    // 2. per run of stripes with one pattern: rebuild missing data
     st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) -> int {
         const uint64_t cnt = s1 - s0;
         int valid = 0, missing_data = 0, e;
@@ -776,12 +810,7 @@ int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64
         const int run_status = valid < k ? RSG_ERR_TOO_FEW_SHARDS : RSG_OK;
         for (uint64_t x = s0; x < s1; ++x) h_status[x] = run_status;
         if (run_status != RSG_OK) return RSG_OK;
-        uint8_t* out = d_out + s0 * (uint64_t)k * shard_len;
-        for (int i = 0; i < k; ++i)  // present data shards: strided copy out of the records
-            if (present[i] && (e = hip_status(hipMemcpy2DAsync(out + i * shard_len, (size_t)k * shard_len,
-                                                               d_files[i] + s0 * rec + 32, rec, shard_len, cnt,
-                                                               hipMemcpyDeviceToDevice, s))))
-                return e;
+        uint8_t* out = d_out + s0 * (uint64_t)k * shard_len;  // verified data already gathered here
         if (!missing_data) return RSG_OK;
         auto plan = cd->plan(present.data());
         if (!plan) return RSG_ERR_TOO_FEW_SHARDS;
@@ -850,8 +879,8 @@ int rsg_decode_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t 
     hipStream_t s = pick_stream(ctx, stream);
     std::lock_guard<std::mutex> g(ctx->mu);
     std::vector<uint8_t> flags;
-    return decode_records_locked(ctx, k, m, shard_len, n, d_files, key, verify_surplus != 0, d_out, h_status, flags,
-                                 s);
+    return decode_records_locked(ctx, k, m, shard_len, n, d_files, key, verify_surplus != 0, false, d_out, h_status,
+                                 flags, s);
 }
 
 // Heal (Erasure::heal, heal.rs:112-206) over n stripes of bitrot records.
@@ -874,7 +903,7 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
     std::lock_guard<std::mutex> g(ctx->mu);
     // 1. verified sources -> full data of every stripe (read quorum: k verified shards)
     std::vector<uint8_t> flags;
-    if ((st = decode_records_locked(ctx, k, m, shard_len, n, d_files, key, false, d_work, h_status, flags, s)))
+    if ((st = decode_records_locked(ctx, k, m, shard_len, n, d_files, key, false, true, d_work, h_status, flags, s)))
         return st;
     auto cd = get_codec(k, m);
     if (!cd) return RSG_ERR_INVALID_ARG;

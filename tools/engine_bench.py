@@ -1,8 +1,9 @@
 """Device-resident rates of the §8(f) engines on one GPU, RS(8,4), 1 MiB
 stripes, n = 4096 (6 GiB of BitrotWriter records per call):
 
-* GET engine (rsg_decode_records_dev): verify all records + copy/rebuild data,
-  with 0 and 2 lost data shards (surplus parity verified);
+* GET engine (rsg_decode_records_dev): verify-and-gather the data records
+  (parity read only for degraded stripes), rebuild, surplus-parity check; with
+  0 and 2 lost data shards;
 * heal (rsg_heal_records_dev): one data and one parity disk replaced;
 * whole-file bitrot_verify (rsg_bitrot_verify_dev) of the 12 shard files.
 
@@ -67,7 +68,8 @@ def main():
     ms, (o, status) = timed(lambda: e.decode_records_batch(files, S, n, out=out))
     assert all(x == 0 for x in status) and torch.equal(o, want)
     res["get_all_present"] = {"ms": round(ms * 1e3, 3), "GiB_s_payload": round(payload / ms / GiB, 1),
-                              "hbm_GB_s": round((t * n * rec + 2 * payload) / ms / 1e9, 1)}
+                              # data records read once (verify + gather), data written once
+                              "hbm_GB_s": round((k * n * rec + payload) / ms / 1e9, 1)}
     lost = [files[i] if i not in (0, 3) else None for i in range(t)]
     ms, (o, status) = timed(lambda: e.decode_records_batch(lost, S, n, out=out))
     assert all(x == 0 for x in status) and torch.equal(o, want)
