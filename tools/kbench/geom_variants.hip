@@ -7,6 +7,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <stddef.h>
 
 #include <algorithm>
 #include <functional>
@@ -69,6 +70,159 @@ __global__ __launch_bounds__(256) void k_loop(const GfApplyParams p) {
     gf_store<R>(p, obase, off, acc, stripe);
 }
 
+// Table dwords of coefficient (r, c) loaded where used: an opaque zero offset
+// stops the compiler hoisting all C*R*5 dwords into (spilled) SGPRs.
+// (Read straight from the kernel-argument segment: taking &p.tab of the by-value
+// parameter would copy the whole struct to scratch.)
+__device__ __forceinline__ const uint32_t* tab_at(const GfApplyParams&, int r, int c) {
+    uint32_t z;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+    const uint8_t* ka = (const uint8_t*)__builtin_amdgcn_kernarg_segment_ptr();
+    return (const uint32_t*)(ka + offsetof(GfApplyParams, tab) + ((size_t)(r * kMaxC + c) * 5) * 4 + z);
+}
+
+template <int C0, int CN, int R>
+__device__ __forceinline__ void gf_acc_late(const GfApplyParams& p, const uint4* x, uint32_t (&acc)[R][4]) {
+#pragma unroll
+    for (int i = 0; i < CN; ++i) {
+        const int c = C0 + i;
+        const uint32_t w[4] = {x[i].x, x[i].y, x[i].z, x[i].w};
+        const uint32_t* tb[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) tb[r] = tab_at(p, r, c);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t s0 = w[q] & 0x07070707u;
+            const uint32_t s1 = (w[q] >> 3) & 0x07070707u;
+            const uint32_t s2 = (w[q] >> 6) & 0x03030303u;
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r][q] ^= gf_mul_word(tb[r], s0, s1, s2);
+        }
+    }
+}
+
+// Two halves of a 512-thread block split the inputs (C0 = C/2 each) of the
+// same 16-byte units; the upper half hands its partial sums over LDS.
+template <int C, int R>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_split(const GfApplyParams p) {
+    constexpr int H = C / 2;
+    __shared__ uint32_t part[R * 4][256];
+    const uint32_t half = threadIdx.x >> 8, t = threadIdx.x & 255u;
+    const uint32_t stripe = blockIdx.x / p.chunks_per_stripe;
+    const uint32_t chunk = blockIdx.x - stripe * p.chunks_per_stripe;
+    const uint8_t* sbase = p.base + (uint64_t)stripe * p.stripe_stride;
+    uint8_t* obase = p.out_base + (uint64_t)stripe * p.out_stripe_stride;
+    const uint32_t u = chunk * 256u + t;
+    const bool ok = u < p.units;
+    const uint64_t off = (uint64_t)(ok ? u : 0) * 16u;
+    uint32_t acc[R][4];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
+    uint4 x[H];
+    if (__builtin_amdgcn_readfirstlane(half) == 0) {
+#pragma unroll
+        for (int i = 0; i < H; ++i) x[i] = ld16(sbase + p.in_off[i] + off);
+        gf_acc_late<0, H, R>(p, x, acc);
+    } else {
+#pragma unroll
+        for (int i = 0; i < H; ++i) x[i] = ld16(sbase + p.in_off[H + i] + off);
+        gf_acc_late<H, H, R>(p, x, acc);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) part[r * 4 + q][t] = acc[r][q];
+    }
+    __syncthreads();
+    if (half == 0 && ok) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[r][q] ^= part[r * 4 + q][t];
+        gf_store<R>(p, obase, off, acc, stripe);
+    }
+}
+
+// Compile-time C, 8-byte units (uint2): 32 VGPRs of inputs at C = 16.
+template <int C, int R>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_narrow(const GfApplyParams p) {
+    const uint32_t stripe = blockIdx.x / (p.chunks_per_stripe * 2);
+    const uint32_t chunk = blockIdx.x - stripe * (p.chunks_per_stripe * 2);
+    const uint8_t* sbase = p.base + (uint64_t)stripe * p.stripe_stride;
+    uint8_t* obase = p.out_base + (uint64_t)stripe * p.out_stripe_stride;
+    const uint32_t u = chunk * 256u + threadIdx.x;  // 8-byte unit
+    if (u >= p.units * 2) return;
+    const uint64_t off = (uint64_t)u * 8u;
+    uint2 x[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) x[c] = *(const uint2*)(sbase + p.in_off[c] + off);
+    uint32_t acc[R][2];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = 0u;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const uint32_t w[2] = {x[c].x, x[c].y};
+        const uint32_t* tb[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) tb[r] = tab_at(p, r, c);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t s0 = w[q] & 0x07070707u;
+            const uint32_t s1 = (w[q] >> 3) & 0x07070707u;
+            const uint32_t s2 = (w[q] >> 6) & 0x03030303u;
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r][q] ^= gf_mul_word(tb[r], s0, s1, s2);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) *(uint2*)(obase + p.out_off[r] + off) = make_uint2(acc[r][0], acc[r][1]);
+}
+
+// Compile-time C, rolled groups of G (fully unrolled by the compiler).
+template <int C, int R, int G>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_cloop(const GfApplyParams p) {
+    const uint32_t stripe = blockIdx.x / p.chunks_per_stripe;
+    const uint32_t chunk = blockIdx.x - stripe * p.chunks_per_stripe;
+    const uint8_t* sbase = p.base + (uint64_t)stripe * p.stripe_stride;
+    uint8_t* obase = p.out_base + (uint64_t)stripe * p.out_stripe_stride;
+    const uint32_t u = chunk * 256u + threadIdx.x;
+    if (u >= p.units) return;
+    const uint64_t off = (uint64_t)u * 16u;
+    uint32_t acc[R][4];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
+    uint4 x[G], y[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) x[g] = ld16(sbase + p.in_off[g] + off);
+#pragma unroll
+    for (int c0 = 0; c0 < C; c0 += G) {
+        if (c0 + G < C) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) y[g] = ld16(sbase + p.in_off[c0 + G + g] + off);
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int c = c0 + g;
+            const uint32_t w[4] = {x[g].x, x[g].y, x[g].z, x[g].w};
+            const uint32_t* tb[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) tb[r] = tab_at(p, r, c);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t s0 = w[q] & 0x07070707u;
+                const uint32_t s1 = (w[q] >> 3) & 0x07070707u;
+                const uint32_t s2 = (w[q] >> 6) & 0x03030303u;
+#pragma unroll
+                for (int r = 0; r < R; ++r) acc[r][q] ^= gf_mul_word(tb[r], s0, s1, s2);
+            }
+        }
+        if (c0 + G < C) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) x[g] = y[g];
+        }
+    }
+    gf_store<R>(p, obase, off, acc, stripe);
+}
+
 static uint8_t gmul(uint8_t a, uint8_t b) {
     uint8_t r = 0;
     while (b) { if (b & 1) r ^= a; b >>= 1; a = (a << 1) ^ ((a & 0x80) ? 0x1d : 0); }
@@ -111,6 +265,10 @@ int main(int argc, char** argv) {
         {"loop G=2", [&] { k_loop<MM, 2><<<blocks, 256>>>(p); }},
         {"loop G=4", [&] { k_loop<MM, 4><<<blocks, 256>>>(p); }},
         {"loop G=8", [&] { k_loop<MM, 8><<<blocks, 256>>>(p); }},
+        {"split 512", [&] { k_split<KK, MM><<<blocks, 512>>>(p); }},
+        {"narrow 8B", [&] { k_narrow<KK, MM><<<blocks * 2, 256>>>(p); }},
+        {"cloop G=4", [&] { k_cloop<KK, MM, 4><<<blocks, 256>>>(p); }},
+        {"cloop G=8", [&] { k_cloop<KK, MM, 8><<<blocks, 256>>>(p); }},
     };
     std::vector<uint8_t> ref(MM * S), got(MM * S);
     vs[0].f();
