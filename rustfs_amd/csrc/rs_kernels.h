@@ -13,6 +13,10 @@ enum GfMode : uint32_t {
     GF_MODE_STORE = 0,    // out = M * in
     GF_MODE_XOR = 1,      // out ^= M * in  (continuation of a C > 16 product)
     GF_MODE_COMPARE = 2,  // ok_flags[stripe] = 0 where out != M * in  (verify)
+    // rows r < n_store: STORE at out_base + s*out_stripe_stride + out_off[r];
+    // rows r >= n_store: COMPARE at out_base + s*cmp_stripe_stride + out_off[r]
+    // (GET: rebuild missing data and check surplus parity in one pass)
+    GF_MODE_STORE_COMPARE = 3,
 };
 
 // Passed by value: lands in the kernel-argument segment (SGPR-loaded).
@@ -29,6 +33,8 @@ struct GfApplyParams {
     uint32_t units;              // 16-byte units per shard (vector path)
     uint32_t chunks_per_stripe;  // set by the launcher
     uint64_t byte_begin, byte_end;  // byte path column range
+    uint32_t n_store;               // GF_MODE_STORE_COMPARE split
+    uint64_t cmp_stripe_stride;     // GF_MODE_STORE_COMPARE compare-row stripe stride
 };
 
 constexpr int kMaxHashBases = 32;

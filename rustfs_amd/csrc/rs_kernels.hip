@@ -76,11 +76,16 @@ __device__ __forceinline__ void gf_store(const GfApplyParams& p, uint8_t* obase,
                                          const uint32_t (&acc)[R][4], uint32_t stripe) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
+        uint32_t mode = p.mode;
         uint8_t* dst = obase + p.out_off[r] + off;
+        if (mode == GF_MODE_STORE_COMPARE) {
+            mode = (uint32_t)r < p.n_store ? GF_MODE_STORE : GF_MODE_COMPARE;
+            if (mode == GF_MODE_COMPARE) dst = p.out_base + (uint64_t)stripe * p.cmp_stripe_stride + p.out_off[r] + off;
+        }
         const uint4 v = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
-        if (p.mode == GF_MODE_STORE) {
+        if (mode == GF_MODE_STORE) {
             st16(dst, v);
-        } else if (p.mode == GF_MODE_XOR) {
+        } else if (mode == GF_MODE_XOR) {
             const uint4 o = ld16(dst);
             st16(dst, make_uint4(o.x ^ v.x, o.y ^ v.y, o.z ^ v.z, o.w ^ v.w));
         } else {  // GF_MODE_COMPARE: clear the stripe's ok flag on mismatch
@@ -183,10 +188,15 @@ __global__ __launch_bounds__(256) void k_gf_apply_byte(const GfApplyParams p) {
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
+        uint32_t mode = p.mode;
         uint8_t* dst = obase + p.out_off[r] + b;
+        if (mode == GF_MODE_STORE_COMPARE) {
+            mode = (uint32_t)r < p.n_store ? GF_MODE_STORE : GF_MODE_COMPARE;
+            if (mode == GF_MODE_COMPARE) dst = p.out_base + (uint64_t)stripe * p.cmp_stripe_stride + p.out_off[r] + b;
+        }
         const uint8_t v = (uint8_t)acc[r];
-        if (p.mode == GF_MODE_STORE) *dst = v;
-        else if (p.mode == GF_MODE_XOR) *dst ^= v;
+        if (mode == GF_MODE_STORE) *dst = v;
+        else if (mode == GF_MODE_XOR) *dst ^= v;
         else if (*dst != v) p.ok_flags[stripe] = 0;
     }
 }

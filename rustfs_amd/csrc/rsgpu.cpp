@@ -324,6 +324,34 @@ int apply_rows(const RowSet& rs, const uint8_t* base, uint8_t* out_base, uint64_
     return RSG_OK;
 }
 
+// One pass that stores rows [0, n_store) (at out_base, out_stride) and compares
+// rows [n_store, R) (at out_base + out_off, cmp_stride per stripe) into
+// ok_flags: the GET rebuild and its surplus-parity check read the survivors
+// once.  Needs R <= kMaxR and C <= kMaxC (callers fall back otherwise).
+int apply_store_compare(const RowSet& rs, int n_store, const uint8_t* base, uint8_t* out_base, uint64_t stride,
+                        uint64_t out_stride, uint64_t cmp_stride, uint64_t len, uint64_t n, uint8_t* ok_flags,
+                        hipStream_t stream) {
+    if (rs.R > rsg::kMaxR || rs.C > rsg::kMaxC) return RSG_ERR_UNSUPPORTED;
+    if (rs.R == 0 || n == 0 || len == 0) return RSG_OK;
+    const uint64_t units = len / 16;
+    if (units > 0xffffffffull) return RSG_ERR_UNSUPPORTED;
+    rsg::GfApplyParams p;
+    fill_params(rs, 0, 0, base, out_base, stride, out_stride, rsg::GF_MODE_STORE_COMPARE, ok_flags, p);
+    p.n_store = (uint32_t)n_store;
+    p.cmp_stripe_stride = cmp_stride;
+    int st;
+    if (units) {
+        p.units = (uint32_t)units;
+        if ((st = hip_status(rsg::launch_gf_apply_vec(p, n, stream)))) return st;
+    }
+    if (units * 16 < len) {
+        p.byte_begin = units * 16;
+        p.byte_end = len;
+        if ((st = hip_status(rsg::launch_gf_apply_byte(p, n, stream)))) return st;
+    }
+    return RSG_OK;
+}
+
 const uint64_t kMagicKey[4] = {0xcd8a238efa34e74bull, 0x528596bbe6833e26ull, 0x14449fa35d930f04ull,
                                0xa036de22139de097ull};
 const uint64_t kLegacyKey[4] = {3, 4, 2, 1};
@@ -827,25 +855,36 @@ int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64
             rs.out_off.push_back((uint64_t)i * shard_len);
             ++rs.R;
         }
-        if ((e = apply_rows(rs, base, out, rec, (uint64_t)k * shard_len, shard_len, cnt, rsg::GF_MODE_STORE,
-                            nullptr, s)))
-            return e;
         // 3. surplus parity must agree with the rebuilt data (erasure.rs:935-973)
-        if (!verify_surplus || valid <= k) return RSG_OK;
         RowSet vs;
         vs.C = k;
         vs.in_off = rs.in_off;
-        for (int p = k; p < t; ++p) {
-            if (!present[p]) continue;
-            if (std::find(plan->survivors.begin(), plan->survivors.end(), p) != plan->survivors.end())
-                continue;  // a survivor re-derives to itself
-            vs.coef.resize((size_t)(vs.R + 1) * k);
-            plan_row(*cd, *plan, p, &vs.coef[(size_t)vs.R * k]);
-            vs.out_off.push_back((uint64_t)(uintptr_t)(d_files[p] + s0 * rec + 32) - (uint64_t)(uintptr_t)base);
-            ++vs.R;
+        if (verify_surplus && valid > k) {
+            for (int p = k; p < t; ++p) {
+                if (!present[p]) continue;
+                if (std::find(plan->survivors.begin(), plan->survivors.end(), p) != plan->survivors.end())
+                    continue;  // a survivor re-derives to itself
+                vs.coef.resize((size_t)(vs.R + 1) * k);
+                plan_row(*cd, *plan, p, &vs.coef[(size_t)vs.R * k]);
+                vs.out_off.push_back((uint64_t)(uintptr_t)(d_files[p] + s0 * rec + 32) - (uint64_t)(uintptr_t)base);
+                ++vs.R;
+            }
         }
+        if (vs.R) any_verify = true;
+        if (vs.R && rs.R + vs.R <= rsg::kMaxR && k <= rsg::kMaxC) {
+            // rebuild + check in one pass over the survivors
+            RowSet both = rs;
+            both.coef.insert(both.coef.end(), vs.coef.begin(), vs.coef.end());
+            for (uint64_t o : vs.out_off)  // compare targets relative to `out`
+                both.out_off.push_back(o + (uint64_t)(uintptr_t)base - (uint64_t)(uintptr_t)out);
+            both.R = rs.R + vs.R;
+            return apply_store_compare(both, rs.R, base, out, rec, (uint64_t)k * shard_len, rec, shard_len, cnt,
+                                       d_ok + s0, s);
+        }
+        if ((e = apply_rows(rs, base, out, rec, (uint64_t)k * shard_len, shard_len, cnt, rsg::GF_MODE_STORE,
+                            nullptr, s)))
+            return e;
         if (!vs.R) return RSG_OK;
-        any_verify = true;
         return apply_rows(vs, base, const_cast<uint8_t*>(base), rec, rec, shard_len, cnt, rsg::GF_MODE_COMPARE,
                           d_ok + s0, s);
     });
