@@ -947,45 +947,51 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
     auto cd = get_codec(k, m);
     if (!cd) return RSG_ERR_INVALID_ARG;
     // 2. every verified source parity must equal the parity re-encoded from the
-    //    (rebuilt) data: "inconsistent heal source shards" (heal.rs:180-196)
+    //    (rebuilt) data: "inconsistent heal source shards" (heal.rs:180-196);
+    //    parity targets are encoded in the same pass over the data
     uint8_t* d_ok = ctx->d_scratch + (size_t)t * n;
     if ((st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
     bool any_verify = false;
     st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) -> int {
         if (h_status[s0] != RSG_OK) return RSG_OK;
-        RowSet vs;
-        vs.C = k;
-        for (int c = 0; c < k; ++c) vs.in_off.push_back((uint64_t)c * shard_len);
         const uint8_t* base = d_work + s0 * ks;
+        RowSet ps, vs;  // parity targets (store), verified source parity (compare)
+        ps.C = vs.C = k;
+        for (int c = 0; c < k; ++c) ps.in_off.push_back((uint64_t)c * shard_len);
+        vs.in_off = ps.in_off;
         for (int p = k; p < t; ++p) {
-            if (!present[p]) continue;
-            vs.coef.insert(vs.coef.end(), cd->matrix.begin() + (size_t)p * k, cd->matrix.begin() + (size_t)(p + 1) * k);
-            vs.out_off.push_back((uint64_t)(uintptr_t)(d_files[p] + s0 * rec + 32) - (uint64_t)(uintptr_t)base);
-            ++vs.R;
+            const auto row_b = cd->matrix.begin() + (size_t)p * k, row_e = row_b + k;
+            if (d_targets[p]) {
+                ps.coef.insert(ps.coef.end(), row_b, row_e);
+                ps.out_off.push_back((uint64_t)(uintptr_t)(d_targets[p] + s0 * rec + 32) - (uint64_t)(uintptr_t)base);
+                ++ps.R;
+            }
+            if (present[p]) {
+                vs.coef.insert(vs.coef.end(), row_b, row_e);
+                vs.out_off.push_back((uint64_t)(uintptr_t)(d_files[p] + s0 * rec + 32) - (uint64_t)(uintptr_t)base);
+                ++vs.R;
+            }
         }
-        if (!vs.R) return RSG_OK;
-        any_verify = true;
-        return apply_rows(vs, base, const_cast<uint8_t*>(base), ks, rec, shard_len, s1 - s0, rsg::GF_MODE_COMPARE,
-                          d_ok + s0, s);
+        if (vs.R) any_verify = true;
+        uint8_t* ob = const_cast<uint8_t*>(base);
+        if (ps.R + vs.R <= rsg::kMaxR && k <= rsg::kMaxC) {
+            RowSet both = ps;
+            both.coef.insert(both.coef.end(), vs.coef.begin(), vs.coef.end());
+            both.out_off.insert(both.out_off.end(), vs.out_off.begin(), vs.out_off.end());
+            both.R = ps.R + vs.R;
+            return apply_store_compare(both, ps.R, base, ob, ks, rec, rec, shard_len, s1 - s0, d_ok + s0, s);
+        }
+        int e = apply_rows(ps, base, ob, ks, rec, shard_len, s1 - s0, rsg::GF_MODE_STORE, nullptr, s);
+        if (e || !vs.R) return e;
+        return apply_rows(vs, base, ob, ks, rec, shard_len, s1 - s0, rsg::GF_MODE_COMPARE, d_ok + s0, s);
     });
     if (st) return st;
-    // 3. targets: [HH256S][shard] records of the rebuilt shards (BitrotWriter::write)
-    RowSet ps;
-    ps.C = k;
-    for (int c = 0; c < k; ++c) ps.in_off.push_back((uint64_t)c * shard_len);
-    for (int i = 0; i < t; ++i) {
-        if (!d_targets[i]) continue;
-        if (i < k) {
-            if ((st = hip_status(hipMemcpy2DAsync(d_targets[i] + 32, rec, d_work + (uint64_t)i * shard_len, ks,
-                                                  shard_len, n, hipMemcpyDeviceToDevice, s))))
-                return st;
-        } else {
-            ps.coef.insert(ps.coef.end(), cd->matrix.begin() + (size_t)i * k, cd->matrix.begin() + (size_t)(i + 1) * k);
-            ps.out_off.push_back((uint64_t)(uintptr_t)(d_targets[i] + 32) - (uint64_t)(uintptr_t)d_work);
-            ++ps.R;
-        }
-    }
-    if ((st = apply_rows(ps, d_work, d_work, ks, rec, shard_len, n, rsg::GF_MODE_STORE, nullptr, s))) return st;
+    // 3. data targets: copied out of the gathered/rebuilt data; then every
+    //    target record gets its HH256S header (BitrotWriter::write)
+    for (int i = 0; i < k; ++i)
+        if (d_targets[i] && (st = hip_status(hipMemcpy2DAsync(d_targets[i] + 32, rec, d_work + (uint64_t)i * shard_len,
+                                                                ks, shard_len, n, hipMemcpyDeviceToDevice, s))))
+            return st;
     if ((st = hash_records_inplace(d_targets, t, shard_len, n, key, s))) return st;
     if (any_verify) {
         std::vector<uint8_t> ok(n, 1);
