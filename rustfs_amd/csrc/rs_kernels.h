@@ -81,4 +81,12 @@ bool fused_supported(int C, int R, uint64_t shard_len);
 hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                     hipStream_t stream);
 
+// Ring variant (one stripe per workgroup, E encoder waves, E KiB chunks,
+// double-buffered LDS rows) for batches of few large stripes.  Requires
+// shard_len % (1024*E) == 0, E in {1,2,4}, C <= 16, R <= 4.
+size_t ring_lds_bytes(int C, int R, uint32_t E);
+bool ring_supported(int C, int R, uint64_t shard_len, uint32_t E);
+hipError_t launch_encode_hash_ring(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
+                                   uint32_t E, hipStream_t stream);
+
 }  // namespace rsg

@@ -559,6 +559,164 @@ void k_encode_hash_fused(const GfApplyParams p,
 }
 
 // ---------------------------------------------------------------------------
+// Fused RS encode + HighwayHash-256, ring variant for batches of few large
+// stripes (config 4's 4-16 MiB stripes at 4 GiB per launch: 256-1024 stripes).
+// There the packed kernel above has too few bytes in flight (one 512-B chunk
+// per stripe) and at most n/4 workgroups: it waits on HBM latency, not on the
+// SIMDs.  Here one workgroup owns ONE stripe:
+//   waves 0..E-1 (encoders): each owns a 1 KiB column of every E KiB chunk
+//     (16 B per lane per shard), keeps the loads of the next chunk in flight
+//     (D = 2 register sets, rotated by unrolling, never copied: a copy of a
+//     register with a load pending would wait for it; D = 3 measured no
+//     faster), computes and stores parity, and writes all k+m rows of the
+//     chunk into LDS slot ch & 1;
+//   waves E.. (hashers): one 4-lane quad per shard stream; after the barrier
+//     that publishes slot ch & 1 they hash it while the encoders fill the other.
+// One barrier per chunk (double-buffered rows): the encoders write slot ch & 1
+// only after the barrier that ended the hashers' pass over chunk ch - 2.  Per
+// stripe the hash is sequential (HighwayHash), so the floor is the issue time
+// of the quad's update chain (~19 instructions per 32-byte packet, one wave
+// alone on its SIMD: ~95 cycles); everything else hides under it.  E = 2 for
+// up to ~3 stripes per CU, E = 1 above; E = 4 puts the hasher on a SIMD with
+// an encoder and runs 20 % slower.
+constexpr uint32_t kRingCol = 1024;  // bytes per encoder wave per shard per chunk
+
+constexpr int kRingMaxC = 8;  // C > 8 takes the packed kernel
+
+template <int C, int R, int D = 2>
+__global__ __launch_bounds__(64 * (2 + (C + R + 15) / 16))
+void k_encode_hash_ring(const GfApplyParams p, const HashParams h, const uint32_t E) {
+    extern __shared__ uint8_t lds_all[];
+    constexpr int T = C + R;
+    constexpr uint32_t kTabBytes = C * R * 32;
+    const uint32_t CW = kRingCol * E, pitch = CW + 32, slot = T * pitch;
+    uint8_t* rows = lds_all + kTabBytes;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u, q = lane & 3u;
+    const uint64_t stripe = blockIdx.x;
+    const uint32_t nch = p.units;  // S / CW
+
+    for (uint32_t i = threadIdx.x; i < (uint32_t)(C * R); i += blockDim.x) {
+        const int c = i / R, r = i % R;
+        uint8_t* d = lds_all + i * 32;
+        *(uint4*)d = make_uint4(p.tab[r][c][0], p.tab[r][c][1], p.tab[r][c][2], p.tab[r][c][3]);
+        *(uint32_t*)(d + 16) = p.tab[r][c][4];
+    }
+    __syncthreads();
+
+    if (wave < E) {
+        // ------------------------------ encoder ------------------------------
+        uint8_t* sb = p.out_base + stripe * p.stripe_stride;
+        const uint32_t col = wave * kRingCol + lane * 16u;
+        const uint32_t m7 = vgpr_const(0x07070707u), m3 = vgpr_const(0x03030303u);
+        uint4 b[D][C];
+        auto load = [&](uint4 (&x)[C], uint32_t ch) {
+#pragma unroll
+            for (int c = 0; c < C; ++c) x[c] = ld16(sb + p.in_off[c] + (uint64_t)ch * CW + col);
+        };
+        auto step = [&](uint4 (&x)[C], uint4 (&nxt)[C], uint32_t ch) {
+            if (ch + (D - 1) < nch) load(nxt, ch + (D - 1));
+            uint32_t tz;  // opaque zero: table reads stay at their use
+            asm volatile("s_mov_b32 %0, 0" : "=s"(tz));
+            const uint8_t* tabs = lds_all + tz;
+            uint32_t acc[R][4];
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
+            // tables of input c+1 are read (LDS broadcast) while input c is
+            // multiplied.  Their address carries an opaque zero computed from
+            // the accumulator after input c-1, so the compiler cannot hoist
+            // all C*R tables (160 VGPRs at RS(8,4)) to the top of the chunk.
+            uint4 ta[R], na[R];
+            uint32_t tb[R], nb[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                ta[r] = *(const uint4*)(tabs + r * 32);
+                tb[r] = *(const uint32_t*)(tabs + r * 32 + 16);
+            }
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                if (c + 1 < C) {
+#pragma unroll
+                    for (int r = 0; r < R; ++r)
+                        asm volatile("" : "+v"(acc[r][0]), "+v"(acc[r][1]), "+v"(acc[r][2]), "+v"(acc[r][3]));
+                    // likewise input c+1's field selectors stay after this point
+                    asm volatile("" : "+v"(x[c + 1].x), "+v"(x[c + 1].y), "+v"(x[c + 1].z), "+v"(x[c + 1].w));
+                    uint32_t z;
+                    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+                    const uint8_t* tn = tabs + z + (c + 1) * R * 32;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        na[r] = *(const uint4*)(tn + r * 32);
+                        nb[r] = *(const uint32_t*)(tn + r * 32 + 16);
+                    }
+                }
+                const uint32_t w[4] = {x[c].x, x[c].y, x[c].z, x[c].w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t s0 = w[k] & m7, s1 = (w[k] >> 3) & m7, s2 = (w[k] >> 6) & m3;
+#pragma unroll
+                    for (int r = 0; r < R; ++r)
+                        acc[r][k] ^= __builtin_amdgcn_perm(ta[r].y, ta[r].x, s0) ^
+                                     __builtin_amdgcn_perm(ta[r].w, ta[r].z, s1) ^ __builtin_amdgcn_perm(tb[r], tb[r], s2);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    ta[r] = na[r];
+                    tb[r] = nb[r];
+                }
+            }
+            const uint64_t off = (uint64_t)ch * CW + col;
+#pragma unroll
+            for (int r = 0; r < R; ++r) st16(sb + p.out_off[r] + off, make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]));
+            uint8_t* buf = rows + (ch & 1u) * slot + col;
+#pragma unroll
+            for (int c = 0; c < C; ++c) *(uint4*)(buf + c * pitch) = x[c];
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                *(uint4*)(buf + (C + r) * pitch) = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+            lds_barrier();  // rows of chunk ch published in slot ch & 1
+        };
+#pragma unroll
+        for (int d = 0; d < D - 1; ++d)
+            if ((uint32_t)d < nch) load(b[d], d);
+#pragma unroll 1
+        for (uint32_t ch = 0; ch < nch; ch += D) {
+            step(b[0], b[D - 1], ch);
+            if (ch + 1 >= nch) break;
+            step(b[1], b[0], ch + 1);
+            if constexpr (D == 3) {
+                if (ch + 2 >= nch) break;
+                step(b[2], b[1], ch + 2);
+            }
+        }
+    } else {
+        // ------------------------------ hasher -------------------------------
+        const uint32_t g = (wave - E) * 16u + (lane >> 2);  // shard stream of this quad
+        const bool live = g < (uint32_t)T;
+        const uint32_t roff = (live ? g * pitch : 0) + 8 * q;
+        const uint32_t packets = CW / 32;
+        HHQuad st;
+        hhq_init(st, h.key, q);
+#pragma unroll 1
+        for (uint32_t ch = 0; ch < nch; ++ch) {
+            lds_barrier();
+            if (live) {
+                const uint8_t* row = rows + (ch & 1u) * slot + roff;
+#pragma unroll 1
+                for (uint32_t t = 0; t < packets; t += 8) {
+                    u32x2 v[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) v[i] = *(const u32x2*)(row + (t + i) * 32);
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) hhq_update(st, __builtin_bit_cast(uint64_t, v[i]));
+                }
+            }
+        }
+        if (live) hhq_finish(st, h.out + (stripe * T + g) * 32u, q);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Launchers.
 
 using GfKernel = void (*)(const GfApplyParams);
@@ -716,6 +874,20 @@ hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shar
         const char* e = getenv("RSG_FUSED_SPW1");
         return e && e[0] == '1';
     }();
+    // Few stripes (below ~8 per CU): the ring kernel (one stripe per
+    // workgroup, E KiB chunks, next chunk in flight) beats the packed one
+    // 1.1-3.2x (tools/kbench/ring_variants.hip);
+    // RSG_FUSED_KIND=packed|ring forces one for A/B runs.
+    static const int kind = [] {
+        const char* e = getenv("RSG_FUSED_KIND");
+        return !e ? 0 : (e[0] == 'p' ? 1 : e[0] == 'r' ? 2 : 0);
+    }();
+    if (kind != 1 && (kind == 2 || n_stripes < 2048)) {
+        uint32_t E = n_stripes <= 768 ? 2u : 1u;
+        if (E == 2 && !ring_supported((int)p.C, (int)p.R, shard_len, E)) E = 1;
+        if (ring_supported((int)p.C, (int)p.R, shard_len, E))
+            return launch_encode_hash_ring(p, h, shard_len, n_stripes, E, stream);
+    }
     const FusedPick f = pick_fused((int)p.C, (int)p.R, !unpacked);
     if (!f.k || !fused_supported((int)p.C, (int)p.R, shard_len) || n_stripes == 0 || n_stripes > 0x7fffffffull)
         return hipErrorInvalidValue;
@@ -724,6 +896,60 @@ hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shar
     const size_t lds = (size_t)p.C * p.R * 32 + (size_t)f.spw * (p.C + p.R) * kFusedPitch;
     const uint64_t blocks = (n_stripes + f.spw - 1) / f.spw;
     hipLaunchKernelGGL(f.k, dim3((uint32_t)blocks), dim3(64 * f.waves), lds, stream, p, h);
+    return hipGetLastError();
+}
+
+using RingKernel = void (*)(const GfApplyParams, const HashParams, const uint32_t);
+
+template <int C>
+static RingKernel pick_ring_r(int R) {
+    switch (R) {
+        case 1: return k_encode_hash_ring<C, 1>;
+        case 2: return k_encode_hash_ring<C, 2>;
+        case 3: return k_encode_hash_ring<C, 3>;
+        case 4: return k_encode_hash_ring<C, 4>;
+    }
+    return nullptr;
+}
+
+static RingKernel pick_ring(int C, int R) {
+    switch (C) {
+        case 1: return pick_ring_r<1>(R);
+        case 2: return pick_ring_r<2>(R);
+        case 3: return pick_ring_r<3>(R);
+        case 4: return pick_ring_r<4>(R);
+        case 5: return pick_ring_r<5>(R);
+        case 6: return pick_ring_r<6>(R);
+        case 7: return pick_ring_r<7>(R);
+        case 8: return pick_ring_r<8>(R);
+    }
+    return nullptr;
+}
+
+size_t ring_lds_bytes(int C, int R, uint32_t E) {
+    return (size_t)C * R * 32 + 2ull * (C + R) * (kRingCol * E + 32);
+}
+
+bool ring_supported(int C, int R, uint64_t shard_len, uint32_t E) {
+    return C >= 1 && C <= kRingMaxC && R >= 1 && R <= 4 && (E == 1 || E == 2) &&
+           shard_len >= kRingCol * E && shard_len % (kRingCol * E) == 0 &&
+           shard_len / (kRingCol * E) <= 0xffffffffull && ring_lds_bytes(C, R, E) <= 160 * 1024;
+}
+
+hipError_t launch_encode_hash_ring(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
+                                   uint32_t E, hipStream_t stream) {
+    RingKernel k = pick_ring((int)p.C, (int)p.R);
+    if (!k || !ring_supported((int)p.C, (int)p.R, shard_len, E) || n_stripes == 0 || n_stripes > 0x7fffffffull)
+        return hipErrorInvalidValue;
+    p.units = (uint32_t)(shard_len / (kRingCol * E));
+    h.n = n_stripes;
+    const uint32_t waves = E + (p.C + p.R + 15) / 16;
+    const size_t lds = ring_lds_bytes((int)p.C, (int)p.R, E);
+    if (lds > 64 * 1024) {
+        const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k, dim3((uint32_t)n_stripes), dim3(64 * waves), lds, stream, p, h, E);
     return hipGetLastError();
 }
 

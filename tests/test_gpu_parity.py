@@ -319,3 +319,34 @@ def test_host_batch_pipeline_matches_oracle(gpu, oracle, k, m, S, n, hashed):
         if hashed:
             for i in range(k + m):
                 assert dig[s, i].tobytes() == oracle.hh256s(ref[i]), (s, i)
+
+
+@pytest.mark.parametrize("k,m,S,n", [
+    (8, 4, 2048, 5),     # ring kernel, E = 2 (2 KiB chunks)
+    (8, 4, 3072, 5),     # ring kernel, E = 1 (S not a multiple of 2 KiB)
+    (8, 4, 1024, 1000),  # ring kernel, E = 1 (above ~3 stripes per CU)
+    (4, 2, 8192, 33),    # ring kernel, narrow stripe
+    (1, 1, 4096, 4),     # ring kernel, single data shard
+    (8, 4, 1536, 3),     # packed kernel (S % 1024 != 0)
+    (8, 4, 512, 2048),   # packed kernel (n >= 2048)
+    (12, 4, 4096, 3),    # packed kernel (k > 8)
+])
+def test_fused_kernel_selection_matches_oracle(gpu, oracle, k, m, S, n):
+    """Every fused encode+HH256S kernel the launcher can pick (ring E=1/2,
+    packed) against the oracle; large batches are checked on a sample of
+    stripes that includes the first and last."""
+    import torch
+    from rustfs_amd import Erasure
+    st = _device_batch(torch, n, k, m, S, seed=7 * S + n)
+    dig = torch.zeros((n, k + m, 32), dtype=torch.uint8, device="cuda")
+    Erasure(k, m, k * S).encode_batch(st, dig)
+    torch.cuda.synchronize()
+    host = st.cpu().numpy()
+    hd = dig.cpu().numpy()
+    sample = range(n) if n <= 40 else sorted({0, n - 1, *range(1, n, max(1, n // 37))})
+    for s in sample:
+        ref = host[s].copy()
+        oracle.encode(k, m, ref)
+        assert (host[s] == ref).all(), s
+        for i in range(k + m):
+            assert hd[s, i].tobytes() == oracle.hh256s(ref[i]), (s, i)
