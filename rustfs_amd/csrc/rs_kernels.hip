@@ -37,6 +37,26 @@ __device__ __forceinline__ uint32_t gf_mul_word(const uint32_t* t, uint32_t s0, 
            __builtin_amdgcn_perm(t[4], t[4], s2);
 }
 
+// acc ^= a ^ b ^ c for the three lookups of one word x coefficient, with the
+// gfx950 three-input XOR (v_bitop3_b32, truth table 0x96), which issues at the
+// full v_xor rate (2.3 SIMD cycles per wave64 op, tools/kbench/op_rates.hip).
+// Taking inputs in pairs folds the six lookups into the accumulator with three
+// ops instead of six v_xor: even input: acc = x3(acc, a, b), pend = c; odd
+// input: acc = x3(acc, pend, a), acc = x3(acc, b, c).
+__device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+// odd: input index parity (a compile-time constant in the unrolled loops)
+__device__ __forceinline__ void gf_fold(bool odd, uint32_t& acc, uint32_t& pend, uint32_t a, uint32_t b, uint32_t c) {
+    if (odd) {
+        acc = x3(acc, pend, a);
+        acc = x3(acc, b, c);
+    } else {
+        acc = x3(acc, a, b);
+        pend = c;
+    }
+}
+
 // One 16-byte unit per thread and no loop (126 VGPRs for RS(8,4): 4 waves per
 // SIMD).  A per-thread unit loop pushed it to 130 VGPRs (3 waves per SIMD) and
 // ran ~8 % slower; 2 or 4 units with all loads issued first ran 12-60 % slower
@@ -136,6 +156,7 @@ __global__ __launch_bounds__(256) void k_gf_apply_loop(const GfApplyParams p) {
     uint32_t acc[R][4];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
+    uint32_t pend[R][4];
     uint4 x[G], y[G];
 #pragma unroll
     for (int g = 0; g < G; ++g)
@@ -149,6 +170,7 @@ __global__ __launch_bounds__(256) void k_gf_apply_loop(const GfApplyParams p) {
         for (int g = 0; g < G; ++g) {
             const uint32_t c = c0 + g;
             if (c >= C) break;  // wave-uniform
+            const bool last = c + 1 == C;  // an even last input flushes its third lookup
             const uint32_t w[4] = {x[g].x, x[g].y, x[g].z, x[g].w};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -156,7 +178,14 @@ __global__ __launch_bounds__(256) void k_gf_apply_loop(const GfApplyParams p) {
                 const uint32_t s1 = (w[q] >> 3) & 0x07070707u;
                 const uint32_t s2 = (w[q] >> 6) & 0x03030303u;
 #pragma unroll
-                for (int r = 0; r < R; ++r) acc[r][q] ^= gf_mul_word(p.tab[r][c], s0, s1, s2);
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t* t = p.tab[r][c];
+                    const uint32_t a = __builtin_amdgcn_perm(t[1], t[0], s0), b = __builtin_amdgcn_perm(t[3], t[2], s1),
+                                   d = __builtin_amdgcn_perm(t[4], t[4], s2);
+                    if (g % 2) gf_fold(true, acc[r][q], pend[r][q], a, b, d);
+                    else if (!last) gf_fold(false, acc[r][q], pend[r][q], a, b, d);
+                    else acc[r][q] = x3(acc[r][q], a, b) ^ d;
+                }
             }
         }
 #pragma unroll
@@ -484,9 +513,9 @@ void k_encode_hash_fused(const GfApplyParams p,
             uint32_t tz;
             asm volatile("s_mov_b32 %0, 0" : "=s"(tz));
             const uint8_t* tabs = lds_all + tz;
-            uint32_t acc[R][2];
+            uint32_t acc[R][2], pend[R][2];
 #pragma unroll
-            for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = 0u;
+            for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = pend[r][0] = pend[r][1] = 0u;
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 if constexpr (ABLATE & 1) {
@@ -502,10 +531,17 @@ void k_encode_hash_fused(const GfApplyParams p,
                     const uint8_t* tp = tabs + (c * R + r) * 32;  // wave-uniform: broadcast read
                     const uint4 t4 = *(const uint4*)tp;
                     const uint32_t t2 = *(const uint32_t*)(tp + 16);
-                    acc[r][0] ^= __builtin_amdgcn_perm(t4.y, t4.x, s0a) ^ __builtin_amdgcn_perm(t4.w, t4.z, s1a) ^
-                                 __builtin_amdgcn_perm(t2, t2, s2a);
-                    acc[r][1] ^= __builtin_amdgcn_perm(t4.y, t4.x, s0b) ^ __builtin_amdgcn_perm(t4.w, t4.z, s1b) ^
-                                 __builtin_amdgcn_perm(t2, t2, s2b);
+                    gf_fold(c & 1, acc[r][0], pend[r][0], __builtin_amdgcn_perm(t4.y, t4.x, s0a),
+                            __builtin_amdgcn_perm(t4.w, t4.z, s1a), __builtin_amdgcn_perm(t2, t2, s2a));
+                    gf_fold(c & 1, acc[r][1], pend[r][1], __builtin_amdgcn_perm(t4.y, t4.x, s0b),
+                            __builtin_amdgcn_perm(t4.w, t4.z, s1b), __builtin_amdgcn_perm(t2, t2, s2b));
+                }
+            }
+            if constexpr (C % 2 == 1 && !(ABLATE & 1)) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    acc[r][0] ^= pend[r][0];
+                    acc[r][1] ^= pend[r][1];
                 }
             }
             if (live) {
@@ -618,7 +654,7 @@ void k_encode_hash_ring(const GfApplyParams p, const HashParams h, const uint32_
             uint32_t tz;  // opaque zero: table reads stay at their use
             asm volatile("s_mov_b32 %0, 0" : "=s"(tz));
             const uint8_t* tabs = lds_all + tz;
-            uint32_t acc[R][4];
+            uint32_t acc[R][4], pend[R][4];
 #pragma unroll
             for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
             // tables of input c+1 are read (LDS broadcast) while input c is
@@ -655,8 +691,8 @@ void k_encode_hash_ring(const GfApplyParams p, const HashParams h, const uint32_
                     const uint32_t s0 = w[k] & m7, s1 = (w[k] >> 3) & m7, s2 = (w[k] >> 6) & m3;
 #pragma unroll
                     for (int r = 0; r < R; ++r)
-                        acc[r][k] ^= __builtin_amdgcn_perm(ta[r].y, ta[r].x, s0) ^
-                                     __builtin_amdgcn_perm(ta[r].w, ta[r].z, s1) ^ __builtin_amdgcn_perm(tb[r], tb[r], s2);
+                        gf_fold(c & 1, acc[r][k], pend[r][k], __builtin_amdgcn_perm(ta[r].y, ta[r].x, s0),
+                                __builtin_amdgcn_perm(ta[r].w, ta[r].z, s1), __builtin_amdgcn_perm(tb[r], tb[r], s2));
                 }
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -664,6 +700,12 @@ void k_encode_hash_ring(const GfApplyParams p, const HashParams h, const uint32_
                     ta[r] = na[r];
                     tb[r] = nb[r];
                 }
+            }
+            if constexpr (C % 2 == 1) {
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) acc[r][k] ^= pend[r][k];
             }
             const uint64_t off = (uint64_t)ch * CW + col;
 #pragma unroll

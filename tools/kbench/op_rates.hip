@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s\n", hipGetErrorString(e_)); return 1; } } while (0)
 constexpr int ITERS = 4096;
@@ -37,6 +38,8 @@ __global__ __launch_bounds__(256) void k(uint64_t* out, uint64_t seed) {
             if constexpr (OP == 16) asm volatile("v_lshl_add_u64 %0, %1, 0, %0" : "+v"(a[i]) : "s"(seed));
             if constexpr (OP == 17) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(b[i]) : "s"(seed_s));
             if constexpr (OP == 18) asm volatile("v_perm_b32 %0, %0, %0, %1" : "+v"(b[i]) : "v"(b[(i + 1) & 7]));
+            if constexpr (OP == 19) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(b[i]) : "v"(b[(i + 1) & 7]), "v"(b[(i + 3) & 7]));
+            if constexpr (OP == 20) asm volatile("v_and_b32 %0, %0, %1" : "+v"(b[i]) : "v"(b[(i + 1) & 7]));
         }
     }
     uint64_t r = 0;
@@ -60,20 +63,23 @@ float run(uint64_t* d, int blocks) {
     return ms;
 }
 
-int main() {
-    const int blocks = 256 * 8;  // 8 blocks of 4 waves per CU = 8 waves per SIMD
+int main(int argc, char** argv) {
+    // default 8 blocks of 4 waves per CU = 8 waves per SIMD; argv[1] = waves per SIMD
+    const int wps = argc > 1 ? atoi(argv[1]) : 8;
+    const int blocks = 256 * wps;
     uint64_t* d;
     CK(hipMalloc(&d, (size_t)blocks * 256 * 8));
     const char* names[] = {"v_lshl_add_u64 v,v", "v_mad_u64_u32", "v_perm_b32 v,v,v", "v_xor_b32 v,v", "add_co+addc (2 ops)",
                            "v_mov_b32_dpp", "v_mul_lo_u32", "v_mul_hi_u32", "v_perm_b32 v,v,s", "v_perm_b32 x,x,v",
                            "v_perm_b32 s,s,v", "v_add3_u32 v,v,v", "v_and_or_b32 v,v,s", "v_lshrrev_b32 imm", "v_bfe_u32",
-                           "v_xad_u32 v,v,v", "v_lshl_add_u64 s,v", "v_xor_b32 s,v", "v_perm_b32 v0,v0,v"};
-    float ms[19] = {run<0>(d, blocks), run<1>(d, blocks), run<2>(d, blocks), run<3>(d, blocks), run<4>(d, blocks),
+                           "v_xad_u32 v,v,v", "v_lshl_add_u64 s,v", "v_xor_b32 s,v", "v_perm_b32 v0,v0,v",
+                           "v_bitop3_b32 xor3", "v_and_b32 v,v"};
+    float ms[21] = {run<0>(d, blocks), run<1>(d, blocks), run<2>(d, blocks), run<3>(d, blocks), run<4>(d, blocks),
                     run<5>(d, blocks), run<6>(d, blocks), run<7>(d, blocks), run<8>(d, blocks), run<9>(d, blocks),
                     run<10>(d, blocks), run<11>(d, blocks), run<12>(d, blocks), run<13>(d, blocks), run<14>(d, blocks),
-                    run<15>(d, blocks), run<16>(d, blocks), run<17>(d, blocks), run<18>(d, blocks)};
-    const double waves_per_simd = 8, clk = 2.1e9;
-    for (int i = 0; i < 19; ++i) {
+                    run<15>(d, blocks), run<16>(d, blocks), run<17>(d, blocks), run<18>(d, blocks), run<19>(d, blocks), run<20>(d, blocks)};
+    const double waves_per_simd = wps, clk = 2.1e9;
+    for (int i = 0; i < 21; ++i) {
         const double ops = waves_per_simd * ITERS * 8;  // wave-ops per SIMD
         printf("%-22s %.3f ms  ~%.2f SIMD cycles per wave-op (at %.1f GHz)\n", names[i], ms[i], ms[i] * 1e-3 * clk / ops,
                clk / 1e9);

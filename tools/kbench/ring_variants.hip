@@ -1,5 +1,5 @@
 // ring_variants.hip — fused encode + HH256S for few large stripes: the packed
-// production kernel against the ring kernel at E = 1, 2, 4 encoder waves, plus
+// production kernel against the ring kernel at E = 1, 2 encoder waves (D = 2, 3), plus
 // the unfused pair, RS(8,4), interleaved timing in one process.  Checks every
 // variant's digests and parity against the packed kernel.  Not part of the
 // product.  Usage: ring_variants S n [iters]
@@ -39,9 +39,10 @@ __global__ void k_fill(uint8_t* p, uint64_t n, uint64_t seed) {
     }
 }
 
-// the ring kernel with two register sets (next chunk only in flight)
-static hipError_t ring_d2(GfApplyParams p, HashParams h, uint64_t S, uint64_t n, uint32_t E) {
-    auto k = k_encode_hash_ring<K, M, 2>;
+// the ring kernel with three register sets (next two chunks in flight)
+static hipError_t ring_d3(GfApplyParams p, HashParams h, uint64_t S, uint64_t n, uint32_t E) {
+    if (!ring_supported(K, M, S, E)) return hipErrorInvalidValue;
+    auto k = k_encode_hash_ring<K, M, 3>;
     p.units = (uint32_t)(S / (kRingCol * E));
     h.n = n;
     const size_t lds = ring_lds_bytes(K, M, E);
@@ -90,9 +91,7 @@ int main(int argc, char** argv) {
         {"packed (prod)", [&] { return launch_encode_hash_fused(p, h, S, n, 0); }},
         {"ring E=1", [&] { return launch_encode_hash_ring(p, h, S, n, 1, 0); }},
         {"ring E=2", [&] { return launch_encode_hash_ring(p, h, S, n, 2, 0); }},
-        {"ring E=4", [&] { return launch_encode_hash_ring(p, h, S, n, 4, 0); }},
-        {"ring D=2 E=2", [&] { return ring_d2(p, h, S, n, 2); }},
-        {"ring D=2 E=4", [&] { return ring_d2(p, h, S, n, 4); }},
+        {"ring D=3 E=2", [&] { return ring_d3(p, h, S, n, 2); }},
         {"encode+quad hash", [&] { hipError_t e = launch_gf_apply_vec(pe, n, 0); return e ? e : launch_hh256(hq, 0); }},
         {"encode only", [&] { return launch_gf_apply_vec(pe, n, 0); }},
     };
