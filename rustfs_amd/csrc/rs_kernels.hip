@@ -134,17 +134,18 @@ __global__ __launch_bounds__(256) void k_gf_apply_vec(const GfApplyParams p) {
     gf_store<R>(p, obase, off, acc, stripe);
 }
 
-// Rolled over the inputs in groups of G=4 (any C <= 16, R <= 8): the next
-// group's loads are issued before the current group's arithmetic, and the
-// tables are indexed by the scalar loop counter.  The unrolled kernel above
-// keeps all C inputs and, for C > 8, parks all C*R coefficient tables in
-// VGPRs (~250 VGPRs at C=16, R=4: 2 waves per SIMD); rolled, RS(16,4) needs
-// 95 VGPRs and ran at 68 % of HBM peak against 49 % unrolled
-// (tools/kbench/geom_variants.hip).  For C <= 8, R <= 4 the unrolled kernel is
-// 1-2 % faster and stays the default there.
+// Rolled over the inputs in groups of G=8 (any C <= 16, R <= 8): the next
+// group's 8 loads are issued before the current group's arithmetic, and the
+// tables are indexed by the scalar loop counter (scalar loads, one group's
+// worth in SGPRs).  The unrolled kernel above keeps all C inputs and, for
+// C > 8, parks all C*R coefficient tables in VGPRs (~250 VGPRs at C=16, R=4:
+// 2 waves per SIMD); rolled in groups of 4, RS(16,4) ran at 65-66 % of HBM
+// peak, in groups of 8 (128 B in flight per lane, 105 VGPRs) at 72-73 %
+// (tools/kbench/xor3_variants.hip).  For C <= 8, R <= 4 the unrolled kernel is
+// faster and stays the default there.
 template <int R>
 __global__ __launch_bounds__(256) void k_gf_apply_loop(const GfApplyParams p) {
-    constexpr int G = 4;
+    constexpr int G = 8;
     const uint32_t stripe = blockIdx.x / p.chunks_per_stripe;
     const uint32_t chunk = blockIdx.x - stripe * p.chunks_per_stripe;
     const uint8_t* sbase = p.base + (uint64_t)stripe * p.stripe_stride;
@@ -153,10 +154,11 @@ __global__ __launch_bounds__(256) void k_gf_apply_loop(const GfApplyParams p) {
     if (u >= p.units) return;
     const uint64_t off = (uint64_t)u * 16u;
     const uint32_t C = p.C;
-    uint32_t acc[R][4];
+    uint32_t acc[R][4], pend[R][4];
 #pragma unroll
-    for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
-    uint32_t pend[R][4];
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[r][q] = pend[r][q] = 0u;
     uint4 x[G], y[G];
 #pragma unroll
     for (int g = 0; g < G; ++g)
@@ -170,7 +172,6 @@ __global__ __launch_bounds__(256) void k_gf_apply_loop(const GfApplyParams p) {
         for (int g = 0; g < G; ++g) {
             const uint32_t c = c0 + g;
             if (c >= C) break;  // wave-uniform
-            const bool last = c + 1 == C;  // an even last input flushes its third lookup
             const uint32_t w[4] = {x[g].x, x[g].y, x[g].z, x[g].w};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -180,16 +181,19 @@ __global__ __launch_bounds__(256) void k_gf_apply_loop(const GfApplyParams p) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const uint32_t* t = p.tab[r][c];
-                    const uint32_t a = __builtin_amdgcn_perm(t[1], t[0], s0), b = __builtin_amdgcn_perm(t[3], t[2], s1),
-                                   d = __builtin_amdgcn_perm(t[4], t[4], s2);
-                    if (g % 2) gf_fold(true, acc[r][q], pend[r][q], a, b, d);
-                    else if (!last) gf_fold(false, acc[r][q], pend[r][q], a, b, d);
-                    else acc[r][q] = x3(acc[r][q], a, b) ^ d;
+                    gf_fold(g & 1, acc[r][q], pend[r][q], __builtin_amdgcn_perm(t[1], t[0], s0),
+                            __builtin_amdgcn_perm(t[3], t[2], s1), __builtin_amdgcn_perm(t[4], t[4], s2));
                 }
             }
         }
 #pragma unroll
         for (int g = 0; g < G; ++g) x[g] = y[g];
+    }
+    if (C & 1u) {  // an odd C leaves the last input's third lookup pending
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[r][q] ^= pend[r][q];
     }
     gf_store<R>(p, obase, off, acc, stripe);
 }

@@ -18,10 +18,6 @@
 
 using namespace rsg;
 
-__device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-
 template <int C, int R>
 __global__ __launch_bounds__(256) void k_vec_x3(const GfApplyParams p) {
     const uint32_t stripe = blockIdx.x / p.chunks_per_stripe;
@@ -120,6 +116,99 @@ __global__ __launch_bounds__(256) void k_loop_x3(const GfApplyParams p) {
     gf_store<R>(p, obase, off, acc, stripe);
 }
 
+// RS(16,4) candidates.  V2: groups of 8 inputs in flight (next group's loads
+// issued before the current group's arithmetic), arithmetic in halves of 4 so
+// the tables of one half (80 dwords) fit in SGPRs.
+template <int R>
+__global__ __launch_bounds__(256) void k_loop8(const GfApplyParams p) {
+    const uint32_t stripe = blockIdx.x / p.chunks_per_stripe;
+    const uint32_t chunk = blockIdx.x - stripe * p.chunks_per_stripe;
+    const uint8_t* sbase = p.base + (uint64_t)stripe * p.stripe_stride;
+    uint8_t* obase = p.out_base + (uint64_t)stripe * p.out_stripe_stride;
+    const uint32_t u = chunk * 256u + threadIdx.x;
+    if (u >= p.units) return;
+    const uint64_t off = (uint64_t)u * 16u;
+    const uint32_t C = p.C;  // multiple of 8 here
+    uint32_t acc[R][4], pend[R][4];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
+    uint4 x[8], y[8];
+#pragma unroll
+    for (int g = 0; g < 8; ++g) x[g] = ld16(sbase + p.in_off[g] + off);
+#pragma unroll 1
+    for (uint32_t c0 = 0; c0 < C; c0 += 8) {
+        if (c0 + 8 < C) {
+#pragma unroll
+            for (int g = 0; g < 8; ++g) y[g] = ld16(sbase + p.in_off[c0 + 8 + g] + off);
+        }
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            const uint32_t c = c0 + g;
+            const uint32_t w[4] = {x[g].x, x[g].y, x[g].z, x[g].w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t s0 = w[q] & 0x07070707u, s1 = (w[q] >> 3) & 0x07070707u, s2 = (w[q] >> 6) & 0x03030303u;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t* t = p.tab[r][c];
+                    gf_fold(g & 1, acc[r][q], pend[r][q], __builtin_amdgcn_perm(t[1], t[0], s0),
+                            __builtin_amdgcn_perm(t[3], t[2], s1), __builtin_amdgcn_perm(t[4], t[4], s2));
+                }
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < 8; ++g) x[g] = y[g];
+    }
+    gf_store<R>(p, obase, off, acc, stripe);
+}
+
+// V3: all C inputs loaded up front (unrolled), tables re-read from the
+// kernel-argument segment per input behind an accumulator fence (scalar
+// loads), so they never pile up in VGPRs.
+template <int C, int R>
+__global__ __launch_bounds__(256) void k_unroll_s(const GfApplyParams p) {
+    const uint32_t stripe = blockIdx.x / p.chunks_per_stripe;
+    const uint32_t chunk = blockIdx.x - stripe * p.chunks_per_stripe;
+    const uint8_t* sbase = p.base + (uint64_t)stripe * p.stripe_stride;
+    uint8_t* obase = p.out_base + (uint64_t)stripe * p.out_stripe_stride;
+    const uint32_t u = chunk * 256u + threadIdx.x;
+    if (u >= p.units) return;
+    const uint64_t off = (uint64_t)u * 16u;
+    uint4 x[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) x[c] = ld16(sbase + p.in_off[c] + off);
+    uint32_t acc[R][4], pend[R][4];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            asm volatile("" : "+v"(acc[r][0]), "+v"(acc[r][1]), "+v"(acc[r][2]), "+v"(acc[r][3]));
+        uint32_t z;
+        asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+        const uint32_t* tc = &p.tab[0][c][0] + z;
+        const uint32_t w[4] = {x[c].x, x[c].y, x[c].z, x[c].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t s0 = w[q] & 0x07070707u, s1 = (w[q] >> 3) & 0x07070707u, s2 = (w[q] >> 6) & 0x03030303u;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint32_t* t = tc + r * (kMaxC * 5);
+                gf_fold(c & 1, acc[r][q], pend[r][q], __builtin_amdgcn_perm(t[1], t[0], s0),
+                        __builtin_amdgcn_perm(t[3], t[2], s1), __builtin_amdgcn_perm(t[4], t[4], s2));
+            }
+        }
+    }
+    if (C % 2) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[r][q] ^= pend[r][q];
+    }
+    gf_store<R>(p, obase, off, acc, stripe);
+}
+
 __global__ void k_fill(uint8_t* p, uint64_t n, uint64_t seed) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n / 8; i += (uint64_t)gridDim.x * blockDim.x) {
         uint64_t z = (i + seed) * 0x9E3779B97F4A7C15ull;
@@ -169,6 +258,12 @@ int main(int argc, char** argv) {
         {"RS(8,4) vec xor3", [&] { k_vec_x3<8, 4><<<b84, 256>>>(p84); }, n * 12.0 * 131072, 0},
         {"RS(16,4) loop (prod)", [&] { k_gf_apply_loop<4><<<b164, 256>>>(p164); }, n * 20.0 * 65536, 1},
         {"RS(16,4) loop xor3", [&] { k_loop_x3<4><<<b164, 256>>>(p164); }, n * 20.0 * 65536, 1},
+        {"RS(16,4) loop (prod)", [&] { k_gf_apply_loop<4><<<b164, 256>>>(p164); }, n * 20.0 * 65536, 1},
+        {"RS(16,4) loop8", [&] { k_loop8<4><<<b164, 256>>>(p164); }, n * 20.0 * 65536, 1},
+        {"RS(16,4) loop (prod)", [&] { k_gf_apply_loop<4><<<b164, 256>>>(p164); }, n * 20.0 * 65536, 1},
+        {"RS(16,4) unroll sload", [&] { k_unroll_s<16, 4><<<b164, 256>>>(p164); }, n * 20.0 * 65536, 1},
+        {"RS(8,4) vec (prod)", [&] { k_gf_apply_vec<8, 4><<<b84, 256>>>(p84); }, n * 12.0 * 131072, 0},
+        {"RS(8,4) unroll sload", [&] { k_unroll_s<8, 4><<<b84, 256>>>(p84); }, n * 12.0 * 131072, 0},
     };
     // correctness: each variant's parity against the production kernel of its geometry
     std::vector<uint8_t> ref, got;
@@ -197,6 +292,26 @@ int main(int argc, char** argv) {
             CK(hipEventElapsedTime(&ms, a, b));
             if (it) t[v].push_back(ms);
         }
+    // back-to-back launches (as bench.py times them): 20 in a row, events between
+    for (size_t v : {(size_t)0, (size_t)5}) {
+        std::vector<hipEvent_t> ev(21);
+        for (auto& e : ev) CK(hipEventCreate(&e));
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(ev[0]));
+        for (int i = 0; i < 20; ++i) {
+            vs[v].f();
+            CK(hipEventRecord(ev[i + 1]));
+        }
+        CK(hipEventSynchronize(ev[20]));
+        float tot = 0, mx = 0;
+        for (int i = 0; i < 20; ++i) {
+            float ms;
+            CK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+            tot += ms;
+            mx = std::max(mx, ms);
+        }
+        printf("%-22s back-to-back x20: avg %.4f ms max %.4f\n", vs[v].name, tot / 20, mx);
+    }
     for (size_t v = 0; v < vs.size(); ++v) {
         auto& x = t[v];
         std::sort(x.begin(), x.end());
