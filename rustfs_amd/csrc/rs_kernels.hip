@@ -364,9 +364,14 @@ __device__ __forceinline__ void hhq_finish(HHQuad& s, uint8_t* out, uint32_t q) 
 __device__ __forceinline__ void st64_any(uint8_t* p, uint64_t v) { __builtin_memcpy(p, &v, 8); }
 
 // Plain / per-shard batch hash: quad j hashes message j (16 messages per wave).
-// Every lane issues its own 8-byte loads; 8 packets are fetched ahead.  COPY:
-// also store the message bytes to copy_base[b] + r*copy_stride (multi-file).
-template <bool COPY>
+// Every lane issues its own 8-byte loads.  DEEP = 0: one batch of 8 packets
+// fetched ahead; DEEP = 1: two batches (16 packets, 128 B per lane) in flight,
+// double-buffered: the next batch's loads are issued before the current batch
+// is hashed.  A launch of few messages (the GET engine's 8 data records per
+// stripe: 2 waves per SIMD at 4096 stripes) needs the deeper pipeline to keep
+// enough bytes in flight per CU.  COPY: also store the message bytes to
+// copy_base[b] + r*copy_stride (multi-file).
+template <bool COPY, int DEEP>
 __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
     const uint64_t j = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 2;
     const uint32_t q = threadIdx.x & 3u;
@@ -388,16 +393,41 @@ __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
     const uint64_t packets = p.len >> 5;
     uint64_t t = 0;
     // 8-byte loads at any alignment (records put data 32 B after the digest,
-    // shards of unaligned length are common); 8 packets fetched ahead
-    for (; t + 8 <= packets; t += 8) {
-        uint64_t w[8];
+    // shards of unaligned length are common)
+    auto fetch = [&](uint64_t (&w)[8], uint64_t t0) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) w[i] = ld64_any(msg + (t + i) * 32 + 8 * q);
+        for (int i = 0; i < 8; ++i) w[i] = ld64_any(msg + (t0 + i) * 32 + 8 * q);
+    };
+    auto consume = [&](const uint64_t (&w)[8], uint64_t t0) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) hhq_update(s, w[i]);
         if constexpr (COPY) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) st64_any(dst + (t + i) * 32 + 8 * q, w[i]);
+            for (int i = 0; i < 8; ++i) st64_any(dst + (t0 + i) * 32 + 8 * q, w[i]);
+        }
+    };
+    const uint64_t nb = packets / 8;  // whole 8-packet batches
+    if constexpr (DEEP) {
+        if (nb) {
+            uint64_t wa[8], wb[8];
+            fetch(wa, 0);
+            uint64_t b = 0;
+            for (; b + 2 <= nb; b += 2) {
+                fetch(wb, (b + 1) * 8);
+                consume(wa, b * 8);
+                // clamped, so the loads stay unconditional: past the last
+                // batch this re-reads it (inside the message) and is unused
+                fetch(wa, (b + 2 < nb ? b + 2 : nb - 1) * 8);
+                consume(wb, (b + 1) * 8);
+            }
+            if (b < nb) consume(wa, b * 8);  // odd batch count: wa holds batch nb-1
+            t = nb * 8;
+        }
+    } else {
+        for (; t + 8 <= packets; t += 8) {
+            uint64_t w[8];
+            fetch(w, t);
+            consume(w, t);
         }
     }
     for (; t < packets; ++t) {
@@ -852,8 +882,17 @@ hipError_t launch_hh256(const HashParams& p, hipStream_t stream) {
     const uint64_t blocks = (p.n * 4u + 255u) / 256u;  // one quad per message
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
     const bool copy = p.nbases && p.copy_base[0];
-    hipLaunchKernelGGL(copy ? k_hh256_quad<true> : k_hh256_quad<false>, dim3((uint32_t)blocks), dim3(256), 0,
-                       stream, p);
+    // Two batches in flight per lane (DEEP) unless the launch alone fills the
+    // GPU with waves; RSG_HASH_DEEP=0/1 forces one for A/B runs.
+    static const int force = [] {
+        const char* e = getenv("RSG_HASH_DEEP");
+        return !e ? -1 : (e[0] == '1' ? 1 : 0);
+    }();
+    const bool deep = force >= 0 ? force == 1 : true;
+    using HashKernel = void (*)(const HashParams);
+    const HashKernel k = copy ? (deep ? k_hh256_quad<true, 1> : k_hh256_quad<true, 0>)
+                              : (deep ? k_hh256_quad<false, 1> : k_hh256_quad<false, 0>);
+    hipLaunchKernelGGL(k, dim3((uint32_t)blocks), dim3(256), 0, stream, p);
     return hipGetLastError();
 }
 

@@ -1,0 +1,236 @@
+// fused_deep.hip — production fused encode+hash structure with deeper load
+// pipelining: D register sets (loads issued D-1 chunks ahead), double-buffered
+// LDS rows (one barrier per chunk), ~55 KB LDS per workgroup so two
+// workgroups share a CU and a 4096-stripe batch runs in two even rounds.
+// Not part of the product.  Usage: fused_deep n [iters]
+#include "../../rustfs_amd/csrc/rs_kernels.hip"
+#include "gf_bitslice.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <functional>
+#include <vector>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+using namespace rsg;
+
+constexpr int K = 8, M = 4;
+
+template <int C, int R, int SPW, int D, int WPE>
+__global__ __launch_bounds__(64 * (SPW + (SPW * (C + R) + 15) / 16)) __attribute__((amdgpu_waves_per_eu(WPE)))
+void k_fused_deep(const GfApplyParams p, const HashParams h) {
+    extern __shared__ uint8_t lds_all[];
+    constexpr int T = C + R;
+    constexpr uint32_t kStripeRows = T * kFusedPitch;
+    constexpr uint32_t kBuf = SPW * kStripeRows;
+    constexpr uint32_t kTabBytes = C * R * 32;
+    uint8_t* rows = lds_all + kTabBytes;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u, q = lane & 3u;
+    const uint64_t n = h.n;
+    const uint32_t chunks = p.units;
+    for (uint32_t i = threadIdx.x; i < (uint32_t)(C * R); i += blockDim.x) {
+        const int c = i / R, r = i % R;
+        uint8_t* d = lds_all + i * 32;
+        *(uint4*)d = make_uint4(p.tab[r][c][0], p.tab[r][c][1], p.tab[r][c][2], p.tab[r][c][3]);
+        *(uint32_t*)(d + 16) = p.tab[r][c][4];
+    }
+    __syncthreads();
+    if (wave < (uint32_t)SPW) {
+        const uint64_t stripe = (uint64_t)blockIdx.x * SPW + wave;
+        const bool live = stripe < n;
+        uint8_t* sb = p.out_base + (live ? stripe : 0) * p.stripe_stride;
+        const uint32_t m7 = vgpr_const(0x07070707u), m3 = vgpr_const(0x03030303u);
+        uint2 b[D][C];
+        auto load = [&](uint2 (&x)[C], uint32_t ch) {
+#pragma unroll
+            for (int c = 0; c < C; ++c) x[c] = *(const uint2*)(sb + p.in_off[c] + (uint64_t)ch * kFusedChunk + lane * 8u);
+        };
+        auto step = [&](uint2 (&x)[C], uint32_t ch) {
+            uint32_t tz;
+            asm volatile("s_mov_b32 %0, 0" : "=s"(tz));
+            const uint8_t* tabs = lds_all + tz;
+            uint32_t acc[R][2], pend[R][2];
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = pend[r][0] = pend[r][1] = 0u;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const uint32_t s0a = x[c].x & m7, s0b = x[c].y & m7;
+                const uint32_t s1a = (x[c].x >> 3) & m7, s1b = (x[c].y >> 3) & m7;
+                const uint32_t s2a = (x[c].x >> 6) & m3, s2b = (x[c].y >> 6) & m3;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint8_t* tp = tabs + (c * R + r) * 32;
+                    const uint4 t4 = *(const uint4*)tp;
+                    const uint32_t t2 = *(const uint32_t*)(tp + 16);
+                    gf_fold(c & 1, acc[r][0], pend[r][0], __builtin_amdgcn_perm(t4.y, t4.x, s0a),
+                            __builtin_amdgcn_perm(t4.w, t4.z, s1a), __builtin_amdgcn_perm(t2, t2, s2a));
+                    gf_fold(c & 1, acc[r][1], pend[r][1], __builtin_amdgcn_perm(t4.y, t4.x, s0b),
+                            __builtin_amdgcn_perm(t4.w, t4.z, s1b), __builtin_amdgcn_perm(t2, t2, s2b));
+                }
+            }
+            if constexpr (C % 2 == 1) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    acc[r][0] ^= pend[r][0];
+                    acc[r][1] ^= pend[r][1];
+                }
+            }
+            const uint64_t off = (uint64_t)ch * kFusedChunk + lane * 8u;
+            if (live) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) *(uint2*)(sb + p.out_off[r] + off) = make_uint2(acc[r][0], acc[r][1]);
+            }
+            uint8_t* buf = rows + (ch & 1u) * kBuf + wave * kStripeRows;
+#pragma unroll
+            for (int c = 0; c < C; ++c) *(uint2*)(buf + c * kFusedPitch + lane * 8u) = x[c];
+#pragma unroll
+            for (int r = 0; r < R; ++r) *(uint2*)(buf + (C + r) * kFusedPitch + lane * 8u) = make_uint2(acc[r][0], acc[r][1]);
+            // this set is free again: refill it D chunks ahead (clamped: a
+            // harmless re-read of the last chunk keeps the code straight-line)
+            const uint32_t nx = ch + D < chunks ? ch + D : chunks - 1;
+            load(x, nx);
+            lds_barrier();  // rows of chunk ch published in buffer ch & 1
+        };
+#pragma unroll
+        for (int d = 0; d < D; ++d) load(b[d], d < (int)chunks ? d : chunks - 1);
+#pragma unroll 1
+        for (uint32_t ch = 0; ch < chunks; ch += D) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                if (ch + d >= chunks) break;
+                step(b[d], ch + d);
+            }
+        }
+    } else {
+        const uint32_t g = (wave - SPW) * 16u + (lane >> 2);
+        const uint32_t ls = g / T, shard = g - ls * T;
+        const uint64_t stripe = (uint64_t)blockIdx.x * SPW + ls;
+        const bool live = g < (uint32_t)(SPW * T) && stripe < n;
+        const uint32_t roff = (live ? ls * kStripeRows + shard * kFusedPitch : 0) + 8 * q;
+        HHQuad st;
+        hhq_init(st, h.key, q);
+#pragma unroll 1
+        for (uint32_t ch = 0; ch < chunks; ++ch) {
+            lds_barrier();
+            if (live) {
+                const uint8_t* row = rows + (ch & 1u) * kBuf + roff;
+                u32x2 v[16];
+#pragma unroll
+                for (int t = 0; t < 16; ++t) v[t] = *(const u32x2*)(row + t * 32);
+#pragma unroll
+                for (int t = 0; t < 16; ++t) hhq_update(st, __builtin_bit_cast(uint64_t, v[t]));
+            }
+        }
+        if (live) hhq_finish(st, h.out + (stripe * T + shard) * 32u, q);
+    }
+}
+
+__global__ void k_fill(uint8_t* p, uint64_t n, uint64_t seed) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n / 8; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t z = (i + seed) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        ((uint64_t*)p)[i] = z ^ (z >> 31);
+    }
+}
+
+int main(int argc, char** argv) {
+    const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : 4096;
+    const int iters = argc > 2 ? atoi(argv[2]) : 10;
+    const uint64_t S = 131072, STRIDE = (K + M) * S;
+    uint8_t *d, *dig;
+    CK(hipMalloc(&d, n * STRIDE));
+    CK(hipMalloc(&dig, n * (K + M) * 32));
+    k_fill<<<4096, 256>>>(d, n * STRIDE, 3);
+    constexpr bs::EncodeRows<K, M> E{};
+    GfApplyParams p;
+    memset(&p, 0, sizeof(p));
+    p.base = d; p.out_base = d; p.stripe_stride = STRIDE; p.out_stripe_stride = STRIDE;
+    for (int c = 0; c < K; ++c) p.in_off[c] = c * S;
+    for (int r = 0; r < M; ++r) p.out_off[r] = (K + r) * S;
+    for (int r = 0; r < M; ++r)
+        for (int c = 0; c < K; ++c) {
+            const uint8_t co = E.g[r][c];
+            auto pack = [&](int sh, int f) { uint32_t v = 0; for (int i = 0; i < 4; ++i) v |= (uint32_t)bs::gmul(co, (uint8_t)((f + i) << sh)) << (8 * i); return v; };
+            p.tab[r][c][0] = pack(0, 0); p.tab[r][c][1] = pack(0, 4); p.tab[r][c][2] = pack(3, 0); p.tab[r][c][3] = pack(3, 4); p.tab[r][c][4] = pack(6, 0);
+        }
+    p.C = K; p.R = M; p.mode = GF_MODE_STORE; p.units = S / kFusedChunk;
+    HashParams h;
+    memset(&h, 0, sizeof(h));
+    const uint64_t key[4] = {0xcd8a238efa34e74bull, 0x528596bbe6833e26ull, 0x14449fa35d930f04ull, 0xa036de22139de097ull};
+    memcpy(h.key, key, sizeof(key));
+    h.out = dig;
+    h.n = n;
+    const uint32_t g4 = (uint32_t)((n + 3) / 4);
+    const uint32_t thr = 64 * (4 + (4 * (K + M) + 15) / 16);
+    const size_t lds2 = (size_t)K * M * 32 + 2ull * 4 * (K + M) * kFusedPitch;
+    const size_t lds3 = 3 * 54 * 1024;  // pads LDS so 3 workgroups fit per CU? no: forces 1 (A/B)
+    (void)lds3;
+    auto big = [&](const void* f, size_t lds) { CK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); };
+    big((const void*)k_fused_deep<K, M, 4, 2, 4>, 80 * 1024);
+    big((const void*)k_fused_deep<K, M, 4, 3, 4>, 80 * 1024);
+    big((const void*)k_fused_deep<K, M, 4, 4, 4>, 80 * 1024);
+    big((const void*)k_fused_deep<K, M, 4, 2, 5>, 80 * 1024);
+    GfApplyParams pe = p;
+    pe.units = S / 16;
+    struct V { const char* name; std::function<void()> f; };
+    std::vector<V> vs = {
+        {"fused (prod)", [&] { CK(launch_encode_hash_fused(p, h, S, n, 0)); }},
+        {"D2 w4 52K", [&] { k_fused_deep<K, M, 4, 2, 4><<<g4, thr, lds2>>>(p, h); }},
+        {"D3 w4 52K", [&] { k_fused_deep<K, M, 4, 3, 4><<<g4, thr, lds2>>>(p, h); }},
+        {"D2 w5 52K", [&] { k_fused_deep<K, M, 4, 2, 5><<<g4, thr, lds2>>>(p, h); }},
+        {"D2 w4 56K", [&] { k_fused_deep<K, M, 4, 2, 4><<<g4, thr, 56 * 1024>>>(p, h); }},
+        {"D2 w4 64K", [&] { k_fused_deep<K, M, 4, 2, 4><<<g4, thr, 64 * 1024>>>(p, h); }},
+        {"D2 w4 80K", [&] { k_fused_deep<K, M, 4, 2, 4><<<g4, thr, 80 * 1024>>>(p, h); }},
+        {"D2 spw2 w4", [&] { k_fused_deep<K, M, 2, 2, 4><<<(uint32_t)((n + 1) / 2), 64 * 4, K * M * 32 + 2 * 2 * (K + M) * kFusedPitch>>>(p, h); }},
+        {"D3 spw2 w4", [&] { k_fused_deep<K, M, 2, 3, 4><<<(uint32_t)((n + 1) / 2), 64 * 4, K * M * 32 + 2 * 2 * (K + M) * kFusedPitch>>>(p, h); }},
+        {"fused (prod) again", [&] { CK(launch_encode_hash_fused(p, h, S, n, 0)); }},
+        {"encode only", [&] { CK(launch_gf_apply_vec(pe, n, 0)); }},
+    };
+    {
+        const size_t nd = n * (K + M) * 32;
+        std::vector<uint8_t> ref(nd), got(nd), pref(M * S), pgot(M * S);
+        vs[0].f();
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(ref.data(), dig, nd, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(pref.data(), d + (n - 1) * STRIDE + K * S, M * S, hipMemcpyDeviceToHost));
+        for (size_t v = 1; v + 1 < vs.size(); ++v) {
+            CK(hipMemset(dig, 0, nd));
+            CK(hipMemset(d + (n - 1) * STRIDE + K * S, 0, M * S));
+            vs[v].f();
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(got.data(), dig, nd, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(pgot.data(), d + (n - 1) * STRIDE + K * S, M * S, hipMemcpyDeviceToHost));
+            printf("%s: digests %s, parity %s\n", vs[v].name, memcmp(ref.data(), got.data(), nd) ? "MISMATCH" : "ok",
+                   memcmp(pref.data(), pgot.data(), M * S) ? "MISMATCH" : "ok");
+        }
+        vs[0].f();  // restore parity for the timing runs
+        CK(hipDeviceSynchronize());
+    }
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    std::vector<std::vector<float>> t(vs.size());
+    for (int it = 0; it < iters; ++it)
+        for (size_t v = 0; v < vs.size(); ++v) {
+            CK(hipEventRecord(a));
+            vs[v].f();
+            CK(hipEventRecord(b));
+            CK(hipEventSynchronize(b));
+            float ms;
+            CK(hipEventElapsedTime(&ms, a, b));
+            if (it > 1) t[v].push_back(ms);
+        }
+    const double alg = (double)n * STRIDE;
+    for (size_t v = 0; v < vs.size(); ++v) {
+        auto& x = t[v];
+        std::sort(x.begin(), x.end());
+        printf("%-18s med %.4f ms min %.4f -> %.1f GB/s (%.1f%%)\n", vs[v].name, x[x.size() / 2], x[0],
+               alg / (x[x.size() / 2] * 1e-3) / 1e9, 100 * alg / (x[x.size() / 2] * 1e-3) / 8e12);
+    }
+    return 0;
+}
