@@ -350,3 +350,56 @@ def test_fused_kernel_selection_matches_oracle(gpu, oracle, k, m, S, n):
         assert (host[s] == ref).all(), s
         for i in range(k + m):
             assert hd[s, i].tobytes() == oracle.hh256s(ref[i]), (s, i)
+
+
+@pytest.mark.parametrize("k,m,S", [(200, 56, 67), (128, 128, 48), (255, 1, 33), (1, 255, 40)])
+def test_max_geometry_encode_and_reconstruct(gpu, oracle, k, m, S):
+    """k + m = 256, the reference's cap (erasure.rs:72, 738): encode is chained
+    over launches of <= 16 inputs (GF_MODE_XOR) and <= 8 outputs; reconstruct
+    with every parity budget spent (m missing, data and parity mixed)."""
+    from rustfs_amd import ReedSolomonEncoder
+    rng = np.random.default_rng(k * 7 + m)
+    ref = rand_stripe(rng, k, m, S)
+    oracle.encode(k, m, ref)
+    got = ref.copy()
+    got[k:] = 0x5C
+    enc = ReedSolomonEncoder(k, m)
+    enc.encode([got[i] for i in range(k + m)])
+    assert (got == ref).all()
+    miss = set(rng.choice(k + m, size=m, replace=False).tolist())
+    shards = [None if i in miss else ref[i].tobytes() for i in range(k + m)]
+    enc.reconstruct_opt(shards)
+    for i in range(k + m):
+        assert bytes(shards[i]) == ref[i].tobytes(), i
+
+
+def test_max_geometry_batch_roundtrip(gpu, oracle):
+    """Device batch path at k + m = 256: encode with fused digests off the
+    fused kernels' range (C > 16), erase m shards across data and parity,
+    reconstruct, compare with the oracle stripe by stripe."""
+    import torch
+    from rustfs_amd import Erasure, RSG_RECONSTRUCT_MISSING
+    from oracle import oracle as O
+    k, m, S, n = 192, 64, 96, 3
+    e = Erasure(k, m, k * S)
+    g = torch.Generator(device="cuda:0").manual_seed(77)
+    st = torch.zeros((n, k + m, S), dtype=torch.uint8, device="cuda:0")
+    st[:, :k] = torch.randint(0, 256, (n, k, S), dtype=torch.uint8, device="cuda:0", generator=g)
+    dig = torch.zeros((n, k + m, 32), dtype=torch.uint8, device="cuda:0")
+    e.encode_batch(st, dig)
+    torch.cuda.synchronize()
+    host, hd = st.cpu().numpy(), dig.cpu().numpy()
+    for s in range(n):
+        ref = host[s].copy()
+        O.encode(k, m, ref)
+        assert (ref == host[s]).all()
+        for i in (0, k - 1, k, k + m - 1):
+            assert hd[s, i].tobytes() == O.hh256s(ref[i])
+    full = st.clone()
+    lost = list(range(0, k, 4))[:40] + list(range(k, k + m, 2))[:24]  # m shards: 40 data + 24 parity
+    assert len(lost) == m
+    present = [i not in lost for i in range(k + m)]
+    st[:, lost] = 0
+    e.reconstruct_batch(st, present, RSG_RECONSTRUCT_MISSING)
+    torch.cuda.synchronize()
+    assert torch.equal(st, full)
