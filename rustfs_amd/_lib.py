@@ -114,6 +114,14 @@ def load():
         return L
 
 
+def status_list(status, n: int) -> list:
+    """Per-stripe status codes of a ctypes int array as a list, in one C-level
+    pass (indexing the ctypes array element by element costs ~0.1 us each:
+    0.4 ms per 4096-stripe call, a fifth of a GET call's kernel time)."""
+    import numpy as np
+    return np.frombuffer(status, dtype=np.int32, count=n).tolist() if n else []
+
+
 def strerror(code: int) -> str:
     return load().rsg_strerror(code).decode()
 

@@ -144,7 +144,7 @@ def bitrot_verify_batch(files, want_size: int, part_size: int, algo: HashAlgorit
     _lib.check(_lib.load().rsg_bitrot_verify_dev(
         _lib.context(dev.index or 0).handle, algo.value, n, ptrs, lens, want_size, part_size, shard_size, status,
         s), "bitrot_verify")
-    return [int(status[i]) for i in range(n)]
+    return _lib.status_list(status, n)
 
 
 def raise_for_status(code: int) -> None:

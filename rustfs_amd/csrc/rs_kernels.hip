@@ -371,11 +371,20 @@ __device__ __forceinline__ void st64_any(uint8_t* p, uint64_t v) { __builtin_mem
 // stripe: 2 waves per SIMD at 4096 stripes) needs the deeper pipeline to keep
 // enough bytes in flight per CU.  COPY: also store the message bytes to
 // copy_base[b] + r*copy_stride (multi-file).
-template <bool COPY, int DEEP>
+//
+// COPY = 2 (staged copy, multi-file mode): each wave passes its 16 messages'
+// 8-packet batches (16 x 256 B) through a wave-private LDS tile and stores them
+// 16 B per lane, 256 contiguous bytes per message (four whole messages' pieces
+// per instruction) instead of 16 scattered 32-byte pieces of 8 B per lane.
+// The whole wave stays in the loop (a quad past n hashes message 0 and stores
+// nothing) because its lanes store other quads' bytes.
+template <int COPY, int DEEP>
 __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
-    const uint64_t j = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 2;
+    const uint64_t j0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 2;
     const uint32_t q = threadIdx.x & 3u;
-    if (j >= p.n) return;  // whole quads exit together
+    const bool alive = j0 < p.n;
+    if (COPY != 2 && !alive) return;  // whole quads exit together
+    const uint64_t j = alive ? j0 : 0;
     const uint8_t* msg;
     uint8_t* dst = nullptr;
     uint8_t* flag = p.flags ? p.flags + j : nullptr;
@@ -383,10 +392,27 @@ __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
         const uint64_t b = j / p.per_base, r = j - b * p.per_base;
         msg = p.base[b] + r * p.stripe_stride;
         if (p.flag_base[b]) flag = p.flag_base[b] + r;
-        if constexpr (COPY) dst = p.copy_base[b] + r * p.copy_stride;
+        if constexpr (COPY != 0) dst = p.copy_base[b] + r * p.copy_stride;
     } else {
         const uint64_t stripe = j / p.shards, shard = j - stripe * p.shards;
         msg = p.data + stripe * p.stripe_stride + shard * p.shard_pitch;
+    }
+    // staged copy: this lane stores bytes [16 (lane & 15), +16) of every
+    // 256-byte batch of wave messages 4 kk + (lane >> 4), kk = 0..3
+    __shared__ __attribute__((aligned(16))) uint8_t stage[COPY == 2 ? 4 * 4096 : 16];
+    uint8_t* sdst[4] = {nullptr, nullptr, nullptr, nullptr};
+    uint8_t* const stg = stage + (COPY == 2 ? (threadIdx.x >> 6) * 4096u : 0u);
+    const uint32_t lane = threadIdx.x & 63u;
+    if constexpr (COPY == 2) {
+        const uint64_t wj = ((uint64_t)blockIdx.x * 256u + (threadIdx.x & ~63u)) >> 2;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const uint64_t jj = wj + 4 * kk + (lane >> 4);
+            if (jj < p.n) {
+                const uint64_t b = jj / p.per_base, r = jj - b * p.per_base;
+                sdst[kk] = p.copy_base[b] + r * p.copy_stride + (lane & 15u) * 16u;
+            }
+        }
     }
     HHQuad s;
     hhq_init(s, p.key, q);
@@ -401,9 +427,19 @@ __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
     auto consume = [&](const uint64_t (&w)[8], uint64_t t0) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) hhq_update(s, w[i]);
-        if constexpr (COPY) {
+        if constexpr (COPY == 1) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) st64_any(dst + (t0 + i) * 32 + 8 * q, w[i]);
+        } else if constexpr (COPY == 2) {
+            // one wave's LDS instructions execute in order: the reads below see
+            // these writes, and the next batch's writes follow these reads
+#pragma unroll
+            for (int i = 0; i < 8; ++i) *(uint64_t*)(stg + (lane >> 2) * 256u + i * 32 + 8 * q) = w[i];
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const uint4 v = *(const uint4*)(stg + (4 * kk + (lane >> 4)) * 256u + (lane & 15u) * 16u);
+                if (sdst[kk]) st16(sdst[kk] + t0 * 32, v);
+            }
         }
     };
     const uint64_t nb = packets / 8;  // whole 8-packet batches
@@ -430,6 +466,7 @@ __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
             consume(w, t);
         }
     }
+    if (!alive) return;  // (COPY == 2) the wave-wide staged batches are done
     for (; t < packets; ++t) {
         const uint64_t w = ld64_any(msg + t * 32 + 8 * q);
         hhq_update(s, w);
@@ -882,6 +919,12 @@ hipError_t launch_hh256(const HashParams& p, hipStream_t stream) {
     const uint64_t blocks = (p.n * 4u + 255u) / 256u;  // one quad per message
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
     const bool copy = p.nbases && p.copy_base[0];
+    // copy mode: staged 16-byte stores (COPY = 2) by default; RSG_HASH_COPY=1
+    // selects the direct 8-byte stores for A/B runs
+    static const bool direct_copy = [] {
+        const char* e = getenv("RSG_HASH_COPY");
+        return e && e[0] == '1';
+    }();
     // Two batches in flight per lane (DEEP) unless the launch alone fills the
     // GPU with waves; RSG_HASH_DEEP=0/1 forces one for A/B runs.
     static const int force = [] {
@@ -890,8 +933,9 @@ hipError_t launch_hh256(const HashParams& p, hipStream_t stream) {
     }();
     const bool deep = force >= 0 ? force == 1 : true;
     using HashKernel = void (*)(const HashParams);
-    const HashKernel k = copy ? (deep ? k_hh256_quad<true, 1> : k_hh256_quad<true, 0>)
-                              : (deep ? k_hh256_quad<false, 1> : k_hh256_quad<false, 0>);
+    const HashKernel k = copy ? (direct_copy ? (deep ? k_hh256_quad<1, 1> : k_hh256_quad<1, 0>)
+                                             : (deep ? k_hh256_quad<2, 1> : k_hh256_quad<2, 0>))
+                              : (deep ? k_hh256_quad<0, 1> : k_hh256_quad<0, 0>);
     hipLaunchKernelGGL(k, dim3((uint32_t)blocks), dim3(256), 0, stream, p);
     return hipGetLastError();
 }

@@ -325,7 +325,7 @@ class Erasure:
         check(_lib.load().rsg_decode_records_dev(
             _lib.context(dev.index or 0).handle, self.data_shards, self.parity_shards, shard_len, n, ptrs, algo,
             1 if verify_surplus else 0, out.data_ptr(), status, s), "RustFS codec reconstruct failed")
-        return out, [int(status[i]) for i in range(n)]
+        return out, _lib.status_list(status, n)
 
     def heal_records_batch(self, files: Sequence, targets: Sequence, shard_len: int, n: int,
                            algo: int = _lib.RSG_HASH_HIGHWAY256S, work=None, stream=None):
@@ -359,7 +359,7 @@ class Erasure:
         check(_lib.load().rsg_heal_records_dev(
             _lib.context(dev.index or 0).handle, self.data_shards, self.parity_shards, shard_len, n, src, dst,
             algo, work.data_ptr(), status, s), "erasure heal")
-        return [int(status[i]) for i in range(n)]
+        return _lib.status_list(status, n)
 
     def reconstruct_batch(self, stripes, present: Sequence[bool], mode: int = _lib.RSG_RECONSTRUCT_MISSING,
                           stream=None) -> None:
