@@ -16,6 +16,7 @@
 #include <list>
 #include <map>
 #include <memory>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -386,12 +387,44 @@ uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 // --------------------------------------------------------------------------
 // Context.
 
+// One lane of the host-buffer API (rsg_encode / rsg_reconstruct / rsg_verify /
+// rsg_hash): its own stream and device buffer, so calls from several host
+// threads (the reference encodes from many tokio workers, encode.rs:511-526)
+// run their copies and kernels concurrently instead of queueing on one lock.
+struct HostLane {
+    std::mutex mu;
+    hipStream_t stream = nullptr;
+    uint8_t* d_buf = nullptr;
+    size_t cap = 0;
+
+    int ensure(size_t bytes) {
+        if (!stream) {
+            hipError_t e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+            if (e != hipSuccess) return hip_status(e);
+        }
+        if (bytes <= cap) return RSG_OK;
+        if (d_buf) (void)hipFree(d_buf);
+        d_buf = nullptr;
+        cap = 0;
+        const size_t want = std::max(bytes, (size_t)1 << 20);
+        hipError_t e = hipMalloc((void**)&d_buf, want);
+        if (e != hipSuccess) return hip_status(e);
+        cap = want;
+        return RSG_OK;
+    }
+};
+
+constexpr int kHostLanes = 8;
+
 struct rsg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    std::mutex mu;  // serialises the host-buffer API on this context
+    std::mutex mu;  // serialises the device-batch record engines' scratch use
     uint8_t* d_scratch = nullptr;
     size_t scratch_cap = 0;
+
+    HostLane lanes[kHostLanes];
+    std::atomic<unsigned> next_lane{0};
 
     // host-batch pipeline (rsg_encode_batch_host): two stream/staging pairs
     std::mutex pipe_mu;
@@ -437,6 +470,31 @@ int enter(rsg_ctx* ctx) {
     if (!ctx) return RSG_ERR_INVALID_ARG;
     return hip_status(hipSetDevice(ctx->device));
 }
+// A free host lane, locked: try every lane once starting round-robin, then
+// wait on the starting one.
+std::unique_lock<std::mutex> acquire_lane(rsg_ctx* ctx, HostLane*& lane) {
+    const unsigned start = ctx->next_lane.fetch_add(1, std::memory_order_relaxed);
+    for (int i = 0; i < kHostLanes; ++i) {
+        HostLane& l = ctx->lanes[(start + i) % kHostLanes];
+        std::unique_lock<std::mutex> g(l.mu, std::try_to_lock);
+        if (g.owns_lock()) {
+            lane = &l;
+            return g;
+        }
+    }
+    lane = &ctx->lanes[start % kHostLanes];
+    return std::unique_lock<std::mutex>(lane->mu);
+}
+
+// Shards laid out back to back (the reference's encode_buffer block:
+// [shard 0 .. shard k+m-1], S bytes each, erasure.rs:848-887) move with one
+// copy per direction instead of one per shard.
+bool contiguous(const uint8_t* const* shards, int first, int count, size_t len) {
+    for (int i = 1; i < count; ++i)
+        if (shards[first + i] != shards[first] + (size_t)i * len) return false;
+    return true;
+}
+
 // Device-batch calls run on the caller's stream; NULL is the HIP null (default)
 // stream, which is also torch's default stream, so ordering with the caller holds.
 hipStream_t pick_stream(rsg_ctx*, void* s) { return (hipStream_t)s; }
@@ -504,6 +562,13 @@ void rsg_destroy(rsg_ctx* ctx) {
         (void)hipStreamDestroy(ctx->stream);
     }
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+    for (HostLane& l : ctx->lanes) {
+        if (l.stream) {
+            (void)hipStreamSynchronize(l.stream);
+            (void)hipStreamDestroy(l.stream);
+        }
+        if (l.d_buf) (void)hipFree(l.d_buf);
+    }
     for (int i = 0; i < 2; ++i) {
         if (ctx->pipe_stream[i]) {
             (void)hipStreamSynchronize(ctx->pipe_stream[i]);
@@ -1110,23 +1175,36 @@ int rsg_encode(rsg_ctx* ctx, int k, int m, size_t shard_len, uint8_t* const* sha
     for (int i = 0; i < k + m; ++i)
         if (!shards[i]) return RSG_ERR_INVALID_ARG;
     if (shard_len == 0) return RSG_ERR_EMPTY_SHARD;
-    std::lock_guard<std::mutex> g(ctx->mu);
-    const uint64_t pitch = round_up(shard_len, 256);
-    if ((st = ctx->ensure_scratch((size_t)pitch * (k + m)))) return st;
-    hipStream_t s = ctx->stream;
-    for (int i = 0; i < k; ++i)
-        if ((st = hip_status(hipMemcpyAsync(ctx->d_scratch + i * pitch, shards[i], shard_len,
-                                            hipMemcpyHostToDevice, s))))
-            return st;
     auto cd = get_codec(k, m);
     if (!cd) return RSG_ERR_INVALID_ARG;
+    HostLane* lane;
+    auto g = acquire_lane(ctx, lane);
+    // one block per call: data in, parity out, the kernels read the device
+    // copy at pitch S (back-to-back shards) or 256-aligned slots
+    const bool in_one = contiguous(shards, 0, k, shard_len), out_one = contiguous(shards, k, m, shard_len);
+    const uint64_t pitch = in_one ? shard_len : round_up(shard_len, 256);
+    if ((st = lane->ensure((size_t)pitch * (k + m)))) return st;
+    hipStream_t s = lane->stream;
+    uint8_t* d = lane->d_buf;
+    if (in_one) {
+        if ((st = hip_status(hipMemcpyAsync(d, shards[0], (size_t)k * shard_len, hipMemcpyHostToDevice, s)))) return st;
+    } else {
+        for (int i = 0; i < k; ++i)
+            if ((st = hip_status(hipMemcpyAsync(d + i * pitch, shards[i], shard_len, hipMemcpyHostToDevice, s))))
+                return st;
+    }
     RowSet rs = encode_rows(*cd, pitch);
-    if ((st = apply_rows(rs, ctx->d_scratch, ctx->d_scratch, 0, 0, shard_len, 1, rsg::GF_MODE_STORE, nullptr, s)))
-        return st;
-    for (int p = 0; p < m; ++p)
-        if ((st = hip_status(hipMemcpyAsync(shards[k + p], ctx->d_scratch + (k + p) * pitch, shard_len,
+    if ((st = apply_rows(rs, d, d, 0, 0, shard_len, 1, rsg::GF_MODE_STORE, nullptr, s))) return st;
+    if (out_one && pitch == shard_len) {
+        if ((st = hip_status(hipMemcpyAsync(shards[k], d + (size_t)k * pitch, (size_t)m * shard_len,
                                             hipMemcpyDeviceToHost, s))))
             return st;
+    } else {
+        for (int p = 0; p < m; ++p)
+            if ((st = hip_status(hipMemcpyAsync(shards[k + p], d + (k + p) * pitch, shard_len, hipMemcpyDeviceToHost,
+                                                s))))
+                return st;
+    }
     return hip_status(hipStreamSynchronize(s));
 }
 
@@ -1164,24 +1242,25 @@ int rsg_reconstruct(rsg_ctx* ctx, int k, int m, size_t shard_len, uint8_t* const
             (!is_data && mode == RSG_RECONSTRUCT_REENCODE_PARITY))
             targets.push_back(i);
     }
-    std::lock_guard<std::mutex> g(ctx->mu);
+    HostLane* lane;
+    auto g = acquire_lane(ctx, lane);
     const uint64_t pitch = round_up(shard_len, 256);
-    if ((st = ctx->ensure_scratch((size_t)pitch * (k + targets.size())))) return st;
-    hipStream_t s = ctx->stream;
+    if ((st = lane->ensure((size_t)pitch * (k + targets.size())))) return st;
+    hipStream_t s = lane->stream;
+    uint8_t* d = lane->d_buf;
     rs.in_off.clear();
     rs.out_off.clear();
-    // Survivors go to slots 0..k-1 of the scratch, outputs to slots k.. .
+    // Survivors go to slots 0..k-1 of the lane buffer, outputs to slots k.. .
     for (int c = 0; c < k; ++c) {
-        if ((st = hip_status(hipMemcpyAsync(ctx->d_scratch + c * pitch, shards[plan->survivors[c]], shard_len,
+        if ((st = hip_status(hipMemcpyAsync(d + c * pitch, shards[plan->survivors[c]], shard_len,
                                             hipMemcpyHostToDevice, s))))
             return st;
         rs.in_off.push_back((uint64_t)c * pitch);
     }
     for (size_t r = 0; r < targets.size(); ++r) rs.out_off.push_back((uint64_t)(k + r) * pitch);
-    if ((st = apply_rows(rs, ctx->d_scratch, ctx->d_scratch, 0, 0, shard_len, 1, rsg::GF_MODE_STORE, nullptr, s)))
-        return st;
+    if ((st = apply_rows(rs, d, d, 0, 0, shard_len, 1, rsg::GF_MODE_STORE, nullptr, s))) return st;
     for (size_t r = 0; r < targets.size(); ++r)
-        if ((st = hip_status(hipMemcpyAsync(shards[targets[r]], ctx->d_scratch + (k + r) * pitch, shard_len,
+        if ((st = hip_status(hipMemcpyAsync(shards[targets[r]], d + (k + r) * pitch, shard_len,
                                             hipMemcpyDeviceToHost, s))))
             return st;
     return hip_status(hipStreamSynchronize(s));
@@ -1199,44 +1278,45 @@ int rsg_verify(rsg_ctx* ctx, int k, int m, size_t shard_len, const uint8_t* cons
     }
     for (int i = 0; i < k + m; ++i)
         if (!shards[i]) return RSG_ERR_INVALID_ARG;
-    std::lock_guard<std::mutex> g(ctx->mu);
-    const uint64_t pitch = round_up(shard_len, 256);
-    const uint64_t flag_off = pitch * (uint64_t)(2 * m + k);
-    if ((st = ctx->ensure_scratch((size_t)flag_off + 256))) return st;
-    hipStream_t s = ctx->stream;
-    for (int i = 0; i < k + m; ++i)
-        if ((st = hip_status(hipMemcpyAsync(ctx->d_scratch + i * pitch, shards[i], shard_len, hipMemcpyHostToDevice,
-                                            s))))
-            return st;
     auto cd = get_codec(k, m);
     if (!cd) return RSG_ERR_INVALID_ARG;
+    HostLane* lane;
+    auto g = acquire_lane(ctx, lane);
+    const uint64_t pitch = round_up(shard_len, 256);
+    const uint64_t flag_off = pitch * (uint64_t)(2 * m + k);
+    if ((st = lane->ensure((size_t)flag_off + 256))) return st;
+    hipStream_t s = lane->stream;
+    uint8_t* d = lane->d_buf;
+    for (int i = 0; i < k + m; ++i)
+        if ((st = hip_status(hipMemcpyAsync(d + i * pitch, shards[i], shard_len, hipMemcpyHostToDevice, s)))) return st;
     RowSet rs = encode_rows(*cd, pitch);
-    uint8_t* d_flag = ctx->d_scratch + flag_off;
+    uint8_t* d_flag = d + flag_off;
+    if ((st = hip_status(hipMemsetAsync(d_flag, 1, 1, s)))) return st;
     if (k <= rsg::kMaxC) {
-        if ((st = hip_status(hipMemsetAsync(d_flag, 1, 1, s)))) return st;
-        if ((st = apply_rows(rs, ctx->d_scratch, ctx->d_scratch, 0, 0, shard_len, 1, rsg::GF_MODE_COMPARE, d_flag,
-                             s)))
-            return st;
-        uint8_t h = 0;
-        if ((st = hip_status(hipMemcpyAsync(&h, d_flag, 1, hipMemcpyDeviceToHost, s)))) return st;
-        if ((st = hip_status(hipStreamSynchronize(s)))) return st;
-        *ok = h ? 1 : 0;
-        return RSG_OK;
+        // re-encode and compare in one pass (erasure.rs:430-441)
+        if ((st = apply_rows(rs, d, d, 0, 0, shard_len, 1, rsg::GF_MODE_COMPARE, d_flag, s))) return st;
+    } else {
+        // k > 16 cannot compare inside a chained (GF_MODE_XOR) product: re-encode
+        // into spare slots, then compare them with the given parity on the
+        // device (identity rows in compare mode, <= 16 per launch)
+        for (int p = 0; p < m; ++p) rs.out_off[p] = (uint64_t)(k + m + p) * pitch;
+        if ((st = apply_rows(rs, d, d, 0, 0, shard_len, 1, rsg::GF_MODE_STORE, nullptr, s))) return st;
+        for (int p0 = 0; p0 < m; p0 += rsg::kMaxC) {
+            RowSet id;
+            id.R = id.C = std::min(rsg::kMaxC, m - p0);
+            id.coef.assign((size_t)id.R * id.C, 0);
+            for (int i = 0; i < id.R; ++i) {
+                id.coef[(size_t)i * id.C + i] = 1;
+                id.in_off.push_back((uint64_t)(k + m + p0 + i) * pitch);
+                id.out_off.push_back((uint64_t)(k + p0 + i) * pitch);
+            }
+            if ((st = apply_rows(id, d, d, 0, 0, shard_len, 1, rsg::GF_MODE_COMPARE, d_flag, s))) return st;
+        }
     }
-    // k > 16: re-encode into spare slots and compare on the device copy.
-    for (int p = 0; p < m; ++p) rs.out_off[p] = (uint64_t)(k + m + p) * pitch;
-    if ((st = apply_rows(rs, ctx->d_scratch, ctx->d_scratch, 0, 0, shard_len, 1, rsg::GF_MODE_STORE, nullptr, s)))
-        return st;
-    std::vector<uint8_t> buf(shard_len);
-    int good = 1;
-    for (int p = 0; p < m && good; ++p) {
-        if ((st = hip_status(hipMemcpyAsync(buf.data(), ctx->d_scratch + (k + m + p) * pitch, shard_len,
-                                            hipMemcpyDeviceToHost, s))))
-            return st;
-        if ((st = hip_status(hipStreamSynchronize(s)))) return st;
-        good = std::memcmp(buf.data(), shards[k + p], shard_len) == 0;
-    }
-    *ok = good;
+    uint8_t h = 0;
+    if ((st = hip_status(hipMemcpyAsync(&h, d_flag, 1, hipMemcpyDeviceToHost, s)))) return st;
+    if ((st = hip_status(hipStreamSynchronize(s)))) return st;
+    *ok = h ? 1 : 0;
     return RSG_OK;
 }
 
@@ -1244,13 +1324,15 @@ int rsg_hash(rsg_ctx* ctx, int algo, const uint8_t* data, size_t len, uint8_t ou
     int st = enter(ctx);
     if (st) return st;
     if (!out || (len && !data) || !hash_key(algo)) return RSG_ERR_INVALID_ARG;
-    std::lock_guard<std::mutex> g(ctx->mu);
+    HostLane* lane;
+    auto g = acquire_lane(ctx, lane);
     const uint64_t data_bytes = round_up(len ? len : 1, 256);
-    if ((st = ctx->ensure_scratch((size_t)data_bytes + 256))) return st;
-    hipStream_t s = ctx->stream;
-    if (len && (st = hip_status(hipMemcpyAsync(ctx->d_scratch, data, len, hipMemcpyHostToDevice, s)))) return st;
-    if ((st = hash_messages(algo, ctx->d_scratch, len, 1, 1, 0, 0, ctx->d_scratch + data_bytes, s))) return st;
-    if ((st = hip_status(hipMemcpyAsync(out, ctx->d_scratch + data_bytes, 32, hipMemcpyDeviceToHost, s)))) return st;
+    if ((st = lane->ensure((size_t)data_bytes + 256))) return st;
+    hipStream_t s = lane->stream;
+    uint8_t* d = lane->d_buf;
+    if (len && (st = hip_status(hipMemcpyAsync(d, data, len, hipMemcpyHostToDevice, s)))) return st;
+    if ((st = hash_messages(algo, d, len, 1, 1, 0, 0, d + data_bytes, s))) return st;
+    if ((st = hip_status(hipMemcpyAsync(out, d + data_bytes, 32, hipMemcpyDeviceToHost, s)))) return st;
     return hip_status(hipStreamSynchronize(s));
 }
 

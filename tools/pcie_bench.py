@@ -28,6 +28,52 @@ def copy_rate(nbytes, h2d=True, reps=5):
     return reps * nbytes / (time.perf_counter() - t) / 1e9
 
 
+def per_block_calls(k, m, S, calls=200, threads=8, layout="separate"):
+    """The reference's call pattern: one 1 MiB block per ReedSolomonEncoder::encode
+    call (encode.rs:504-530) through rsg_encode: latency per call on one thread,
+    and the aggregate rate of `threads` callers.  layout: "separate" (one
+    pageable buffer per shard), "block" (shards back to back in one pageable
+    buffer, encode_buffer's layout, erasure.rs:848-887: one copy per
+    direction), "pinned" (that block in page-locked memory, as a pool of
+    rsg_pin'ed block buffers would give)."""
+    import threading
+    from rustfs_amd import ReedSolomonEncoder
+    rng = np.random.default_rng(1)
+
+    def worker(res, idx):
+        enc = ReedSolomonEncoder(k, m)
+        if layout == "separate":
+            sh = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
+        else:
+            blk = (torch.zeros((k + m) * S, dtype=torch.uint8).pin_memory().numpy() if layout == "pinned"
+                   else np.zeros((k + m) * S, np.uint8)).reshape(k + m, S)
+            blk[:k] = rng.integers(0, 256, (k, S), dtype=np.uint8)
+            sh = [blk[i] for i in range(k + m)]
+        enc.encode(sh)
+        ts = []
+        for _ in range(calls):
+            t0 = time.perf_counter()
+            enc.encode(sh)
+            ts.append(time.perf_counter() - t0)
+        res[idx] = ts
+
+    one = {}
+    worker(one, 0)
+    lat = sorted(one[0])
+    many = {}
+    th = [threading.Thread(target=worker, args=(many, i)) for i in range(threads)]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    el = time.perf_counter() - t0
+    return {"median_us": round(lat[len(lat) // 2] * 1e6, 1), "p99_us": round(lat[int(len(lat) * 0.99)] * 1e6, 1),
+            "GiB_s_1_thread": round(k * S / lat[len(lat) // 2] / GiB, 2),
+            f"GiB_s_{threads}_threads": round(threads * calls * k * S / el / GiB, 2),
+            "note": f"host-buffer rsg_encode per 1 MiB block, H2D+kernel+D2H per call, layout {layout}"}
+
+
 def main():
     k, m, S, n = 8, 4, 131072, int(os.environ.get("PCIE_STRIPES", "1024"))
     out = {"h2d_GB_s": round(copy_rate(1 << 30, True), 2), "d2h_GB_s": round(copy_rate(1 << 30, False), 2)}
@@ -46,6 +92,8 @@ def main():
             "GiB_s_payload": round(n * k * S / el / GiB, 2), "ms_per_batch": round(el * 1e3, 2),
             "pcie_bytes_GB_s": round(n * (k + m) * S / el / 1e9 if True else 0, 2)}
     out["config"] = f"RS({k},{m}) S={S} n={n} pinned host buffers"
+    for layout in ("separate", "block", "pinned"):
+        out[f"per_block_call_{layout}"] = per_block_calls(k, m, S, layout=layout)
     print(json.dumps(out), flush=True)
 
 
