@@ -403,3 +403,39 @@ def test_max_geometry_batch_roundtrip(gpu, oracle):
     e.reconstruct_batch(st, present, RSG_RECONSTRUCT_MISSING)
     torch.cuda.synchronize()
     assert torch.equal(st, full)
+
+
+def test_host_api_concurrent_callers(gpu, oracle):
+    """Many threads calling encode / reconstruct / verify at once (the reference
+    encodes from many tokio workers, encode.rs:511-526): every result stays
+    bit-exact while calls spread over the context's host lanes."""
+    import threading
+    from rustfs_amd import ReedSolomonEncoder
+    k, m, S = 8, 4, 4096 + 48
+    errors = []
+
+    def worker(seed):
+        try:
+            rng = np.random.default_rng(seed)
+            enc = ReedSolomonEncoder(k, m)
+            for it in range(12):
+                ref = rand_stripe(rng, k, m, S)
+                oracle.encode(k, m, ref)
+                blk = ref.copy()
+                blk[k:] = 0
+                enc.encode([blk[i] for i in range(k + m)])  # back-to-back block layout
+                assert (blk == ref).all()
+                miss = set(rng.choice(k + m, size=m, replace=False).tolist())
+                shards = [None if i in miss else ref[i].tobytes() for i in range(k + m)]
+                enc.reconstruct_opt(shards)
+                assert all(bytes(shards[i]) == ref[i].tobytes() for i in range(k + m))
+                assert enc.verify([ref[i] for i in range(k + m)])
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(100 + i,)) for i in range(12)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:3]
