@@ -70,3 +70,58 @@ def test_decode_records_detects_inconsistent_parity(gpu, oracle):
     # without surplus verification the rebuilt data is still exact (the parity is not a survivor)
     out, status = e.decode_records_batch(f, S, n, verify_surplus=False)
     assert status == [0] * n and torch.equal(out, want)
+
+
+@pytest.mark.parametrize("k,m,S,n,lost", [
+    (8, 4, 131072, 5, (0,)), (8, 4, 131072, 6, (0, 3)), (8, 4, 4096, 9, (1, 4, 6)), (8, 4, 4096, 7, (0, 2, 5, 7)),
+    (8, 4, 4096, 7, (3, 9)), (8, 4, 4096, 5, (2, 8, 11)), (4, 2, 65536, 4, (1,)), (6, 3, 4096, 3, (0, 5, 7)),
+    (2, 2, 1024, 3, (0,)), (1, 3, 512, 2, (0, 2)), (5, 4, 2048, 9, (4,)),
+])
+def test_decode_records_lost_disk_one_pass(gpu, oracle, k, m, S, n, lost):
+    """A lost disk (whole data shard files missing) takes the one-pass GET
+    kernel (verify + gather + rebuild + surplus check): bit-exact output."""
+    import torch
+    e, st, files = _records(torch, k, m, S, n, seed=S + len(lost))
+    want = st[:, :k].reshape(n, k * S)
+    f = [None if i in lost else files[i] for i in range(k + m)]
+    out, status = e.decode_records_batch(f, S, n)
+    assert status == [0] * n and torch.equal(out, want)
+    out, status = e.decode_records_batch(f, S, n, verify_surplus=False)
+    assert status == [0] * n and torch.equal(out, want)
+
+
+def test_decode_records_lost_disk_with_rotten_record(gpu, oracle):
+    """Lost disk plus a rotten record elsewhere: the one-pass result is not
+    trusted (a digest mismatched), the general path picks other survivors for
+    that stripe and still returns the exact data."""
+    import torch
+    k, m, S, n = 8, 4, 4096, 6
+    e, st, files = _records(torch, k, m, S, n, seed=11)
+    rec = 32 + S
+    want = st[:, :k].reshape(n, k * S)
+    f = [None if i == 2 else files[i].clone() for i in range(k + m)]
+    f[5][3 * rec + 32 + 100] ^= 0x08  # data record body of stripe 3
+    f[k][1 * rec + 7] ^= 0x01  # parity digest of stripe 1
+    out, status = e.decode_records_batch(f, S, n)
+    assert status == [0] * n and torch.equal(out, want)
+
+
+def test_decode_records_lost_disk_inconsistent_surplus(gpu, oracle):
+    """Lost disk, every digest valid, one surplus parity record re-hashed after
+    a bit flip: the one-pass kernel reports InvalidData for that stripe only."""
+    import torch
+    from rustfs_amd import _lib
+    k, m, S, n = 8, 4, 4096, 5
+    e, st, files = _records(torch, k, m, S, n, seed=13)
+    rec = 32 + S
+    bad = files[k + 3].clone()
+    body = bad[4 * rec + 32: 5 * rec].cpu().numpy().copy()
+    body[7] ^= 0x10
+    bad[4 * rec + 32: 5 * rec] = torch.from_numpy(body).cuda()
+    bad[4 * rec: 4 * rec + 32] = torch.from_numpy(np.frombuffer(oracle.hh256s(body), dtype=np.uint8).copy()).cuda()
+    f = [None if i == 0 else files[i] for i in range(k + m)]
+    f[k + 3] = bad
+    out, status = e.decode_records_batch(f, S, n)
+    assert status == [0, 0, 0, 0, _lib.RSG_ERR_INCONSISTENT_SOURCES]
+    want = st[:, :k].reshape(n, k * S)
+    assert torch.equal(out[:4], want[:4])
