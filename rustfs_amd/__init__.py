@@ -19,6 +19,7 @@ from ._lib import (  # noqa: F401
 from .erasure import (  # noqa: F401
     Erasure,
     ErasureConstructionError,
+    GpuCodecDecodeEngine,
     ReedSolomonEncoder,
     UnsupportedModernShardCount,
     ZeroBlockSize,

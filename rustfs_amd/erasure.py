@@ -232,6 +232,28 @@ class Erasure:
         buf = self.encode_buffer(data)
         return [buf[i].tobytes() for i in range(buf.shape[0])]
 
+    def encode_inline_shards(self, data) -> List[bytes]:
+        """encode_inline_shards_with_size_hint (encode.rs:601-628): encode one
+        small object and return each shard as its BitrotWriter payload
+        ``[HighwayHash256S(shard)][shard]`` (empty list for an empty object).
+        Parity and all k+m digests come from one rsg_encode_batch_host call
+        (fused encode + hash on the device)."""
+        data = _as_array(data)
+        if data.size == 0:
+            return []
+        per_shard = calc_shard_size(data.size, self.data_shards)
+        t = self.total_shard_count()
+        buf = np.zeros((1, t, per_shard), dtype=np.uint8)
+        buf.reshape(-1)[: data.size] = data
+        dig = np.zeros((1, t, 32), dtype=np.uint8)
+        if self.parity_shards:
+            self.encode_batch_host(buf, dig)
+        else:
+            from .bitrot import HashAlgorithm
+            for i in range(t):
+                dig[0, i] = np.frombuffer(HashAlgorithm.HighwayHash256S.hash_encode(buf[0, i], self._device), np.uint8)
+        return [dig[0, i].tobytes() + buf[0, i].tobytes() for i in range(t)]
+
     # -- decode (erasure.rs:897-1019) --
     def decode_data(self, shards: List) -> None:
         if self.encoder is not None:
@@ -379,6 +401,88 @@ class Erasure:
             stripes.data_ptr(), S, t * S, ok.data_ptr(), _stream_of(stripes, stream)),
             "Reed-Solomon verify failed")
         return ok
+
+
+# ---------------------------------------------------------------------------
+# The GET decode-engine seam (crates/ecstore/src/erasure/codec/bridge.rs:33-50):
+# a GPU arm beside RustfsCodecDecodeEngine (bridge.rs:137-307), same outcome
+# labels, same error messages.
+
+GET_RECONSTRUCT_OUTCOME_SKIP_DATA_COMPLETE = "skip_data_complete"  # bridge.rs:25
+GET_RECONSTRUCT_OUTCOME_SKIP_EMPTY_PAYLOAD = "skip_empty_payload"  # bridge.rs:26
+GET_RECONSTRUCT_OUTCOME_GPU_CALLED = "rsgpu_called"
+
+
+class GpuDecodeWorkspace:
+    """RustfsCodecDecodeWorkspace's role: carries the shard length the engine
+    was prepared for (the device buffers live in the library's context)."""
+
+    def __init__(self, shard_len: int):
+        self._shard_len = shard_len
+
+    def shard_len(self) -> int:
+        return self._shard_len
+
+
+class GpuCodecDecodeEngine:
+    """ErasureDecodeEngine (bridge.rs:33-50) on librsgpu, with
+    RustfsCodecDecodeEngine::reconstruct_into's semantics (bridge.rs:274-307):
+    data complete -> skip; all-empty payload -> empty data shards; a missing
+    data shard with more than k shards available -> rebuild every missing
+    shard and verify the whole set (InvalidData "inconsistent read source
+    shards", bridge.rs:202-236); otherwise rebuild the missing data only."""
+
+    def __init__(self, erasure: Erasure):
+        self.erasure = erasure
+        self._enc = ReedSolomonEncoder(erasure.data_shards, erasure.parity_shards, erasure._device) \
+            if erasure.parity_shards else None
+
+    def data_shards(self) -> int:
+        return self.erasure.data_shards
+
+    def parity_shards(self) -> int:
+        return self.erasure.parity_shards
+
+    def block_size(self) -> int:
+        return self.erasure.block_size
+
+    def engine_name(self) -> str:
+        return "rsgpu"
+
+    def supports_progressive_decode(self) -> bool:
+        return False
+
+    def supports_aligned_shards(self) -> bool:
+        return False
+
+    def prepare_workspace(self, shard_len: int) -> GpuDecodeWorkspace:
+        return GpuDecodeWorkspace(shard_len)
+
+    def reconstruct_into(self, shards: List, workspace: Optional[GpuDecodeWorkspace] = None) -> str:
+        k, m = self.erasure.data_shards, self.erasure.parity_shards
+        if len(shards) >= k and all(s is not None for s in shards[:k]):  # data_shards_complete, bridge.rs:52
+            return GET_RECONSTRUCT_OUTCOME_SKIP_DATA_COMPLETE
+        if len(shards) != k + m:  # recover_empty_payload_data_shards, bridge.rs:56-84
+            raise RsgError(_lib.RSG_ERR_INVALID_SHARD_COUNT,
+                           f"invalid shard count: got {len(shards)}, expected {k + m}")
+        present = [s for s in shards if s is not None]
+        if present and all(len(s) == 0 for s in present) and len(present) >= k:
+            for i in range(k):
+                if shards[i] is None:
+                    shards[i] = bytearray()
+            return GET_RECONSTRUCT_OUTCOME_SKIP_EMPTY_PAYLOAD
+        if self._enc is not None:
+            needs_verification = any(s is None for s in shards[:k]) and len(present) > k
+            try:
+                if needs_verification:
+                    self._enc.reconstruct_opt(shards)
+                else:
+                    self._enc.reconstruct_data(shards)
+            except RsgError as err:
+                raise RsgError(err.code, "RustFS codec reconstruct failed") from err
+            if needs_verification and not self._enc.verify(shards):
+                raise InvalidDataError(_lib.RSG_ERR_INCONSISTENT_SOURCES)
+        return GET_RECONSTRUCT_OUTCOME_GPU_CALLED
 
 
 def _check_batch(stripes, total: int):
