@@ -495,6 +495,30 @@ bool contiguous(const uint8_t* const* shards, int first, int count, size_t len) 
     return true;
 }
 
+// The device's view of page-locked host memory it can address (hipHostMalloc'd
+// or registered), or nullptr (pageable memory, another device's allocation).
+// Both ends of [p, p + len) must resolve to the same allocation.
+uint8_t* pinned_view(const uint8_t* p, size_t len, int device) {
+    hipPointerAttribute_t a, b;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess || hipPointerGetAttributes(&b, p + len - 1) != hipSuccess) {
+        (void)hipGetLastError();  // pageable: not an error for the caller
+        return nullptr;
+    }
+    if (a.type != hipMemoryTypeHost || b.type != hipMemoryTypeHost || a.device != device || !a.devicePointer ||
+        !b.devicePointer || (uint8_t*)b.devicePointer - (uint8_t*)a.devicePointer != (ptrdiff_t)(len - 1))
+        return nullptr;
+    return (uint8_t*)a.devicePointer;
+}
+
+// RSG_ZERO_COPY=0 disables the in-place kernels on pinned blocks (A/B runs).
+bool zero_copy_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("RSG_ZERO_COPY");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // Device-batch calls run on the caller's stream; NULL is the HIP null (default)
 // stream, which is also torch's default stream, so ordering with the caller holds.
 hipStream_t pick_stream(rsg_ctx*, void* s) { return (hipStream_t)s; }
@@ -1182,6 +1206,16 @@ int rsg_encode(rsg_ctx* ctx, int k, int m, size_t shard_len, uint8_t* const* sha
     // one block per call: data in, parity out, the kernels read the device
     // copy at pitch S (back-to-back shards) or 256-aligned slots
     const bool in_one = contiguous(shards, 0, k, shard_len), out_one = contiguous(shards, k, m, shard_len);
+    if (in_one && out_one && shards[k] == shards[0] + (size_t)k * shard_len && zero_copy_enabled()) {
+        // a whole block in pinned memory: the kernels read the data and write
+        // the parity over PCIe in place, no staging copies (per-block calls)
+        if (uint8_t* dv = pinned_view(shards[0], (size_t)(k + m) * shard_len, ctx->device)) {
+            if ((st = lane->ensure(0))) return st;
+            RowSet rs = encode_rows(*cd, shard_len);
+            if ((st = apply_rows(rs, dv, dv, 0, 0, shard_len, 1, rsg::GF_MODE_STORE, nullptr, lane->stream))) return st;
+            return hip_status(hipStreamSynchronize(lane->stream));
+        }
+    }
     const uint64_t pitch = in_one ? shard_len : round_up(shard_len, 256);
     if ((st = lane->ensure((size_t)pitch * (k + m)))) return st;
     hipStream_t s = lane->stream;
