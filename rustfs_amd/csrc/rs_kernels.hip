@@ -534,7 +534,8 @@ constexpr int fused_spw() {
 
 // ABLATE (measurement builds only, tools/kbench/fused_variants.hip): bit 0
 // skips the GF arithmetic, bit 1 the hash updates, bit 3 records each wave's
-// HW_ID in its stripe's first digest words; production uses 0.
+// HW_ID in its stripe's first digest words, bit 4 raises the hasher waves'
+// issue priority (s_setprio 1), bit 5 the encoder waves'; production uses 0.
 template <int C, int R, int SPW, int ABLATE = 0>
 __global__ __launch_bounds__(64 * (SPW + (SPW * (C + R) + 15) / 16))
 __attribute__((amdgpu_waves_per_eu(R == 1 ? 4 : C <= 8 ? 7 : C <= 12 ? 5 : 4)))
@@ -568,6 +569,7 @@ void k_encode_hash_fused(const GfApplyParams p,
 
     if (wave < (uint32_t)SPW) {
         // ------------------------------ encoder ------------------------------
+        if constexpr (ABLATE & 32) __builtin_amdgcn_s_setprio(1);
         const uint64_t stripe = (uint64_t)blockIdx.x * SPW + wave;
         const bool live = stripe < n;  // a dead stripe re-reads stripe 0 and stores nothing
         uint8_t* sb = p.out_base + (live ? stripe : 0) * p.stripe_stride;
@@ -638,6 +640,7 @@ void k_encode_hash_fused(const GfApplyParams p,
         }
     } else {
         // ------------------------------ hasher -------------------------------
+        if constexpr (ABLATE & 16) __builtin_amdgcn_s_setprio(1);
         const uint32_t g = (wave - SPW) * 16u + (lane >> 2);  // stream of this quad
         const uint32_t ls = g / T, shard = g - ls * T;        // local stripe, shard
         const uint64_t stripe = (uint64_t)blockIdx.x * SPW + ls;

@@ -187,6 +187,8 @@ int main(int argc, char** argv) {
         {"db spw4 512", [&] { GfApplyParams q2 = p; q2.units = S / 512;
                                k_fused_db<K, M, 4, 512><<<g4, 448, K * M * 32 + 2 * 4 * (K + M) * (512 + 32)>>>(q2, h); }},
         {"fused spw2", [&] { k_encode_hash_fused<K, M, 2, 0><<<(n + 1) / 2, 64 * 4, lds1 * 2 - K * M * 32>>>(p, h); }},
+        {"prio spw4 hashers", [&] { k_encode_hash_fused<K, M, 4, 16><<<g4, 448, lds4>>>(p, h); }},
+        {"prio spw4 encoders", [&] { k_encode_hash_fused<K, M, 4, 32><<<g4, 448, lds4>>>(p, h); }},
         {"spw4 no-GF", [&] { k_encode_hash_fused<K, M, 4, 1><<<g4, 448, lds4>>>(p, h); }},
         {"spw4 no-hash", [&] { k_encode_hash_fused<K, M, 4, 2><<<g4, 448, lds4>>>(p, h); }},
         {"spw4 neither", [&] { k_encode_hash_fused<K, M, 4, 3><<<g4, 448, lds4>>>(p, h); }},
@@ -201,7 +203,7 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(ref.data(), dig, nd, hipMemcpyDeviceToHost));
         CK(hipMemcpy(pref.data(), d + (n - 1) * STRIDE + K * S, M * S, hipMemcpyDeviceToHost));
         for (auto& v : vs) {
-            if (strncmp(v.name, "db", 2)) continue;
+            if (strncmp(v.name, "db", 2) && strncmp(v.name, "prio", 4)) continue;
             CK(hipMemset(dig, 0, nd));
             CK(hipMemset(d + (n - 1) * STRIDE + K * S, 0, M * S));
             v.f();
