@@ -75,24 +75,36 @@ def max_over_ranks(x: float, world: int) -> float:
 
 def cpu_baseline(k, m, S, stripes, threads):
     """Restated reference algorithm (oracle/rs_oracle_simd.c: split-nibble
-    pshufb GF MAC, one stripe per thread) on a bounded sample of the workload."""
+    pshufb GF MAC, one stripe per thread) on a bounded sample of the workload:
+    ~10 s on `threads` host cores, then ~4 s on one core (SURVEY.md §8d asks
+    for both; the reference quotes ~110 us per 1 MiB block on one core,
+    encode.rs:512)."""
     import numpy as np
     from oracle import oracle as O
     threads = max(1, min(threads, os.cpu_count() or 1))
     buf = np.zeros((stripes, k + m, S), dtype=np.uint8)
     buf[:, :k] = np.random.default_rng(0).integers(0, 256, (stripes, k, S), dtype=np.uint8)
-    O.encode_batch_mt(k, m, S, buf, None, threads)  # warm-up
-    reps, t0 = 0, time.perf_counter()
-    while True:  # ~12 s of CPU work regardless of the host's speed
-        O.encode_batch_mt(k, m, S, buf, None, threads)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el > 12.0:
-            break
-    gibs = reps * stripes * k * S / el / GiB
+
+    def timed(nthreads, nstripes, budget_s):
+        view = buf[:nstripes]
+        O.encode_batch_mt(k, m, S, view, None, nthreads)  # warm-up
+        reps, t0 = 0, time.perf_counter()
+        while True:  # a fixed amount of wall time regardless of the host's speed
+            O.encode_batch_mt(k, m, S, view, None, nthreads)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el > budget_s:
+                return reps, el, reps * nstripes * k * S / el / GiB
+
+    reps, el, gibs = timed(threads, stripes, 10.0)
+    n1 = min(stripes, 16)
+    reps1, el1, gibs1 = timed(1, n1, 4.0)
     return {"value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": f"{reps} passes x {stripes} stripes RS({k},{m}) S={S} ({el:.1f}s), "
-                      f"AVX2={'yes' if O.lib().ro_simd_level() >= 2 else 'no'}"}
+                      f"AVX2={'yes' if O.lib().ro_simd_level() >= 2 else 'no'}",
+            "value_1core": round(gibs1, 3),
+            "sample_1core": f"{reps1} passes x {n1} stripes on 1 thread ({el1:.1f}s); "
+                            f"{el1 / (reps1 * n1) * 1e6 * (1 << 20) / (k * S):.1f} us per 1 MiB of payload"}
 
 
 def main():
