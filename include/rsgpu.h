@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RSG_ABI_VERSION 2
+#define RSG_ABI_VERSION 3
 #define RSG_MAX_TOTAL_SHARDS 256 /* galois_8::Field::ORDER, erasure.rs:72 */
 #define RSG_DIGEST_BYTES 32      /* HighwayHash-256 */
 
@@ -170,7 +170,8 @@ int rsg_decode_records_dev(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t 
  * workspace of n*k*shard_len bytes (receives the data of every stripe).
  * h_status[s]: RSG_OK, RSG_ERR_TOO_FEW_SHARDS (ErasureReadQuorum) or
  * RSG_ERR_INCONSISTENT_SOURCES ("inconsistent heal source shards"); target
- * records of a failed stripe are unspecified.  Synchronous. */
+ * records of a failed stripe carry an all-zero digest header (they never
+ * verify) and unspecified bodies.  Synchronous. */
 int rsg_heal_records_dev(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t n,
                          const uint8_t *const *d_files, uint8_t *const *d_targets, int algo,
                          uint8_t *d_work, int *h_status, void *stream);
@@ -195,13 +196,31 @@ int rsg_sync(rsg_ctx *ctx, void *stream);
 
 /* ---- host-batch API: the PUT path starts and ends in host memory ----
  * Encode n stripes held in HOST memory (same addressing as the device-batch
- * API): sub-batches are pipelined over two streams (H2D data -> encode + fused
- * digests -> D2H parity + digests) and the call returns when all are done.
- * This is the batched replacement for encode_batched's per-block
- * encode_data_block calls (encode.rs:795-919); pin the buffers (rsg_pin or a
- * pinned allocation) for full PCIe bandwidth. */
+ * API): sub-batches are pipelined over the context's stream/staging slots
+ * (H2D data -> encode + fused digests -> D2H parity + digests).  This is the
+ * batched replacement for encode_batched's per-block encode_data_block calls
+ * (encode.rs:795-919); pin the buffers (rsg_pin or a pinned allocation) for
+ * full PCIe bandwidth and for the copies to run asynchronously.  With m == 0
+ * only the digests are computed; an empty shard hashes as the empty message.
+ *
+ * Asynchronous form: rsg_encode_batch_host_submit queues the job and returns
+ * a ticket at once; jobs run in submission order and the sub-batches of
+ * consecutive jobs overlap, so a producer reads and submits batch i+1 (and
+ * writes batch i-1's shards) while the GPU encodes batch i — the bounded
+ * in-flight queue of encode_batched (RUSTFS_ERASURE_ENCODE_MAX_INFLIGHT_BYTES,
+ * encode.rs:64-72) with the caller choosing the bound.  h_stripes / h_digests
+ * must stay alive and untouched until the ticket completes.
+ * rsg_poll sets *done = 1 (and releases the ticket) when the job has finished,
+ * returning its status; rsg_wait blocks until then.  An unknown or already
+ * released ticket is RSG_ERR_INVALID_ARG.  rsg_encode_batch_host = submit +
+ * wait. */
 int rsg_encode_batch_host(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t n, uint8_t *h_stripes,
                           size_t shard_pitch, size_t stripe_stride, uint8_t *h_digests, int algo);
+int rsg_encode_batch_host_submit(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t n, uint8_t *h_stripes,
+                                 size_t shard_pitch, size_t stripe_stride, uint8_t *h_digests, int algo,
+                                 uint64_t *ticket);
+int rsg_poll(rsg_ctx *ctx, uint64_t ticket, int *done);
+int rsg_wait(rsg_ctx *ctx, uint64_t ticket);
 
 /* Page-lock / release host memory for DMA (hipHostRegister). */
 int rsg_pin(void *ptr, size_t bytes);

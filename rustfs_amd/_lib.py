@@ -55,6 +55,7 @@ EXPORTED = (
     "rsg_hash", "rsg_encode_batch_dev", "rsg_reconstruct_batch_dev", "rsg_verify_batch_dev",
     "rsg_hash_batch_dev", "rsg_sync", "rsg_encode_batch_host", "rsg_pin", "rsg_unpin",
     "rsg_decode_records_dev", "rsg_heal_records_dev", "rsg_bitrot_verify_dev",
+    "rsg_encode_batch_host_submit", "rsg_poll", "rsg_wait",
 )
 
 
@@ -105,6 +106,9 @@ def load():
         L.rsg_hash_batch_dev.argtypes = [P, I, P, S, S, S, P, P]
         L.rsg_sync.argtypes = [P, P]
         L.rsg_encode_batch_host.argtypes = [P, I, I, S, S, P, S, S, P, I]
+        L.rsg_encode_batch_host_submit.argtypes = [P, I, I, S, S, P, S, S, P, I, ctypes.POINTER(ctypes.c_uint64)]
+        L.rsg_poll.argtypes = [P, ctypes.c_uint64, ctypes.POINTER(I)]
+        L.rsg_wait.argtypes = [P, ctypes.c_uint64]
         L.rsg_decode_records_dev.argtypes = [P, I, I, S, S, P, I, I, P, P, P]
         L.rsg_heal_records_dev.argtypes = [P, I, I, S, S, P, P, I, P, P, P]
         L.rsg_bitrot_verify_dev.argtypes = [P, I, S, P, P, S, S, S, P, P]

@@ -234,17 +234,32 @@ void plan_row(const Codec& cd, const DecodePlan& p, int idx, uint8_t* row) {
     }
 }
 
-RowSet reconstruct_rows(const Codec& cd, const DecodePlan& p, const uint8_t* present, int mode, uint64_t pitch) {
-    RowSet rs;
-    rs.C = cd.k;
-    for (int s : p.survivors) rs.in_off.push_back((uint64_t)s * pitch);
+bool is_survivor(const DecodePlan& p, int idx) {
+    return std::find(p.survivors.begin(), p.survivors.end(), idx) != p.survivors.end();
+}
+
+// Shards a reconstruct in `mode` writes.  RSG_RECONSTRUCT_REENCODE_PARITY
+// re-encodes every parity shard (erasure.rs:425-428, 505-561), but a parity
+// shard that is one of the survivors re-encodes to itself byte for byte
+// (G[p] * inv is the unit row selecting it, whatever the other shards hold),
+// so it is not a target: no launch ever overwrites a shard another launch of
+// the same product still reads (chained C > 16 inputs, R > 8 rows).
+std::vector<int> reconstruct_targets(const Codec& cd, const DecodePlan& p, const uint8_t* present, int mode) {
     std::vector<int> targets;
     for (int i = 0; i < cd.k + cd.m; ++i) {
         const bool is_data = i < cd.k;
         if (is_data && !present[i]) targets.push_back(i);
         else if (!is_data && mode == RSG_RECONSTRUCT_MISSING && !present[i]) targets.push_back(i);
-        else if (!is_data && mode == RSG_RECONSTRUCT_REENCODE_PARITY) targets.push_back(i);
+        else if (!is_data && mode == RSG_RECONSTRUCT_REENCODE_PARITY && !is_survivor(p, i)) targets.push_back(i);
     }
+    return targets;
+}
+
+RowSet reconstruct_rows(const Codec& cd, const DecodePlan& p, const uint8_t* present, int mode, uint64_t pitch) {
+    RowSet rs;
+    rs.C = cd.k;
+    for (int s : p.survivors) rs.in_off.push_back((uint64_t)s * pitch);
+    const std::vector<int> targets = reconstruct_targets(cd, p, present, mode);
     rs.R = (int)targets.size();
     rs.coef.assign((size_t)rs.R * cd.k, 0);
     for (int r = 0; r < rs.R; ++r) {
@@ -256,6 +271,8 @@ RowSet reconstruct_rows(const Codec& cd, const DecodePlan& p, const uint8_t* pre
 
 // --------------------------------------------------------------------------
 // GPU dispatch of out = M * in over n stripes.
+
+uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
 int hip_status(hipError_t e) {
     if (e == hipSuccess) return RSG_OK;
@@ -295,9 +312,50 @@ bool fused_enabled() {
 }
 
 int apply_rows(const RowSet& rs, const uint8_t* base, uint8_t* out_base, uint64_t stride, uint64_t out_stride,
+               uint64_t len, uint64_t n, uint32_t mode, uint8_t* ok_flags, hipStream_t stream);
+
+// Compare mode over more than kMaxC inputs (k > 16: RS(20,4), RS(192,64), ...).
+// A chained product (STORE, then XOR launches) cannot compare inside the
+// chain, so the rows are computed into stream-ordered scratch (groups of
+// stripes, <= ~256 MiB) and compared against their targets with identity rows
+// (<= kMaxR per launch).  Same verdict as the one-pass compare: ok_flags[s]
+// cleared where any row differs (erasure.rs:430-441).
+int apply_rows_compare_wide(const RowSet& rs, const uint8_t* base, uint8_t* out_base, uint64_t stride,
+                            uint64_t out_stride, uint64_t len, uint64_t n, uint8_t* ok_flags, hipStream_t stream) {
+    const uint64_t pitch = round_up(len, 256);
+    const uint64_t per_stripe = pitch * (uint64_t)rs.R;
+    const uint64_t group = std::max<uint64_t>(1, std::min<uint64_t>(n, (256ull << 20) / per_stripe));
+    uint8_t* tmp = nullptr;
+    int st = hip_status(hipMallocAsync((void**)&tmp, (size_t)(group * per_stripe), stream));
+    if (st) return st;
+    RowSet enc = rs;
+    for (int r = 0; r < rs.R; ++r) enc.out_off[r] = (uint64_t)r * pitch;
+    for (uint64_t s0 = 0; s0 < n && !st; s0 += group) {
+        const uint64_t cnt = std::min(group, n - s0);
+        st = apply_rows(enc, base + s0 * stride, tmp, stride, per_stripe, len, cnt, rsg::GF_MODE_STORE, nullptr,
+                        stream);
+        for (int r0 = 0; r0 < rs.R && !st; r0 += rsg::kMaxR) {
+            RowSet id;
+            id.R = id.C = std::min(rsg::kMaxR, rs.R - r0);
+            id.coef.assign((size_t)id.R * id.C, 0);
+            for (int i = 0; i < id.R; ++i) {
+                id.coef[(size_t)i * id.C + i] = 1;
+                id.in_off.push_back((uint64_t)(r0 + i) * pitch);
+                id.out_off.push_back(rs.out_off[r0 + i]);
+            }
+            st = apply_rows(id, tmp, out_base + s0 * out_stride, per_stripe, out_stride, len, cnt,
+                            rsg::GF_MODE_COMPARE, ok_flags + s0, stream);
+        }
+    }
+    const int fst = hip_status(hipFreeAsync(tmp, stream));
+    return st ? st : fst;
+}
+
+int apply_rows(const RowSet& rs, const uint8_t* base, uint8_t* out_base, uint64_t stride, uint64_t out_stride,
                uint64_t len, uint64_t n, uint32_t mode, uint8_t* ok_flags, hipStream_t stream) {
     if (rs.R == 0 || n == 0 || len == 0) return RSG_OK;
-    if (mode == rsg::GF_MODE_COMPARE && rs.C > rsg::kMaxC) return RSG_ERR_UNSUPPORTED;
+    if (mode == rsg::GF_MODE_COMPARE && rs.C > rsg::kMaxC)
+        return apply_rows_compare_wide(rs, base, out_base, stride, out_stride, len, n, ok_flags, stream);
     // The vector kernel's 16-byte accesses need no alignment (ld16/st16 in
     // rs_kernels.hip); only the len % 16 tail of each shard takes the byte path.
     const uint64_t units = len / 16;
@@ -380,7 +438,6 @@ int hash_messages(int algo, const uint8_t* d_data, uint64_t len, uint64_t n, uin
     return hip_status(rsg::launch_hh256(h, stream));
 }
 
-uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
 }  // namespace
 
@@ -426,11 +483,22 @@ struct rsg_ctx {
     HostLane lanes[kHostLanes];
     std::atomic<unsigned> next_lane{0};
 
-    // host-batch pipeline (rsg_encode_batch_host): two stream/staging pairs
+    // host-batch pipeline (rsg_encode_batch_host_submit): kPipeSlots
+    // stream/staging pairs used round-robin by consecutive sub-batches of all
+    // submitted jobs, so a slot's staging buffer is reused only after its own
+    // stream has finished the previous sub-batch (stream order); a job's ticket
+    // maps to one event per slot it used.
+    static constexpr int kPipeSlots = 3;
     std::mutex pipe_mu;
-    hipStream_t pipe_stream[2] = {nullptr, nullptr};
-    uint8_t* d_stage[2] = {nullptr, nullptr};
+    hipStream_t pipe_stream[kPipeSlots] = {};
+    uint8_t* d_stage[kPipeSlots] = {};
     size_t stage_cap = 0;
+    unsigned next_slot = 0;
+    uint64_t next_ticket = 1;
+    struct Job {
+        std::vector<hipEvent_t> done;
+    };
+    std::map<uint64_t, Job> jobs;
 
     int ensure_scratch(size_t bytes) {
         if (bytes <= scratch_cap) return RSG_OK;
@@ -444,19 +512,25 @@ struct rsg_ctx {
         return RSG_OK;
     }
 
+    // pipe_mu held.  Growing the staging buffers waits for every sub-batch in
+    // flight (they may still be reading the old ones).
     int ensure_pipeline(size_t bytes) {
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < kPipeSlots; ++i)
             if (!pipe_stream[i]) {
                 hipError_t e = hipStreamCreateWithFlags(&pipe_stream[i], hipStreamNonBlocking);
                 if (e != hipSuccess) return hip_status(e);
             }
         if (bytes <= stage_cap) return RSG_OK;
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < kPipeSlots; ++i) {
+            hipError_t e = hipStreamSynchronize(pipe_stream[i]);
+            if (e != hipSuccess) return hip_status(e);
+        }
+        for (int i = 0; i < kPipeSlots; ++i) {
             if (d_stage[i]) (void)hipFree(d_stage[i]);
             d_stage[i] = nullptr;
         }
         stage_cap = 0;
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < kPipeSlots; ++i) {
             hipError_t e = hipMalloc((void**)&d_stage[i], bytes);
             if (e != hipSuccess) return hip_status(e);
         }
@@ -593,13 +667,15 @@ void rsg_destroy(rsg_ctx* ctx) {
         }
         if (l.d_buf) (void)hipFree(l.d_buf);
     }
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < rsg_ctx::kPipeSlots; ++i) {
         if (ctx->pipe_stream[i]) {
             (void)hipStreamSynchronize(ctx->pipe_stream[i]);
             (void)hipStreamDestroy(ctx->pipe_stream[i]);
         }
         if (ctx->d_stage[i]) (void)hipFree(ctx->d_stage[i]);
     }
+    for (auto& j : ctx->jobs)
+        for (hipEvent_t e : j.second.done) (void)hipEventDestroy(e);
     delete ctx;
 }
 
@@ -615,57 +691,134 @@ int rsg_unpin(void* ptr) {
     return hip_status(hipHostUnregister(ptr));
 }
 
-// Host-memory batch encode: stripes in host memory (pinned for full PCIe rate),
-// a3 layout.  Sub-batches of `chunk` stripes alternate over two stream/staging
-// pairs: H2D of the data shards (one 2-D copy), encode (+ fused digests), D2H of
-// parity (+ digests); the copy engines overlap the kernel of the other pair.
-int rsg_encode_batch_host(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n, uint8_t* h_stripes,
-                          size_t shard_pitch, size_t stripe_stride, uint8_t* h_digests, int algo) {
+// Host-memory batch encode (the PUT path: encode_batched's producer,
+// encode.rs:795-919), asynchronous.  Sub-batches of `chunk` stripes go
+// round-robin over the context's kPipeSlots stream/staging pairs: H2D of the
+// data shards (one 2-D copy), encode (+ fused digests), D2H of parity (+
+// digests); the copy engines of one slot overlap the kernels of the others,
+// and the sub-batches of consecutive jobs keep the link busy back to back.
+// The ticket completes when every sub-batch has landed in host memory; the
+// caller keeps h_stripes / h_digests alive and untouched until then (the
+// reference's EncodedBlock owns its Bytes the same way, encode.rs:64-72).
+int rsg_encode_batch_host_submit(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n, uint8_t* h_stripes,
+                                 size_t shard_pitch, size_t stripe_stride, uint8_t* h_digests, int algo,
+                                 uint64_t* ticket) {
     int st = enter(ctx);
     if (st) return st;
+    if (!ticket) return RSG_ERR_INVALID_ARG;
+    *ticket = 0;
     if ((st = check_geometry(k, m))) return st;
     if (n && !h_stripes) return RSG_ERR_INVALID_ARG;
     if (shard_pitch < shard_len) return RSG_ERR_INCONSISTENT_LENGTH;
     if (stripe_stride < (size_t)(k + m) * shard_pitch) return RSG_ERR_INVALID_ARG;
-    if (n == 0 || m == 0 || shard_len == 0) return RSG_OK;
     const bool want_hash = h_digests && algo != RSG_HASH_NONE;
+    if (want_hash && !hash_key(algo)) return RSG_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> g(ctx->pipe_mu);
-    // device layout: compact a3 stripes, 256-B aligned shards
-    const uint64_t dpitch = round_up(shard_len, 256);
-    const uint64_t dstride = dpitch * (k + m);
-    const uint64_t target = 96ull << 20;  // ~96 MiB per sub-batch
-    const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(n, target / dstride));
-    const uint64_t dig_bytes = want_hash ? chunk * (k + m) * 32 : 0;
-    if ((st = ctx->ensure_pipeline((size_t)(chunk * dstride + dig_bytes)))) return st;
-    const size_t dpitch_data = (shard_pitch == dpitch) ? (size_t)(k * dpitch) : 0;
-    for (uint64_t s0 = 0, it = 0; s0 < n; s0 += chunk, ++it) {
-        const int b = (int)(it & 1);
-        hipStream_t s = ctx->pipe_stream[b];
-        const uint64_t cnt = std::min<uint64_t>(chunk, n - s0);
-        uint8_t* hbase = h_stripes + s0 * stripe_stride;
-        uint8_t* d = ctx->d_stage[b];
-        if (dpitch_data) {  // data shards contiguous per stripe on both sides
-            st = hip_status(hipMemcpy2DAsync(d, dstride, hbase, stripe_stride, dpitch_data, cnt,
-                                             hipMemcpyHostToDevice, s));
-        } else {
-            for (int i = 0; i < k && !st; ++i)
-                st = hip_status(hipMemcpy2DAsync(d + i * dpitch, dstride, hbase + i * shard_pitch, stripe_stride,
-                                                 shard_len, cnt, hipMemcpyHostToDevice, s));
+    rsg_ctx::Job job;
+    // nothing to move: parity of m = 0 is empty; digests are still computed
+    // (an empty shard hashes to the digest of the empty message)
+    const bool work = n > 0 && ((m > 0 && shard_len > 0) || want_hash);
+    if (work) {
+        // device layout: compact a3 stripes, 256-B aligned shards
+        const uint64_t dpitch = std::max<uint64_t>(256, round_up(shard_len, 256));
+        const uint64_t dstride = dpitch * (k + m);
+        const uint64_t target = 96ull << 20;  // ~96 MiB per sub-batch
+        const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(n, target / dstride));
+        const uint64_t dig_bytes = want_hash ? chunk * (k + m) * 32 : 0;
+        if ((st = ctx->ensure_pipeline((size_t)(chunk * dstride + dig_bytes)))) return st;
+        const size_t dpitch_data = (shard_pitch == dpitch) ? (size_t)(k * dpitch) : 0;
+        bool used[rsg_ctx::kPipeSlots] = {};
+        for (uint64_t s0 = 0; s0 < n; s0 += chunk) {
+            const int b = (int)(ctx->next_slot++ % rsg_ctx::kPipeSlots);
+            used[b] = true;
+            hipStream_t s = ctx->pipe_stream[b];
+            const uint64_t cnt = std::min<uint64_t>(chunk, n - s0);
+            uint8_t* hbase = h_stripes + s0 * stripe_stride;
+            uint8_t* d = ctx->d_stage[b];
+            if (shard_len == 0) {
+            } else if (dpitch_data) {  // data shards contiguous per stripe on both sides
+                st = hip_status(hipMemcpy2DAsync(d, dstride, hbase, stripe_stride, dpitch_data, cnt,
+                                                 hipMemcpyHostToDevice, s));
+            } else {
+                for (int i = 0; i < k && !st; ++i)
+                    st = hip_status(hipMemcpy2DAsync(d + i * dpitch, dstride, hbase + i * shard_pitch,
+                                                     stripe_stride, shard_len, cnt, hipMemcpyHostToDevice, s));
+            }
+            if (st) return st;
+            uint8_t* ddig = want_hash ? d + chunk * dstride : nullptr;
+            if ((st = rsg_encode_batch_dev(ctx, k, m, shard_len, cnt, d, dpitch, dstride, ddig, algo, s))) return st;
+            for (int p = 0; p < m && shard_len && !st; ++p)
+                st = hip_status(hipMemcpy2DAsync(hbase + (k + p) * shard_pitch, stripe_stride, d + (k + p) * dpitch,
+                                                 dstride, shard_len, cnt, hipMemcpyDeviceToHost, s));
+            if (!st && want_hash)
+                st = hip_status(hipMemcpyAsync(h_digests + s0 * (k + m) * 32, ddig, cnt * (k + m) * 32,
+                                               hipMemcpyDeviceToHost, s));
+            if (st) return st;
         }
-        if (st) return st;
-        uint8_t* ddig = want_hash ? d + chunk * dstride : nullptr;
-        if ((st = rsg_encode_batch_dev(ctx, k, m, shard_len, cnt, d, dpitch, dstride, ddig, algo, s))) return st;
-        for (int p = 0; p < m && !st; ++p)
-            st = hip_status(hipMemcpy2DAsync(hbase + (k + p) * shard_pitch, stripe_stride, d + (k + p) * dpitch,
-                                             dstride, shard_len, cnt, hipMemcpyDeviceToHost, s));
-        if (!st && want_hash)
-            st = hip_status(hipMemcpyAsync(h_digests + s0 * (k + m) * 32, ddig, cnt * (k + m) * 32,
-                                           hipMemcpyDeviceToHost, s));
-        if (st) return st;
+        for (int b = 0; b < rsg_ctx::kPipeSlots; ++b) {
+            if (!used[b]) continue;
+            hipEvent_t e;
+            if ((st = hip_status(hipEventCreateWithFlags(&e, hipEventDisableTiming)))) return st;
+            job.done.push_back(e);
+            if ((st = hip_status(hipEventRecord(e, ctx->pipe_stream[b])))) break;
+        }
+        if (st) {
+            for (hipEvent_t e : job.done) (void)hipEventDestroy(e);
+            return st;
+        }
     }
-    for (int i = 0; i < 2; ++i)
-        if ((st = hip_status(hipStreamSynchronize(ctx->pipe_stream[i])))) return st;
+    *ticket = ctx->next_ticket++;
+    ctx->jobs.emplace(*ticket, std::move(job));
     return RSG_OK;
+}
+
+namespace {
+// Query (wait = false) or finish (wait = true) a ticket; a finished ticket is
+// released.  *done = 1 once every sub-batch of the job has completed.
+int finish_ticket(rsg_ctx* ctx, uint64_t ticket, bool wait, int* done) {
+    int st = enter(ctx);
+    if (st) return st;
+    if (done) *done = 0;
+    std::vector<hipEvent_t> evs;
+    {
+        std::lock_guard<std::mutex> g(ctx->pipe_mu);
+        auto it = ctx->jobs.find(ticket);
+        if (it == ctx->jobs.end()) return RSG_ERR_INVALID_ARG;
+        evs = it->second.done;
+    }
+    int res = RSG_OK;
+    for (hipEvent_t e : evs) {
+        const hipError_t q = wait ? hipEventSynchronize(e) : hipEventQuery(e);
+        if (q == hipErrorNotReady) {  // still in flight (poll only)
+            (void)hipGetLastError();  // not an error: keep it out of the next launch check
+            return RSG_OK;
+        }
+        if (q != hipSuccess && !res) res = hip_status(q);
+    }
+    std::lock_guard<std::mutex> g(ctx->pipe_mu);
+    auto it = ctx->jobs.find(ticket);
+    if (it == ctx->jobs.end()) return RSG_ERR_INVALID_ARG;  // finished by a concurrent caller
+    for (hipEvent_t e : it->second.done) (void)hipEventDestroy(e);
+    ctx->jobs.erase(it);
+    if (done) *done = 1;
+    return res;
+}
+}  // namespace
+
+int rsg_poll(rsg_ctx* ctx, uint64_t ticket, int* done) {
+    if (!done) return RSG_ERR_INVALID_ARG;
+    return finish_ticket(ctx, ticket, false, done);
+}
+
+int rsg_wait(rsg_ctx* ctx, uint64_t ticket) { return finish_ticket(ctx, ticket, true, nullptr); }
+
+int rsg_encode_batch_host(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n, uint8_t* h_stripes,
+                          size_t shard_pitch, size_t stripe_stride, uint8_t* h_digests, int algo) {
+    uint64_t t = 0;
+    int st = rsg_encode_batch_host_submit(ctx, k, m, shard_len, n, h_stripes, shard_pitch, stripe_stride, h_digests,
+                                          algo, &t);
+    if (st) return st;
+    return rsg_wait(ctx, t);
 }
 
 int rsg_matrix(int k, int m, uint8_t* out) {
@@ -1089,6 +1242,22 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
         for (uint64_t x = 0; x < n; ++x)
             if (h_status[x] == RSG_OK && !ok[x]) h_status[x] = RSG_ERR_INCONSISTENT_SOURCES;
     }
+    // A failed stripe's target records hold unverified bytes: their digest
+    // headers are zeroed so they can never pass bitrot verification even if a
+    // caller ignores h_status (the reference writes nothing for a failed heal).
+    for (uint64_t s0 = 0; s0 < n;) {
+        if (h_status[s0] == RSG_OK) {
+            ++s0;
+            continue;
+        }
+        uint64_t s1 = s0 + 1;
+        while (s1 < n && h_status[s1] != RSG_OK) ++s1;
+        for (int i = 0; i < t; ++i)
+            if (d_targets[i] &&
+                (st = hip_status(hipMemset2DAsync(d_targets[i] + s0 * rec, rec, 0, 32, s1 - s0, s))))
+                return st;
+        s0 = s1;
+    }
     return hip_status(hipStreamSynchronize(s));
 }
 
@@ -1268,14 +1437,7 @@ int rsg_reconstruct(rsg_ctx* ctx, int k, int m, size_t shard_len, uint8_t* const
     if (!plan) return RSG_ERR_TOO_FEW_SHARDS;
     RowSet rs = reconstruct_rows(*cd, *plan, present, mode, 0);
     if (rs.R == 0) return RSG_OK;
-
-    std::vector<int> targets;
-    for (int i = 0; i < k + m; ++i) {
-        const bool is_data = i < k;
-        if ((is_data && !present[i]) || (!is_data && mode == RSG_RECONSTRUCT_MISSING && !present[i]) ||
-            (!is_data && mode == RSG_RECONSTRUCT_REENCODE_PARITY))
-            targets.push_back(i);
-    }
+    const std::vector<int> targets = reconstruct_targets(*cd, *plan, present, mode);
     HostLane* lane;
     auto g = acquire_lane(ctx, lane);
     const uint64_t pitch = round_up(shard_len, 256);

@@ -68,6 +68,16 @@ def _writable(buf) -> np.ndarray:
     return a
 
 
+def _shard_view(buf) -> np.ndarray:
+    """A shard as the flat uint8 byte run the C ABI reads and writes through
+    one pointer: a strided view (buf[:, i]) or another dtype would make the
+    library touch bytes outside the caller's shard, so those are rejected."""
+    a = _as_array(buf)
+    if a.dtype != np.uint8 or not a.flags.c_contiguous:
+        raise TypeError("shard buffers must be C-contiguous uint8 (bytes, bytearray or numpy uint8 arrays)")
+    return a
+
+
 # ---------------------------------------------------------------------------
 
 class ReedSolomonEncoder:
@@ -94,7 +104,7 @@ class ReedSolomonEncoder:
             return
         if len(shards) != self.total:
             raise RsgError(_lib.RSG_ERR_INVALID_SHARD_COUNT, "Reed-Solomon encode failed")
-        arrs = [_as_array(s) for s in shards]
+        arrs = [_shard_view(s) for s in shards]
         n = arrs[0].size
         if any(a.size != n for a in arrs):
             raise RsgError(_lib.RSG_ERR_INCONSISTENT_LENGTH, "Reed-Solomon encode failed")
@@ -134,7 +144,7 @@ class ReedSolomonEncoder:
             elif is_parity and mode == _lib.RSG_RECONSTRUCT_REENCODE_PARITY and not _as_array(s).flags.writeable:
                 s = bytearray(s)  # re-encoded parity replaces the present buffer
                 shards[i] = s
-            arrs.append(_as_array(s))
+            arrs.append(_shard_view(s))
         st = _lib.load().rsg_reconstruct(self._ctx().handle, self.data_shards, self.parity_shards, n,
                                          _ptrs(arrs), (ctypes.c_uint8 * self.total)(*present), mode)
         check(st, "Reed-Solomon reconstruct failed")
@@ -307,6 +317,27 @@ class Erasure:
                           algo: int = _lib.RSG_HASH_HIGHWAY256S) -> None:
         """Host-memory batch (n, k+m, S) uint8, parity written in place; pipelined
         H2D -> encode(+digests) -> D2H inside librsgpu (rsg_encode_batch_host)."""
+        n, t, S, d = self._host_batch_args(stripes, digests)
+        check(_lib.load().rsg_encode_batch_host(
+            _lib.context(self._device).handle, self.data_shards, self.parity_shards, S, n, stripes.ctypes.data,
+            S, t * S, d, algo if d else _lib.RSG_HASH_NONE), "Reed-Solomon encode failed")
+
+    def encode_batch_host_submit(self, stripes: np.ndarray, digests: Optional[np.ndarray] = None,
+                                 algo: int = _lib.RSG_HASH_HIGHWAY256S) -> "HostBatchTicket":
+        """Asynchronous encode_batch_host (rsg_encode_batch_host_submit): returns
+        at once with a ticket; the arrays must stay alive and untouched until
+        the ticket is done (poll() / wait()).  Jobs run in submission order and
+        overlap each other's copies and kernels (encode_batched's bounded
+        in-flight queue, encode.rs:64-72, 795-919)."""
+        n, t, S, d = self._host_batch_args(stripes, digests)
+        tk = ctypes.c_uint64(0)
+        ctx = _lib.context(self._device)
+        check(_lib.load().rsg_encode_batch_host_submit(
+            ctx.handle, self.data_shards, self.parity_shards, S, n, stripes.ctypes.data, S, t * S, d,
+            algo if d else _lib.RSG_HASH_NONE, ctypes.byref(tk)), "Reed-Solomon encode failed")
+        return HostBatchTicket(ctx, tk.value, (stripes, digests))
+
+    def _host_batch_args(self, stripes, digests):
         if stripes.dtype != np.uint8 or stripes.ndim != 3 or not stripes.flags.c_contiguous:
             raise TypeError("stripes must be a C-contiguous uint8 array (n, k+m, S)")
         n, t, S = stripes.shape
@@ -317,9 +348,7 @@ class Erasure:
             if digests.shape != (n, t, 32) or digests.dtype != np.uint8 or not digests.flags.c_contiguous:
                 raise TypeError("digests must be a C-contiguous uint8 array (n, k+m, 32)")
             d = digests.ctypes.data
-        check(_lib.load().rsg_encode_batch_host(
-            _lib.context(self._device).handle, self.data_shards, self.parity_shards, S, n, stripes.ctypes.data,
-            S, t * S, d, algo if d else _lib.RSG_HASH_NONE), "Reed-Solomon encode failed")
+        return n, t, S, d
 
     def decode_records_batch(self, files: Sequence, shard_len: int, n: int, verify_surplus: bool = True,
                              algo: int = _lib.RSG_HASH_HIGHWAY256S, out=None, stream=None):
@@ -401,6 +430,41 @@ class Erasure:
             stripes.data_ptr(), S, t * S, ok.data_ptr(), _stream_of(stripes, stream)),
             "Reed-Solomon verify failed")
         return ok
+
+
+class HostBatchTicket:
+    """A submitted host-batch encode (rsg_encode_batch_host_submit).  Holds
+    references to the job's arrays until it completes."""
+
+    def __init__(self, ctx, ticket: int, keep):
+        self._ctx = ctx
+        self.ticket = ticket
+        self._keep = keep
+        self._done = False
+
+    def poll(self) -> bool:
+        """True once the job has finished (raises its error, if any)."""
+        if self._done:
+            return True
+        done = ctypes.c_int(0)
+        check(_lib.load().rsg_poll(self._ctx.handle, self.ticket, ctypes.byref(done)), "Reed-Solomon encode failed")
+        if done.value:
+            self._done, self._keep = True, None
+        return self._done
+
+    def wait(self) -> None:
+        if self._done:
+            return
+        st = _lib.load().rsg_wait(self._ctx.handle, self.ticket)
+        self._done, self._keep = True, None
+        check(st, "Reed-Solomon encode failed")
+
+    def __del__(self):  # never leave a job writing into freed arrays
+        try:
+            if not self._done:
+                self.wait()
+        except Exception:
+            pass
 
 
 # ---------------------------------------------------------------------------

@@ -1,0 +1,88 @@
+"""Multi-GPU readiness on one device: what the driver's 8-GPU run relies on.
+
+Stripes are independent, so each rank owns a context and a
+stream and encodes its contiguous slice with no collective.  These tests run
+two contexts with their own streams concurrently on device 0 through the
+device-batch ABI, and the host-side multi-device splitter
+(dispatch.encode_host_multi) — every result checked against the oracle.
+"""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_two_contexts_two_streams_concurrently(gpu, oracle):
+    import torch
+    from rustfs_amd import _lib
+    from rustfs_amd.dispatch import split_batch
+    k, m, S, total = 8, 4, 131072, 96
+    g = torch.Generator(device="cuda").manual_seed(3)
+    st = torch.zeros((total, k + m, S), dtype=torch.uint8, device="cuda")
+    st[:, :k] = torch.randint(0, 256, (total, k, S), dtype=torch.uint8, device="cuda", generator=g)
+    dig = torch.zeros((total, k + m, 32), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    ctxs = [_lib.Context(0), _lib.Context(0)]  # one per "rank"
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    errs = []
+
+    def rank(r):
+        try:
+            s0, cnt = split_batch(total, 2, r)
+            for _ in range(3):  # repeated launches interleave with the other rank's
+                rc = _lib.load().rsg_encode_batch_dev(
+                    ctxs[r].handle, k, m, S, cnt, st[s0].data_ptr(), S, (k + m) * S, dig[s0].data_ptr(),
+                    _lib.RSG_HASH_HIGHWAY256S, streams[r].cuda_stream)
+                _lib.check(rc)
+            _lib.check(_lib.load().rsg_sync(ctxs[r].handle, streams[r].cuda_stream))
+        except Exception as exc:  # surfaced below
+            errs.append(repr(exc))
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    host, hd = st.cpu().numpy(), dig.cpu().numpy()
+    for s in (0, 47, 48, 95):  # both sides of the split
+        ref = host[s].copy()
+        ref[k:] = 0
+        oracle.encode(k, m, ref)
+        assert np.array_equal(ref, host[s]), s
+        for i in range(k + m):
+            assert hd[s, i].tobytes() == oracle.hh256s(ref[i]), (s, i)
+    for c in ctxs:
+        c.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_encode_host_multi(gpu, oracle, world):
+    """dispatch.encode_host_multi: one host thread per (device) slice; on a
+    one-GPU box every slice lands on device 0, as the 2-rank rehearsal does."""
+    import torch
+    from rustfs_amd import Erasure
+    from rustfs_amd.dispatch import encode_host_multi
+    k, m, S, n = 8, 4, 65536, 31
+    st = torch.zeros((n, k + m, S), dtype=torch.uint8).pin_memory().numpy()
+    st[:, :k] = np.random.default_rng(world).integers(0, 256, (n, k, S), dtype=np.uint8)
+    dig = np.zeros((n, k + m, 32), dtype=np.uint8)
+    encode_host_multi([Erasure(k, m, k * S, device=0) for _ in range(world)], st, dig)
+    for s in range(n):
+        ref = st[s].copy()
+        ref[k:] = 0
+        oracle.encode(k, m, ref)
+        assert np.array_equal(ref, st[s]), s
+        assert dig[s, k + m - 1].tobytes() == oracle.hh256s(ref[k + m - 1]), s
+        assert dig[s, 0].tobytes() == oracle.hh256s(ref[0]), s
+
+
+def test_device_count_and_context_per_device(gpu):
+    from rustfs_amd import _lib
+    n = _lib.device_count()
+    assert n >= 1
+    h = ctypes.c_void_p()
+    assert _lib.load().rsg_create(n, ctypes.byref(h)) == _lib.RSG_ERR_NO_DEVICE  # ordinal past the last device
