@@ -115,13 +115,19 @@ __device__ __forceinline__ void gf_store(const GfApplyParams& p, uint8_t* obase,
     }
 }
 
-template <int C, int R>
-__global__ __launch_bounds__(256) void k_gf_apply_vec(const GfApplyParams p) {
+// B threads per workgroup.  One-wave workgroups (B = 64) are the default:
+// consecutive workgroups still sweep one stripe's columns in order, but waves
+// are replaced one at a time instead of four together; RS(8,4) n = 4096 runs
+// 1.06 ms against 1.09-1.15 ms at B = 256 (tools/kbench/block_probe.hip,
+// profiles/r02/experiments/blk1_block_probe.txt).  RSG_VEC_BLOCK=256 selects
+// the 256-thread form for A/B runs.
+template <int C, int R, int B>
+__global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(2))) void k_gf_apply_vec(const GfApplyParams p) {
     const uint32_t stripe = blockIdx.x / p.chunks_per_stripe;
     const uint32_t chunk = blockIdx.x - stripe * p.chunks_per_stripe;
     const uint8_t* sbase = p.base + (uint64_t)stripe * p.stripe_stride;
     uint8_t* obase = p.out_base + (uint64_t)stripe * p.out_stripe_stride;
-    const uint32_t u = chunk * 256u + threadIdx.x;
+    const uint32_t u = chunk * (uint32_t)B + threadIdx.x;
     if (u >= p.units) return;
     const uint64_t off = (uint64_t)u * 16u;
     uint4 x[C];
@@ -143,14 +149,14 @@ __global__ __launch_bounds__(256) void k_gf_apply_vec(const GfApplyParams p) {
 // peak, in groups of 8 (128 B in flight per lane, 105 VGPRs) at 72-73 %
 // (tools/kbench/xor3_variants.hip).  For C <= 8, R <= 4 the unrolled kernel is
 // faster and stays the default there.
-template <int R>
-__global__ __launch_bounds__(256) void k_gf_apply_loop(const GfApplyParams p) {
+template <int R, int B>
+__global__ __launch_bounds__(B) void k_gf_apply_loop(const GfApplyParams p) {
     constexpr int G = 8;
     const uint32_t stripe = blockIdx.x / p.chunks_per_stripe;
     const uint32_t chunk = blockIdx.x - stripe * p.chunks_per_stripe;
     const uint8_t* sbase = p.base + (uint64_t)stripe * p.stripe_stride;
     uint8_t* obase = p.out_base + (uint64_t)stripe * p.out_stripe_stride;
-    const uint32_t u = chunk * 256u + threadIdx.x;
+    const uint32_t u = chunk * (uint32_t)B + threadIdx.x;
     if (u >= p.units) return;
     const uint64_t off = (uint64_t)u * 16u;
     const uint32_t C = p.C;
@@ -837,50 +843,61 @@ void k_encode_hash_ring(const GfApplyParams p, const HashParams h, const uint32_
 
 using GfKernel = void (*)(const GfApplyParams);
 
-template <int C>
+template <int C, int B>
 static GfKernel pick_vec_r(int R) {
     switch (R) {
-        case 1: return k_gf_apply_vec<C, 1>;
-        case 2: return k_gf_apply_vec<C, 2>;
-        case 3: return k_gf_apply_vec<C, 3>;
-        case 4: return k_gf_apply_vec<C, 4>;
+        case 1: return k_gf_apply_vec<C, 1, B>;
+        case 2: return k_gf_apply_vec<C, 2, B>;
+        case 3: return k_gf_apply_vec<C, 3, B>;
+        case 4: return k_gf_apply_vec<C, 4, B>;
     }
     return nullptr;
 }
 
 // Unrolled kernel for C <= 8 inputs and R <= 4 outputs, the rolled one above
 // (k_gf_apply_loop); RSG_ROLLED=1 forces the rolled kernel for A/B runs.
-static GfKernel pick_vec(int C, int R) {
+template <int B>
+static GfKernel pick_vec_b(int C, int R) {
     static const bool force_rolled = [] {
         const char* s = std::getenv("RSG_ROLLED");
         return s && s[0] == '1';
     }();
     if (C <= 8 && R <= 4 && !force_rolled) {
         switch (C) {
-            case 1: return pick_vec_r<1>(R);
-            case 2: return pick_vec_r<2>(R);
-            case 3: return pick_vec_r<3>(R);
-            case 4: return pick_vec_r<4>(R);
-            case 5: return pick_vec_r<5>(R);
-            case 6: return pick_vec_r<6>(R);
-            case 7: return pick_vec_r<7>(R);
-            case 8: return pick_vec_r<8>(R);
+            case 1: return pick_vec_r<1, B>(R);
+            case 2: return pick_vec_r<2, B>(R);
+            case 3: return pick_vec_r<3, B>(R);
+            case 4: return pick_vec_r<4, B>(R);
+            case 5: return pick_vec_r<5, B>(R);
+            case 6: return pick_vec_r<6, B>(R);
+            case 7: return pick_vec_r<7, B>(R);
+            case 8: return pick_vec_r<8, B>(R);
         }
         return nullptr;
     }
     if (C < 1 || C > kMaxC) return nullptr;
     switch (R) {
-        case 1: return k_gf_apply_loop<1>;
-        case 2: return k_gf_apply_loop<2>;
-        case 3: return k_gf_apply_loop<3>;
-        case 4: return k_gf_apply_loop<4>;
-        case 5: return k_gf_apply_loop<5>;
-        case 6: return k_gf_apply_loop<6>;
-        case 7: return k_gf_apply_loop<7>;
-        case 8: return k_gf_apply_loop<8>;
+        case 1: return k_gf_apply_loop<1, B>;
+        case 2: return k_gf_apply_loop<2, B>;
+        case 3: return k_gf_apply_loop<3, B>;
+        case 4: return k_gf_apply_loop<4, B>;
+        case 5: return k_gf_apply_loop<5, B>;
+        case 6: return k_gf_apply_loop<6, B>;
+        case 7: return k_gf_apply_loop<7, B>;
+        case 8: return k_gf_apply_loop<8, B>;
     }
     return nullptr;
 }
+
+static int vec_block() {
+    static const int b = [] {
+        const char* e = std::getenv("RSG_VEC_BLOCK");
+        return (e && std::atoi(e) == 256) ? 256 : 64;
+    }();
+    return b;
+}
+
+static GfKernel pick_vec(int C, int R) { return vec_block() == 256 ? pick_vec_b<256>(C, R) : pick_vec_b<64>(C, R); }
 
 static GfKernel pick_byte(int R) {
     switch (R) {
@@ -899,10 +916,11 @@ static GfKernel pick_byte(int R) {
 hipError_t launch_gf_apply_vec(GfApplyParams p, uint64_t n_stripes, hipStream_t stream) {
     GfKernel k = pick_vec((int)p.C, (int)p.R);
     if (!k || p.units == 0 || n_stripes == 0) return hipErrorInvalidValue;
-    p.chunks_per_stripe = (p.units + 255u) / 256u;
+    const uint32_t B = (uint32_t)vec_block();
+    p.chunks_per_stripe = (p.units + B - 1) / B;
     const uint64_t blocks = (uint64_t)p.chunks_per_stripe * n_stripes;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k, dim3((uint32_t)blocks), dim3(256), 0, stream, p);
+    hipLaunchKernelGGL(k, dim3((uint32_t)blocks), dim3(B), 0, stream, p);
     return hipGetLastError();
 }
 
