@@ -39,8 +39,10 @@ def parse():
     ap.add_argument("--digests", action="store_true", help="fused HH256S digests (config 4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-stripes", type=int, default=256)
-    ap.add_argument("--cpu-threads", type=int, default=16, help="the GPU box's CPU share per GPU")
-    ap.add_argument("--no-extras", action="store_true", help="skip the reconstruct side measurements")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (default: every logical CPU of the box, os.cpu_count())")
+    ap.add_argument("--no-extras", action="store_true", help="skip the reconstruct / GET / heal measurements")
+    ap.add_argument("--no-engines", action="store_true", help="skip the GET / heal / bitrot_verify measurements")
     ap.add_argument("--warm-seconds", type=float, default=0.5,
                     help="keep warming (untimed) until the device has been busy this long (clock ramp)")
     return ap.parse_args()
@@ -73,15 +75,38 @@ def max_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
+def host_cpu_info():
+    """What the CPU baseline ran on: the machine's logical CPUs, the ones this
+    process may use (affinity), the cgroup CPU quota if any, the model."""
+    info = {"nproc_machine": os.cpu_count()}
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except Exception:
+        pass
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except Exception:
+        pass
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                info["model"] = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return info
+
+
 def cpu_baseline(k, m, S, stripes, threads):
     """Restated reference algorithm (oracle/rs_oracle_simd.c: split-nibble
     pshufb GF MAC, one stripe per thread) on a bounded sample of the workload:
-    ~10 s on `threads` host cores, then ~4 s on one core (SURVEY.md §8d asks
-    for both; the reference quotes ~110 us per 1 MiB block on one core,
-    encode.rs:512)."""
+    ~10 s on `threads` host threads (default: every logical CPU of the box,
+    SURVEY.md §8d), then ~4 s on one core (the reference quotes ~110 us per
+    1 MiB block on one core, encode.rs:512)."""
     import numpy as np
     from oracle import oracle as O
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    threads = max(1, min(threads, 512))
     buf = np.zeros((stripes, k + m, S), dtype=np.uint8)
     buf[:, :k] = np.random.default_rng(0).integers(0, 256, (stripes, k, S), dtype=np.uint8)
 
@@ -100,11 +125,80 @@ def cpu_baseline(k, m, S, stripes, threads):
     n1 = min(stripes, 16)
     reps1, el1, gibs1 = timed(1, n1, 4.0)
     return {"value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{reps} passes x {stripes} stripes RS({k},{m}) S={S} ({el:.1f}s), "
+            "sample": f"{reps} passes x {stripes} stripes RS({k},{m}) S={S} on {threads} threads ({el:.1f}s), "
                       f"AVX2={'yes' if O.lib().ro_simd_level() >= 2 else 'no'}",
+            "host": host_cpu_info(),
             "value_1core": round(gibs1, 3),
             "sample_1core": f"{reps1} passes x {n1} stripes on 1 thread ({el1:.1f}s); "
-                            f"{el1 / (reps1 * n1) * 1e6 * (1 << 20) / (k * S):.1f} us per 1 MiB of payload"}
+                            f"{el1 / (reps1 * n1) * 1e6 * (1 << 20) / (k * S):.1f} us per 1 MiB of payload "
+                            f"(reference: ~110 us per 1 MiB block on one core, encode.rs:512)"}
+
+
+def engine_extras(e, stripes, k, m, S, n, stream):
+    """SURVEY §8(f) engines on the same device-resident batch, as BitrotWriter
+    record files ([HH256S][S bytes] per block): GET all present, GET with two
+    data disks lost, heal of one data + one parity disk, whole-file
+    bitrot_verify.  The calls are synchronous (per-stripe status to the host);
+    each is timed with HIP events on the stream around the whole call, and its
+    HBM roofline is priced on the bytes its contract moves at minimum:
+    every record it must verify is read once, every output byte written once."""
+    import torch
+    from rustfs_amd.bitrot import HashAlgorithm, bitrot_verify_batch
+    t, rec = k + m, 32 + S
+    dig = torch.empty((n, t, 32), dtype=torch.uint8, device=stripes.device)
+    e.encode_batch(stripes, dig, stream=stream)
+    files = []
+    for i in range(t):
+        f = torch.empty((n, rec), dtype=torch.uint8, device=stripes.device)
+        f[:, :32] = dig[:, i]
+        f[:, 32:] = stripes[:, i]
+        files.append(f.reshape(-1))
+    del dig
+    out = torch.empty((n, k * S), dtype=torch.uint8, device=stripes.device)
+    want_last = stripes[n - 1, :k].reshape(-1).clone()
+    res = {}
+
+    def timed(name, fn, alg, check, reps=5):
+        fn()
+        torch.cuda.synchronize()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record(stream)
+        for _ in range(reps):
+            r = fn()
+        ev[1].record(stream)
+        torch.cuda.synchronize()
+        ms = ev[0].elapsed_time(ev[1]) / reps
+        check(r)
+        res[name] = {"call_ms": round(ms, 4), "GiB_s_payload": round(n * k * S / (ms * 1e-3) / GiB, 1),
+                     "alg_bytes": alg, "achieved_GB_s": round(alg / (ms * 1e-3) / 1e9, 1),
+                     "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+    def ok_get(r):
+        o, status = r
+        assert all(x == 0 for x in status) and torch.equal(o[n - 1], want_last)
+
+    timed("get_all_present", lambda: e.decode_records_batch(files, S, n, out=out, stream=stream),
+          n * (k * rec + k * S), ok_get)
+    lost = [None if i in (0, 3) else files[i] for i in range(t)]
+    timed("get_2_data_lost", lambda: e.decode_records_batch(lost, S, n, out=out, stream=stream),
+          n * ((t - 2) * rec + k * S), ok_get)
+    tg = [torch.empty(n * rec, dtype=torch.uint8, device=stripes.device) if i in (1, k) else None for i in range(t)]
+    src = [None if i in (1, k) else files[i] for i in range(t)]
+
+    def ok_heal(status):
+        assert all(x == 0 for x in status) and torch.equal(tg[1], files[1]) and torch.equal(tg[k], files[k])
+
+    def ok_verify(status):
+        assert status == [0] * t
+
+    timed("heal_1data_1parity", lambda: e.heal_records_batch(src, tg, S, n, work=out, stream=stream),
+          n * ((t - 2) * rec + 2 * rec), ok_heal)
+    timed("bitrot_verify_all_files",
+          lambda: bitrot_verify_batch(files, n * rec, n * S, HashAlgorithm.HighwayHash256S, S, stream=stream),
+          t * n * rec, ok_verify)
+    del files, lost, tg, src, out
+    torch.cuda.empty_cache()
+    return res
 
 
 def main():
@@ -168,6 +262,11 @@ def main():
     elapsed = max_over_ranks(elapsed, world)
     kern_ms = sorted(s.elapsed_time(t) for s, t in ev)
     avg_ms = sum(kern_ms) / len(kern_ms)
+    rank_ms = [avg_ms]
+    if world > 1:
+        import torch.distributed as dist
+        rank_ms = [None] * world
+        dist.all_gather_object(rank_ms, avg_ms)
 
     payload = n * k * S
     total_stripes = a.total_batch if a.total_batch else n * world
@@ -191,14 +290,18 @@ def main():
             t_ev.record(stream)
             torch.cuda.synchronize()
             ms = s_ev.elapsed_time(t_ev) / reps
+            rb = n * (k + len(miss)) * S
             extras[f"reconstruct_e{len(miss)}"] = {
                 "GiB_s_payload": round(payload / (ms * 1e-3) / GiB, 2),
-                "ms": round(ms, 4),
-                "hbm_GB_s": round(n * (k + len(miss)) * S / (ms * 1e-3) / 1e9, 1)}
+                "kernel_ms": round(ms, 4), "alg_bytes": rb,
+                "hbm_GB_s": round(rb / (ms * 1e-3) / 1e9, 1),
+                "frac": round(rb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
         # round trip correctness of the last pattern (cheap, on device)
         ok = e.verify_batch(stripes, stream=stream)
         torch.cuda.synchronize()
         extras["verify_all_ok_after_reconstruct"] = bool(ok.all().item())
+        if not a.no_engines and world == 1 and not a.digests:
+            extras["engines"] = engine_extras(e, stripes, k, m, S, n, stream)
 
     traffic = None
     prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -211,7 +314,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(k, m, S, min(a.cpu_sample_stripes, n), a.cpu_threads)
+        cpu = cpu_baseline(k, m, S, min(a.cpu_sample_stripes, n), a.cpu_threads or (os.cpu_count() or 1))
 
     if rank == 0:
         line = {
@@ -229,12 +332,16 @@ def main():
             "data": "synthetic (uniform random bytes, torch generator), device-resident",
             "config": {"workload": f"RS(k={k},m={m}) encode{' + fused HH256S' if a.digests else ''}, "
                                    f"{a.stripe_bytes} B stripes (S={S}), batch {n} per GPU",
+                       "timed": "value and roofline: the encode pass (one rsg_encode_batch_dev per step); "
+                                "reconstruct with 1-4 missing shards and the GET/heal engines: extras",
                        "k": k, "m": m, "shard_bytes": S, "stripes_per_gpu": n, "total_stripes": total_stripes,
                        "parallelism": f"stripe-split x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel_ms_avg": round(avg_ms, 4), "kernel_ms_min": round(kern_ms[0], 4),
-                         "alg_bytes_per_launch": alg_bytes},
+                         "alg_bytes_per_launch": alg_bytes,
+                         "per_rank_kernel_ms": [round(x, 4) for x in rank_ms],
+                         "per_rank_frac": [round(alg_bytes / (x * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) for x in rank_ms]},
             "cpu_baseline": cpu,
             "extras": extras,
         }

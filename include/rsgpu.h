@@ -163,11 +163,12 @@ int rsg_decode_records_dev(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t 
  * decode_data_and_parity, erasure.rs:917, per block).  Sources as in
  * rsg_decode_records_dev (d_files[i] == NULL: no reader; every record is
  * verified before use).  d_targets[i] != NULL marks shard i as a heal target
- * (a writer): it receives n BitrotWriter records [HH256S][shard_len bytes]
- * (stride 32+shard_len) of the rebuilt shard i (data shards as read/rebuilt,
- * parity re-encoded).  Every verified source parity is compared with the
- * parity re-encoded from the data (heal.rs:180-196).  d_work: device
- * workspace of n*k*shard_len bytes (receives the data of every stripe).
+ * (a writer, not aliasing any source): it receives n BitrotWriter records
+ * [HH256S][shard_len bytes] (stride 32+shard_len) of the rebuilt shard i (data
+ * shards as read/rebuilt, parity re-encoded), computed in one pass over the
+ * survivors.  Every verified source parity is compared with the parity
+ * re-encoded from the data (heal.rs:180-196).  d_work: unused since ABI 3
+ * (may be NULL; kept so existing bindings stay valid).
  * h_status[s]: RSG_OK, RSG_ERR_TOO_FEW_SHARDS (ErasureReadQuorum) or
  * RSG_ERR_INCONSISTENT_SOURCES ("inconsistent heal source shards"); target
  * records of a failed stripe carry an all-zero digest header (they never

@@ -35,6 +35,11 @@ struct GfApplyParams {
     uint64_t byte_begin, byte_end;  // byte path column range
     uint32_t n_store;               // GF_MODE_STORE_COMPARE split
     uint64_t cmp_stripe_stride;     // GF_MODE_STORE_COMPARE compare-row stripe stride
+    // copy-through: input c with bit c of copy_mask is also stored verbatim at
+    // out_base + s*out_stripe_stride + copy_off[c] (GET: the present data
+    // shards are gathered by the same pass that rebuilds the missing ones)
+    uint32_t copy_mask;
+    uint64_t copy_off[kMaxC];
 };
 
 constexpr int kMaxHashBases = 32;

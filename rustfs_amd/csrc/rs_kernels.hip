@@ -91,9 +91,63 @@ __device__ __forceinline__ uint4 ld16(const uint8_t* p) {
 }
 __device__ __forceinline__ void st16(uint8_t* p, const uint4& v) { __builtin_memcpy(p, &v, 16); }
 
+// Output row r of a launch: its effective mode and address.
+__device__ __forceinline__ uint8_t* gf_dst(const GfApplyParams& p, uint8_t* obase, uint64_t off, int r, uint32_t stripe,
+                                          uint32_t& mode) {
+    mode = p.mode;
+    if (mode == GF_MODE_STORE_COMPARE) {
+        mode = (uint32_t)r < p.n_store ? GF_MODE_STORE : GF_MODE_COMPARE;
+        if (mode == GF_MODE_COMPARE) return p.out_base + (uint64_t)stripe * p.cmp_stripe_stride + p.out_off[r] + off;
+    }
+    return obase + p.out_off[r] + off;
+}
+
+// The bytes an XOR / COMPARE row reads back, loaded together with the inputs
+// so their latency overlaps the arithmetic (STORE rows load nothing).
+template <int R>
+__device__ __forceinline__ void gf_preload(const GfApplyParams& p, uint8_t* obase, uint64_t off, uint32_t stripe,
+                                           uint4 (&old)[R]) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        uint32_t mode;
+        const uint8_t* dst = gf_dst(p, obase, off, r, stripe, mode);
+        if (mode != GF_MODE_STORE) old[r] = ld16(dst);
+    }
+}
+
 template <int R>
 __device__ __forceinline__ void gf_store(const GfApplyParams& p, uint8_t* obase, uint64_t off,
-                                         const uint32_t (&acc)[R][4], uint32_t stripe) {
+                                         const uint32_t (&acc)[R][4], uint32_t stripe, const uint4 (&old)[R]) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        uint32_t mode;
+        uint8_t* dst = gf_dst(p, obase, off, r, stripe, mode);
+        const uint4 v = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+        const uint4 o = old[r];
+        if (mode == GF_MODE_STORE) {
+            st16(dst, v);
+        } else if (mode == GF_MODE_XOR) {
+            st16(dst, make_uint4(o.x ^ v.x, o.y ^ v.y, o.z ^ v.z, o.w ^ v.w));
+        } else {  // GF_MODE_COMPARE: clear the stripe's ok flag on mismatch
+            if ((o.x ^ v.x) | (o.y ^ v.y) | (o.z ^ v.z) | (o.w ^ v.w)) p.ok_flags[stripe] = 0;
+        }
+    }
+}
+
+// B threads per workgroup.  One-wave workgroups (B = 64) are the default:
+// consecutive workgroups still sweep one stripe's columns in order, but waves
+// are replaced one at a time instead of four together; RS(8,4) n = 4096 runs
+// 1.06 ms against 1.09-1.15 ms at B = 256 (tools/kbench/block_probe.hip,
+// profiles/r02/experiments/blk1_block_probe.txt).  RSG_VEC_BLOCK=256 selects
+// the 256-thread form for A/B runs.
+// The !PRE kernels' store: each row loads what it reads back (XOR /
+// COMPARE) only at its store.  The launcher uses them for plain STORE
+// launches, where this form compiles to the fastest measured encode (RS(8,4)
+// n = 4096: 1.065 ms; a store-only body with fewer registers ran 1.10-1.13 ms
+// at every occupancy, profiles/r02/ab_occ/).
+template <int R>
+__device__ __forceinline__ void gf_store_late(const GfApplyParams& p, uint8_t* obase, uint64_t off,
+                                              const uint32_t (&acc)[R][4], uint32_t stripe) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         uint32_t mode = p.mode;
@@ -115,13 +169,18 @@ __device__ __forceinline__ void gf_store(const GfApplyParams& p, uint8_t* obase,
     }
 }
 
-// B threads per workgroup.  One-wave workgroups (B = 64) are the default:
-// consecutive workgroups still sweep one stripe's columns in order, but waves
-// are replaced one at a time instead of four together; RS(8,4) n = 4096 runs
-// 1.06 ms against 1.09-1.15 ms at B = 256 (tools/kbench/block_probe.hip,
-// profiles/r02/experiments/blk1_block_probe.txt).  RSG_VEC_BLOCK=256 selects
-// the 256-thread form for A/B runs.
-template <int C, int R, int B>
+template <int R>
+__device__ __forceinline__ void gf_store(const GfApplyParams& p, uint8_t* obase, uint64_t off,
+                                         const uint32_t (&acc)[R][4], uint32_t stripe) {
+    uint4 old[R];
+    gf_preload<R>(p, obase, off, stripe, old);
+    gf_store<R>(p, obase, off, acc, stripe, old);
+}
+
+// PRE: the launch has XOR / COMPARE rows, whose read-back operands are loaded
+// with the inputs, or copy-through inputs (a separate instantiation: the
+// plain STORE encode and reconstruct kernels keep their register budget).
+template <int C, int R, int B, bool PRE>
 __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(2))) void k_gf_apply_vec(const GfApplyParams p) {
     const uint32_t stripe = blockIdx.x / p.chunks_per_stripe;
     const uint32_t chunk = blockIdx.x - stripe * p.chunks_per_stripe;
@@ -133,11 +192,19 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(2))) void k_g
     uint4 x[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) x[c] = ld16(sbase + p.in_off[c] + off);
+    uint4 old[R];
+    if constexpr (PRE) gf_preload<R>(p, obase, off, stripe, old);
+    if (PRE && p.copy_mask) {  // wave-uniform
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+            if ((p.copy_mask >> c) & 1u) st16(obase + p.copy_off[c] + off, x[c]);
+    }
     uint32_t acc[R][4];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
     gf_accumulate<0, C, R>(p, x, acc);
-    gf_store<R>(p, obase, off, acc, stripe);
+    if constexpr (PRE) gf_store<R>(p, obase, off, acc, stripe, old);
+    else gf_store_late<R>(p, obase, off, acc, stripe);
 }
 
 // Rolled over the inputs in groups of G=8 (any C <= 16, R <= 8): the next
@@ -149,7 +216,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(2))) void k_g
 // peak, in groups of 8 (128 B in flight per lane, 105 VGPRs) at 72-73 %
 // (tools/kbench/xor3_variants.hip).  For C <= 8, R <= 4 the unrolled kernel is
 // faster and stays the default there.
-template <int R, int B>
+template <int R, int B, bool PRE>
 __global__ __launch_bounds__(B) void k_gf_apply_loop(const GfApplyParams p) {
     constexpr int G = 8;
     const uint32_t stripe = blockIdx.x / p.chunks_per_stripe;
@@ -169,6 +236,8 @@ __global__ __launch_bounds__(B) void k_gf_apply_loop(const GfApplyParams p) {
 #pragma unroll
     for (int g = 0; g < G; ++g)
         if ((uint32_t)g < C) x[g] = ld16(sbase + p.in_off[g] + off);
+    uint4 old[R];
+    if constexpr (PRE) gf_preload<R>(p, obase, off, stripe, old);
 #pragma unroll 1
     for (uint32_t c0 = 0; c0 < C; c0 += G) {
 #pragma unroll
@@ -178,6 +247,7 @@ __global__ __launch_bounds__(B) void k_gf_apply_loop(const GfApplyParams p) {
         for (int g = 0; g < G; ++g) {
             const uint32_t c = c0 + g;
             if (c >= C) break;  // wave-uniform
+            if (PRE && ((p.copy_mask >> c) & 1u)) st16(obase + p.copy_off[c] + off, x[g]);
             const uint32_t w[4] = {x[g].x, x[g].y, x[g].z, x[g].w};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -201,7 +271,8 @@ __global__ __launch_bounds__(B) void k_gf_apply_loop(const GfApplyParams p) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) acc[r][q] ^= pend[r][q];
     }
-    gf_store<R>(p, obase, off, acc, stripe);
+    if constexpr (PRE) gf_store<R>(p, obase, off, acc, stripe, old);
+    else gf_store_late<R>(p, obase, off, acc, stripe);
 }
 
 // ---------------------------------------------------------------------------
@@ -221,6 +292,7 @@ __global__ __launch_bounds__(256) void k_gf_apply_byte(const GfApplyParams p) {
     for (int r = 0; r < R; ++r) acc[r] = 0u;
     for (uint32_t c = 0; c < p.C; ++c) {
         const uint32_t x = sbase[p.in_off[c] + b];
+        if ((p.copy_mask >> c) & 1u) obase[p.copy_off[c] + b] = (uint8_t)x;
         const uint32_t s0 = x & 7u, s1 = (x >> 3) & 7u, s2 = x >> 6;
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] ^= gf_mul_word(p.tab[r][c], s0, s1, s2);
@@ -398,7 +470,9 @@ __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
         const uint64_t b = j / p.per_base, r = j - b * p.per_base;
         msg = p.base[b] + r * p.stripe_stride;
         if (p.flag_base[b]) flag = p.flag_base[b] + r;
-        if constexpr (COPY != 0) dst = p.copy_base[b] + r * p.copy_stride;
+        // copy mode: files without a copy_base (parity records verified in
+        // the same launch as the data records they back up) are only hashed
+        if constexpr (COPY != 0) dst = p.copy_base[b] ? p.copy_base[b] + r * p.copy_stride : nullptr;
     } else {
         const uint64_t stripe = j / p.shards, shard = j - stripe * p.shards;
         msg = p.data + stripe * p.stripe_stride + shard * p.shard_pitch;
@@ -416,7 +490,7 @@ __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
             const uint64_t jj = wj + 4 * kk + (lane >> 4);
             if (jj < p.n) {
                 const uint64_t b = jj / p.per_base, r = jj - b * p.per_base;
-                sdst[kk] = p.copy_base[b] + r * p.copy_stride + (lane & 15u) * 16u;
+                if (p.copy_base[b]) sdst[kk] = p.copy_base[b] + r * p.copy_stride + (lane & 15u) * 16u;
             }
         }
     }
@@ -434,8 +508,10 @@ __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) hhq_update(s, w[i]);
         if constexpr (COPY == 1) {
+            if (dst) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) st64_any(dst + (t0 + i) * 32 + 8 * q, w[i]);
+                for (int i = 0; i < 8; ++i) st64_any(dst + (t0 + i) * 32 + 8 * q, w[i]);
+            }
         } else if constexpr (COPY == 2) {
             // one wave's LDS instructions execute in order: the reads below see
             // these writes, and the next batch's writes follow these reads
@@ -476,12 +552,12 @@ __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
     for (; t < packets; ++t) {
         const uint64_t w = ld64_any(msg + t * 32 + 8 * q);
         hhq_update(s, w);
-        if constexpr (COPY) st64_any(dst + t * 32 + 8 * q, w);
+        if (COPY && dst) st64_any(dst + t * 32 + 8 * q, w);
     }
     const uint32_t rem = (uint32_t)(p.len & 31);
     if (rem) {
         hhq_remainder(s, msg + packets * 32, rem, q);
-        if constexpr (COPY)
+        if (COPY && dst)
             for (uint32_t b = 8 * q; b < rem && b < 8 * q + 8; ++b) dst[packets * 32 + b] = msg[packets * 32 + b];
     }
     if (flag) {  // verify before use (split_and_verify, bitrot.rs:227-247)
@@ -843,20 +919,20 @@ void k_encode_hash_ring(const GfApplyParams p, const HashParams h, const uint32_
 
 using GfKernel = void (*)(const GfApplyParams);
 
-template <int C, int B>
+template <int C, int B, bool PRE>
 static GfKernel pick_vec_r(int R) {
     switch (R) {
-        case 1: return k_gf_apply_vec<C, 1, B>;
-        case 2: return k_gf_apply_vec<C, 2, B>;
-        case 3: return k_gf_apply_vec<C, 3, B>;
-        case 4: return k_gf_apply_vec<C, 4, B>;
+        case 1: return k_gf_apply_vec<C, 1, B, PRE>;
+        case 2: return k_gf_apply_vec<C, 2, B, PRE>;
+        case 3: return k_gf_apply_vec<C, 3, B, PRE>;
+        case 4: return k_gf_apply_vec<C, 4, B, PRE>;
     }
     return nullptr;
 }
 
 // Unrolled kernel for C <= 8 inputs and R <= 4 outputs, the rolled one above
 // (k_gf_apply_loop); RSG_ROLLED=1 forces the rolled kernel for A/B runs.
-template <int B>
+template <int B, bool PRE>
 static GfKernel pick_vec_b(int C, int R) {
     static const bool force_rolled = [] {
         const char* s = std::getenv("RSG_ROLLED");
@@ -864,27 +940,27 @@ static GfKernel pick_vec_b(int C, int R) {
     }();
     if (C <= 8 && R <= 4 && !force_rolled) {
         switch (C) {
-            case 1: return pick_vec_r<1, B>(R);
-            case 2: return pick_vec_r<2, B>(R);
-            case 3: return pick_vec_r<3, B>(R);
-            case 4: return pick_vec_r<4, B>(R);
-            case 5: return pick_vec_r<5, B>(R);
-            case 6: return pick_vec_r<6, B>(R);
-            case 7: return pick_vec_r<7, B>(R);
-            case 8: return pick_vec_r<8, B>(R);
+            case 1: return pick_vec_r<1, B, PRE>(R);
+            case 2: return pick_vec_r<2, B, PRE>(R);
+            case 3: return pick_vec_r<3, B, PRE>(R);
+            case 4: return pick_vec_r<4, B, PRE>(R);
+            case 5: return pick_vec_r<5, B, PRE>(R);
+            case 6: return pick_vec_r<6, B, PRE>(R);
+            case 7: return pick_vec_r<7, B, PRE>(R);
+            case 8: return pick_vec_r<8, B, PRE>(R);
         }
         return nullptr;
     }
     if (C < 1 || C > kMaxC) return nullptr;
     switch (R) {
-        case 1: return k_gf_apply_loop<1, B>;
-        case 2: return k_gf_apply_loop<2, B>;
-        case 3: return k_gf_apply_loop<3, B>;
-        case 4: return k_gf_apply_loop<4, B>;
-        case 5: return k_gf_apply_loop<5, B>;
-        case 6: return k_gf_apply_loop<6, B>;
-        case 7: return k_gf_apply_loop<7, B>;
-        case 8: return k_gf_apply_loop<8, B>;
+        case 1: return k_gf_apply_loop<1, B, PRE>;
+        case 2: return k_gf_apply_loop<2, B, PRE>;
+        case 3: return k_gf_apply_loop<3, B, PRE>;
+        case 4: return k_gf_apply_loop<4, B, PRE>;
+        case 5: return k_gf_apply_loop<5, B, PRE>;
+        case 6: return k_gf_apply_loop<6, B, PRE>;
+        case 7: return k_gf_apply_loop<7, B, PRE>;
+        case 8: return k_gf_apply_loop<8, B, PRE>;
     }
     return nullptr;
 }
@@ -897,7 +973,23 @@ static int vec_block() {
     return b;
 }
 
-static GfKernel pick_vec(int C, int R) { return vec_block() == 256 ? pick_vec_b<256>(C, R) : pick_vec_b<64>(C, R); }
+// Waves per SIMD the vector kernels may keep resident (RSG_VEC_OCC, A/B
+// runs; default 0 = whatever their registers allow, 3 for the 163-VGPR
+// RS(8,4) encode).  Enforced with an otherwise unused dynamic LDS allocation
+// per one-wave workgroup: 160 KiB / (4 SIMDs x occ) each.
+static int vec_occupancy() {
+    static const int occ = [] {
+        const char* e = std::getenv("RSG_VEC_OCC");
+        const int v = e ? std::atoi(e) : 0;
+        return (v < 0 || v > 8) ? 0 : v;
+    }();
+    return occ;
+}
+
+static GfKernel pick_vec(int C, int R, bool pre) {
+    if (vec_block() == 256) return pre ? pick_vec_b<256, true>(C, R) : pick_vec_b<256, false>(C, R);
+    return pre ? pick_vec_b<64, true>(C, R) : pick_vec_b<64, false>(C, R);
+}
 
 static GfKernel pick_byte(int R) {
     switch (R) {
@@ -914,13 +1006,15 @@ static GfKernel pick_byte(int R) {
 }
 
 hipError_t launch_gf_apply_vec(GfApplyParams p, uint64_t n_stripes, hipStream_t stream) {
-    GfKernel k = pick_vec((int)p.C, (int)p.R);
+    GfKernel k = pick_vec((int)p.C, (int)p.R, p.mode != GF_MODE_STORE || p.copy_mask != 0);
     if (!k || p.units == 0 || n_stripes == 0) return hipErrorInvalidValue;
     const uint32_t B = (uint32_t)vec_block();
     p.chunks_per_stripe = (p.units + B - 1) / B;
     const uint64_t blocks = (uint64_t)p.chunks_per_stripe * n_stripes;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k, dim3((uint32_t)blocks), dim3(B), 0, stream, p);
+    const int occ = vec_occupancy();
+    const size_t lds = occ ? (size_t)(160 * 1024) / (size_t)(4 * occ * (B / 64)) / 16 * 16 : 0;
+    hipLaunchKernelGGL(k, dim3((uint32_t)blocks), dim3(B), lds, stream, p);
     return hipGetLastError();
 }
 
@@ -939,7 +1033,8 @@ hipError_t launch_hh256(const HashParams& p, hipStream_t stream) {
     if (p.n == 0) return hipSuccess;
     const uint64_t blocks = (p.n * 4u + 255u) / 256u;  // one quad per message
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    const bool copy = p.nbases && p.copy_base[0];
+    bool copy = false;  // copy mode when any file of the launch has a copy target
+    for (uint32_t b = 0; b < p.nbases; ++b) copy = copy || p.copy_base[b];
     // copy mode: staged 16-byte stores (COPY = 2) by default; RSG_HASH_COPY=1
     // selects the direct 8-byte stores for A/B runs
     static const bool direct_copy = [] {

@@ -204,6 +204,10 @@ struct RowSet {
     int R = 0, C = 0;
     Mat coef;                    // R x C
     std::vector<uint64_t> in_off, out_off;
+    // copy-through (optional, C entries): input c is also stored verbatim at
+    // output offset copy_off[c] when copy[c] != 0 (done by the first row group)
+    std::vector<uint8_t> copy;
+    std::vector<uint64_t> copy_off;
 };
 
 // Parity rows of the encode matrix over the data shards.
@@ -300,6 +304,12 @@ void fill_params(const RowSet& rs, int r0, int c0, const uint8_t* base, uint8_t*
     p.C = (uint32_t)C;
     p.R = (uint32_t)R;
     p.mode = mode;
+    if (r0 == 0 && !rs.copy.empty())
+        for (int c = 0; c < C; ++c)
+            if (rs.copy[c0 + c]) {
+                p.copy_mask |= 1u << c;
+                p.copy_off[c] = rs.copy_off[c0 + c];
+            }
 }
 
 // RSG_FUSED=0 disables the fused encode+hash kernel (A/B measurements).
@@ -582,6 +592,15 @@ uint8_t* pinned_view(const uint8_t* p, size_t len, int device) {
         !b.devicePointer || (uint8_t*)b.devicePointer - (uint8_t*)a.devicePointer != (ptrdiff_t)(len - 1))
         return nullptr;
     return (uint8_t*)a.devicePointer;
+}
+
+// RSG_LOST_DISK_FAST=0 disables the optimistic lost-disk GET pass (A/B runs).
+bool lost_disk_fast_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("RSG_LOST_DISK_FAST");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 // RSG_ZERO_COPY=0 disables the in-place kernels on pinned blocks (A/B runs).
@@ -1007,7 +1026,7 @@ int launch_verify_group(const std::vector<int>& idx, const uint8_t* const* d_fil
             const int i = idx[x];
             h.base[x - g0] = d_files[i] + lo * rec + 32;
             h.flag_base[x - g0] = d_flags + (size_t)i * n + lo;
-            if (d_out) h.copy_base[x - g0] = d_out + lo * h.copy_stride + (uint64_t)i * shard_len;
+            if (d_out && i < k) h.copy_base[x - g0] = d_out + lo * h.copy_stride + (uint64_t)i * shard_len;
         }
         if ((st = hip_status(rsg::launch_hh256(h, s)))) return st;
     }
@@ -1025,11 +1044,22 @@ int verify_gather(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64_t n, co
     uint8_t* d_flags = ctx->d_scratch;
     int st;
     if ((st = hip_status(hipMemsetAsync(d_flags, 0, (size_t)t * n, s)))) return st;
-    std::vector<int> data_idx, par_idx;
+    std::vector<int> data_idx, par_idx, all_idx;
     for (int i = 0; i < t; ++i)
-        if (d_files[i]) (i < k ? data_idx : par_idx).push_back(i);
-    if ((st = launch_verify_group(data_idx, d_files, d_flags, k, shard_len, n, 0, n, key, d_out, s))) return st;
+        if (d_files[i]) {
+            (i < k ? data_idx : par_idx).push_back(i);
+            all_idx.push_back(i);
+        }
     flags.assign((size_t)t * n, 0);
+    if (all_parity || (int)data_idx.size() < k) {
+        // every stripe needs its parity (heal, or a lost data disk): all
+        // present records of all stripes in one launch, data gathered
+        if ((st = launch_verify_group(all_idx, d_files, d_flags, k, shard_len, n, 0, n, key, d_out, s))) return st;
+        if ((st = hip_status(hipMemcpyAsync(flags.data(), d_flags, (size_t)t * n, hipMemcpyDeviceToHost, s))))
+            return st;
+        return hip_status(hipStreamSynchronize(s));
+    }
+    if ((st = launch_verify_group(data_idx, d_files, d_flags, k, shard_len, n, 0, n, key, d_out, s))) return st;
     if ((st = hip_status(hipMemcpyAsync(flags.data(), d_flags, (size_t)k * n, hipMemcpyDeviceToHost, s)))) return st;
     if ((st = hip_status(hipStreamSynchronize(s)))) return st;
     uint64_t lo = n, hi = 0;
@@ -1058,21 +1088,23 @@ int verify_gather(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64_t n, co
 // shards of every stripe into d_out (n x k*S), optional surplus-parity check.
 // Uses ctx->d_scratch[0, (t+1)*n).  `flags` returns the verified-shard map.
 int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64_t n, const uint8_t* const* d_files,
-                          const uint64_t* key, bool verify_surplus, bool all_parity, uint8_t* d_out, int* h_status,
-                          std::vector<uint8_t>& flags, hipStream_t s) {
+                          const uint64_t* key, bool verify_surplus, uint8_t* d_out, int* h_status, hipStream_t s) {
     const int t = k + m;
     const uint64_t rec = 32 + shard_len;  // BitrotWriter record: [hash][block]
+    const uint64_t ks = (uint64_t)k * shard_len;
     int st;
     if ((st = ctx->ensure_scratch((size_t)(t + 1) * n))) return st;
     uint8_t* d_ok = ctx->d_scratch + (size_t)t * n;  // surplus-parity verdict per stripe
     if ((st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
-    // 1. verify the data records and gather them into d_out; parity where needed
-    if ((st = verify_gather(ctx, k, m, shard_len, n, d_files, key, d_out, all_parity, flags, s))) return st;
     auto cd = m > 0 ? get_codec(k, m) : nullptr;
     if (m > 0 && !cd) return RSG_ERR_INVALID_ARG;
     bool any_verify = false;
-    // 2. per run of stripes with one pattern: rebuild missing data
-    st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) -> int {
+    // Rebuild the missing data of stripes [s0, s1) that share one valid-shard
+    // pattern from the first k valid shards, read in place from the records,
+    // and (verify_surplus) compare every other valid parity with its
+    // re-derived value (erasure.rs:935-973).  With `gather`, the present data
+    // shards are copied into d_out by the same pass (copy-through).
+    auto rebuild_run = [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present, bool gather) -> int {
         const uint64_t cnt = s1 - s0;
         int valid = 0, missing_data = 0, e;
         for (int i = 0; i < t; ++i) valid += present[i];
@@ -1080,8 +1112,15 @@ int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64
         const int run_status = valid < k ? RSG_ERR_TOO_FEW_SHARDS : RSG_OK;
         for (uint64_t x = s0; x < s1; ++x) h_status[x] = run_status;
         if (run_status != RSG_OK) return RSG_OK;
-        uint8_t* out = d_out + s0 * (uint64_t)k * shard_len;  // verified data already gathered here
-        if (!missing_data) return RSG_OK;
+        uint8_t* out = d_out + s0 * ks;
+        if (!missing_data) {
+            if (!gather) return RSG_OK;  // verified data already gathered here
+            for (int i = 0; i < k; ++i)
+                if ((e = hip_status(hipMemcpy2DAsync(out + (uint64_t)i * shard_len, ks, d_files[i] + s0 * rec + 32, rec,
+                                                     shard_len, cnt, hipMemcpyDeviceToDevice, s))))
+                    return e;
+            return RSG_OK;
+        }
         auto plan = cd->plan(present.data());
         if (!plan) return RSG_ERR_TOO_FEW_SHARDS;
         // survivors read in place from the records; base = first survivor
@@ -1090,6 +1129,15 @@ int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64
         rs.C = k;
         for (int sv : plan->survivors)
             rs.in_off.push_back((uint64_t)(uintptr_t)(d_files[sv] + s0 * rec + 32) - (uint64_t)(uintptr_t)base);
+        if (gather) {
+            rs.copy.assign(k, 0);
+            rs.copy_off.assign(k, 0);
+            for (int c = 0; c < k; ++c)
+                if (plan->survivors[c] < k) {
+                    rs.copy[c] = 1;
+                    rs.copy_off[c] = (uint64_t)plan->survivors[c] * shard_len;
+                }
+        }
         for (int i = 0; i < k; ++i) {
             if (present[i]) continue;
             rs.coef.resize((size_t)(rs.R + 1) * k);
@@ -1097,15 +1145,13 @@ int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64
             rs.out_off.push_back((uint64_t)i * shard_len);
             ++rs.R;
         }
-        // 3. surplus parity must agree with the rebuilt data (erasure.rs:935-973)
+        // surplus parity must agree with the rebuilt data (erasure.rs:935-973)
         RowSet vs;
         vs.C = k;
         vs.in_off = rs.in_off;
         if (verify_surplus && valid > k) {
             for (int p = k; p < t; ++p) {
-                if (!present[p]) continue;
-                if (std::find(plan->survivors.begin(), plan->survivors.end(), p) != plan->survivors.end())
-                    continue;  // a survivor re-derives to itself
+                if (!present[p] || is_survivor(*plan, p)) continue;  // a survivor re-derives to itself
                 vs.coef.resize((size_t)(vs.R + 1) * k);
                 plan_row(*cd, *plan, p, &vs.coef[(size_t)vs.R * k]);
                 vs.out_off.push_back((uint64_t)(uintptr_t)(d_files[p] + s0 * rec + 32) - (uint64_t)(uintptr_t)base);
@@ -1120,17 +1166,57 @@ int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64
             for (uint64_t o : vs.out_off)  // compare targets relative to `out`
                 both.out_off.push_back(o + (uint64_t)(uintptr_t)base - (uint64_t)(uintptr_t)out);
             both.R = rs.R + vs.R;
-            return apply_store_compare(both, rs.R, base, out, rec, (uint64_t)k * shard_len, rec, shard_len, cnt,
-                                       d_ok + s0, s);
+            return apply_store_compare(both, rs.R, base, out, rec, ks, rec, shard_len, cnt, d_ok + s0, s);
         }
-        if ((e = apply_rows(rs, base, out, rec, (uint64_t)k * shard_len, shard_len, cnt, rsg::GF_MODE_STORE,
-                            nullptr, s)))
-            return e;
+        if ((e = apply_rows(rs, base, out, rec, ks, shard_len, cnt, rsg::GF_MODE_STORE, nullptr, s))) return e;
         if (!vs.R) return RSG_OK;
         return apply_rows(vs, base, const_cast<uint8_t*>(base), rec, rec, shard_len, cnt, rsg::GF_MODE_COMPARE,
                           d_ok + s0, s);
-    });
-    if (st) return st;
+    };
+
+    std::vector<uint8_t> present0(t), flags;
+    int nfiles = 0, lost_data = 0;
+    for (int i = 0; i < t; ++i) {
+        present0[i] = d_files[i] ? 1 : 0;
+        nfiles += present0[i];
+        if (i < k && !d_files[i]) ++lost_data;
+    }
+    const int surplus = std::max(0, nfiles - k);  // present shards beyond the k survivors
+    const bool fast = m > 0 && lost_data > 0 && nfiles >= k && k <= rsg::kMaxC &&
+                      lost_data + (verify_surplus ? surplus : 0) <= rsg::kMaxR && lost_disk_fast_enabled();
+    if (fast) {
+        // Lost disk(s): every stripe misses the same data shards, so one
+        // optimistic sweep over the present records rebuilds the missing data,
+        // gathers the present data (copy-through) and checks surplus parity,
+        // as if every present record verifies; then every present record is
+        // verified (read-only).  Stripes where a record fails are redone from
+        // their actual valid shards.  Survivors are read twice (rebuild, then
+        // verify) instead of three times by the general path.
+        if ((st = rebuild_run(0, n, present0, true))) return st;
+        uint8_t* d_flags = ctx->d_scratch;
+        if ((st = hip_status(hipMemsetAsync(d_flags, 0, (size_t)t * n, s)))) return st;
+        std::vector<int> all_idx;
+        for (int i = 0; i < t; ++i)
+            if (d_files[i]) all_idx.push_back(i);
+        if ((st = launch_verify_group(all_idx, d_files, d_flags, k, shard_len, n, 0, n, key, nullptr, s))) return st;
+        flags.assign((size_t)t * n, 0);
+        if ((st = hip_status(hipMemcpyAsync(flags.data(), d_flags, (size_t)t * n, hipMemcpyDeviceToHost, s))))
+            return st;
+        if ((st = hip_status(hipStreamSynchronize(s)))) return st;
+        st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) -> int {
+            if (present == present0) return RSG_OK;  // the optimistic pass was right
+            int e = hip_status(hipMemsetAsync(d_ok + s0, 1, s1 - s0, s));
+            return e ? e : rebuild_run(s0, s1, present, true);
+        });
+        if (st) return st;
+    } else {
+        // verify the data records and gather them into d_out; parity where needed
+        if ((st = verify_gather(ctx, k, m, shard_len, n, d_files, key, d_out, false, flags, s))) return st;
+        st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) {
+            return rebuild_run(s0, s1, present, false);
+        });
+        if (st) return st;
+    }
     if (any_verify) {
         std::vector<uint8_t> ok(n, 1);
         if ((st = hip_status(hipMemcpyAsync(ok.data(), d_ok, n, hipMemcpyDeviceToHost, s)))) return st;
@@ -1159,9 +1245,7 @@ int rsg_decode_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t 
     }
     hipStream_t s = pick_stream(ctx, stream);
     std::lock_guard<std::mutex> g(ctx->mu);
-    std::vector<uint8_t> flags;
-    return decode_records_locked(ctx, k, m, shard_len, n, d_files, key, verify_surplus != 0, false, d_out, h_status,
-                                 flags, s);
+    return decode_records_locked(ctx, k, m, shard_len, n, d_files, key, verify_surplus != 0, d_out, h_status, s);
 }
 
 // Heal (Erasure::heal, heal.rs:112-206) over n stripes of bitrot records.
@@ -1171,7 +1255,7 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
     if (st) return st;
     if ((st = check_geometry(k, m))) return st;
     if (m == 0) return RSG_ERR_ZERO_PARITY_SHARDS;
-    if (!d_files || !d_targets || (n && (!d_work || !h_status))) return RSG_ERR_INVALID_ARG;
+    if (!d_files || !d_targets || (n && !h_status)) return RSG_ERR_INVALID_ARG;
     const uint64_t* key = hash_key(algo);
     if (!key) return RSG_ERR_INVALID_ARG;
     if (n == 0 || shard_len == 0) {
@@ -1182,35 +1266,46 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
     const uint64_t rec = 32 + shard_len, ks = (uint64_t)k * shard_len;
     hipStream_t s = pick_stream(ctx, stream);
     std::lock_guard<std::mutex> g(ctx->mu);
-    // 1. verified sources -> full data of every stripe (read quorum: k verified shards)
+    // 1. verify every source record in place (read quorum: k verified shards
+    //    per stripe); nothing is gathered
     std::vector<uint8_t> flags;
-    if ((st = decode_records_locked(ctx, k, m, shard_len, n, d_files, key, false, true, d_work, h_status, flags, s)))
-        return st;
+    if ((st = ctx->ensure_scratch((size_t)(t + 1) * n))) return st;
+    if ((st = verify_gather(ctx, k, m, shard_len, n, d_files, key, nullptr, true, flags, s))) return st;
     auto cd = get_codec(k, m);
     if (!cd) return RSG_ERR_INVALID_ARG;
-    // 2. every verified source parity must equal the parity re-encoded from the
-    //    (rebuilt) data: "inconsistent heal source shards" (heal.rs:180-196);
-    //    parity targets are encoded in the same pass over the data
+    // 2. per run of stripes with one verified pattern, ONE pass over the
+    //    survivors (first k verified shards) writes every target's record
+    //    body — data rebuilt or, if verified, reproduced (identity row), parity
+    //    re-encoded — and compares every verified source parity that is not a
+    //    survivor with its re-encoded value: "inconsistent heal source shards"
+    //    (heal.rs:180-196; a survivor parity re-encodes to itself)
     uint8_t* d_ok = ctx->d_scratch + (size_t)t * n;
     if ((st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
     bool any_verify = false;
     st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) -> int {
-        if (h_status[s0] != RSG_OK) return RSG_OK;
-        const uint8_t* base = d_work + s0 * ks;
-        RowSet ps, vs;  // parity targets (store), verified source parity (compare)
+        int valid = 0;
+        for (int i = 0; i < t; ++i) valid += present[i];
+        for (uint64_t x = s0; x < s1; ++x) h_status[x] = valid < k ? RSG_ERR_TOO_FEW_SHARDS : RSG_OK;
+        if (valid < k) return RSG_OK;
+        auto plan = cd->plan(present.data());
+        if (!plan) return RSG_ERR_TOO_FEW_SHARDS;
+        const uint8_t* base = d_files[plan->survivors[0]] + s0 * rec + 32;
+        auto rel = [&](const uint8_t* p) { return (uint64_t)(uintptr_t)(p + s0 * rec + 32) - (uint64_t)(uintptr_t)base; };
+        RowSet ps, vs;  // target bodies (store), non-survivor verified parity (compare)
         ps.C = vs.C = k;
-        for (int c = 0; c < k; ++c) ps.in_off.push_back((uint64_t)c * shard_len);
+        for (int sv : plan->survivors) ps.in_off.push_back(rel(d_files[sv]));
         vs.in_off = ps.in_off;
-        for (int p = k; p < t; ++p) {
-            const auto row_b = cd->matrix.begin() + (size_t)p * k, row_e = row_b + k;
-            if (d_targets[p]) {
-                ps.coef.insert(ps.coef.end(), row_b, row_e);
-                ps.out_off.push_back((uint64_t)(uintptr_t)(d_targets[p] + s0 * rec + 32) - (uint64_t)(uintptr_t)base);
+        for (int i = 0; i < t; ++i) {
+            if (d_targets[i]) {
+                ps.coef.resize((size_t)(ps.R + 1) * k);
+                plan_row(*cd, *plan, i, &ps.coef[(size_t)ps.R * k]);
+                ps.out_off.push_back(rel(d_targets[i]));
                 ++ps.R;
             }
-            if (present[p]) {
-                vs.coef.insert(vs.coef.end(), row_b, row_e);
-                vs.out_off.push_back((uint64_t)(uintptr_t)(d_files[p] + s0 * rec + 32) - (uint64_t)(uintptr_t)base);
+            if (i >= k && present[i] && !is_survivor(*plan, i)) {
+                vs.coef.resize((size_t)(vs.R + 1) * k);
+                plan_row(*cd, *plan, i, &vs.coef[(size_t)vs.R * k]);
+                vs.out_off.push_back(rel(d_files[i]));
                 ++vs.R;
             }
         }
@@ -1221,19 +1316,16 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
             both.coef.insert(both.coef.end(), vs.coef.begin(), vs.coef.end());
             both.out_off.insert(both.out_off.end(), vs.out_off.begin(), vs.out_off.end());
             both.R = ps.R + vs.R;
-            return apply_store_compare(both, ps.R, base, ob, ks, rec, rec, shard_len, s1 - s0, d_ok + s0, s);
+            return apply_store_compare(both, ps.R, base, ob, rec, rec, rec, shard_len, s1 - s0, d_ok + s0, s);
         }
-        int e = apply_rows(ps, base, ob, ks, rec, shard_len, s1 - s0, rsg::GF_MODE_STORE, nullptr, s);
+        int e = apply_rows(ps, base, ob, rec, rec, shard_len, s1 - s0, rsg::GF_MODE_STORE, nullptr, s);
         if (e || !vs.R) return e;
-        return apply_rows(vs, base, ob, ks, rec, shard_len, s1 - s0, rsg::GF_MODE_COMPARE, d_ok + s0, s);
+        return apply_rows(vs, base, ob, rec, rec, shard_len, s1 - s0, rsg::GF_MODE_COMPARE, d_ok + s0, s);
     });
     if (st) return st;
-    // 3. data targets: copied out of the gathered/rebuilt data; then every
-    //    target record gets its HH256S header (BitrotWriter::write)
-    for (int i = 0; i < k; ++i)
-        if (d_targets[i] && (st = hip_status(hipMemcpy2DAsync(d_targets[i] + 32, rec, d_work + (uint64_t)i * shard_len,
-                                                                ks, shard_len, n, hipMemcpyDeviceToDevice, s))))
-            return st;
+    (void)d_work;
+    (void)ks;
+    // 3. every target record gets its HH256S header (BitrotWriter::write)
     if ((st = hash_records_inplace(d_targets, t, shard_len, n, key, s))) return st;
     if (any_verify) {
         std::vector<uint8_t> ok(n, 1);

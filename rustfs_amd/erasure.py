@@ -381,6 +381,7 @@ class Erasure:
     def heal_records_batch(self, files: Sequence, targets: Sequence, shard_len: int, n: int,
                            algo: int = _lib.RSG_HASH_HIGHWAY256S, work=None, stream=None):
         """Batched heal (rsg_heal_records_dev; Erasure::heal, heal.rs:112-206).
+        `work` is accepted for compatibility and unused (ABI 3).
 
         `files[i]`: cuda uint8 tensor with shard i's n BitrotWriter records, or
         None (no reader).  `targets[i]`: cuda uint8 tensor of n*(32+shard_len)
@@ -401,15 +402,13 @@ class Erasure:
                 dev = f.device
         if dev is None:
             raise RsgError(_lib.RSG_ERR_INVALID_ARG, "invalid argument")
-        if work is None:
-            work = torch.empty((n, self.data_shards * shard_len), dtype=torch.uint8, device=dev)
         src = (ctypes.c_void_p * t)(*[f.data_ptr() if f is not None else None for f in files])
         dst = (ctypes.c_void_p * t)(*[f.data_ptr() if f is not None else None for f in targets])
         status = (ctypes.c_int * max(n, 1))()
         s = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
         check(_lib.load().rsg_heal_records_dev(
             _lib.context(dev.index or 0).handle, self.data_shards, self.parity_shards, shard_len, n, src, dst,
-            algo, work.data_ptr(), status, s), "erasure heal")
+            algo, work.data_ptr() if work is not None else None, status, s), "erasure heal")
         return _lib.status_list(status, n)
 
     def reconstruct_batch(self, stripes, present: Sequence[bool], mode: int = _lib.RSG_RECONSTRUCT_MISSING,

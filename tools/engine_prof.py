@@ -1,0 +1,46 @@
+"""One engine call repeated (for rocprofv3 --kernel-trace --stats): GET with
+two data disks lost, or heal, RS(8,4) 1 MiB stripes, n = 4096 records.
+Usage: python tools/engine_prof.py get2|get0|heal [reps]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import torch
+    from rustfs_amd import Erasure
+    what = sys.argv[1] if len(sys.argv) > 1 else "get2"
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    k, m, n = 8, 4, 4096
+    S, t = 131072, 12
+    rec = 32 + S
+    e = Erasure(k, m, 1 << 20)
+    st = torch.zeros((n, t, S), dtype=torch.uint8, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(5)
+    for s0 in range(0, n, 256):
+        st[s0:s0 + 256, :k] = torch.randint(0, 256, (min(256, n - s0), k, S), dtype=torch.uint8, device="cuda",
+                                            generator=g)
+    dig = torch.empty((n, t, 32), dtype=torch.uint8, device="cuda")
+    e.encode_batch(st, dig)
+    files = []
+    for i in range(t):
+        f = torch.empty((n, rec), dtype=torch.uint8, device="cuda")
+        f[:, :32] = dig[:, i]
+        f[:, 32:] = st[:, i]
+        files.append(f.reshape(-1))
+    del st, dig
+    out = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
+    for _ in range(reps):
+        if what == "heal":
+            tg = [torch.empty(n * rec, dtype=torch.uint8, device="cuda") if i in (1, k) else None for i in range(t)]
+            e.heal_records_batch([None if i in (1, k) else files[i] for i in range(t)], tg, S, n)
+        else:
+            lost = (0, 3) if what == "get2" else ()
+            e.decode_records_batch([None if i in lost else files[i] for i in range(t)], S, n, out=out)
+    torch.cuda.synchronize()
+    print("done", what, reps)
+
+
+if __name__ == "__main__":
+    main()
