@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-stripes", type=int, default=256)
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="CPU baseline threads (default: every logical CPU of the box, os.cpu_count())")
+                    help="CPU baseline threads (default: every CPU this process may use: affinity and cgroup quota)")
     ap.add_argument("--no-extras", action="store_true", help="skip the reconstruct / GET / heal measurements")
     ap.add_argument("--no-engines", action="store_true", help="skip the GET / heal / bitrot_verify measurements")
     ap.add_argument("--warm-seconds", type=float, default=0.5,
@@ -98,11 +98,25 @@ def host_cpu_info():
     return info
 
 
+def usable_cpus():
+    """Logical CPUs this process can actually run on: the affinity mask,
+    capped by the cgroup CPU quota (the GPU box shows its whole machine,
+    e.g. 256 CPUs, to a job limited to 16 by its cgroup; 256 threads there
+    measure the throttling, not the CPU: 29 GiB/s against 85 GiB/s)."""
+    info = host_cpu_info()
+    n = info.get("affinity_cpus") or info.get("nproc_machine") or 1
+    q = info.get("cgroup_cpu_quota")
+    if q:
+        n = min(n, max(1, int(q + 0.999)))
+    return n
+
+
 def cpu_baseline(k, m, S, stripes, threads):
     """Restated reference algorithm (oracle/rs_oracle_simd.c: split-nibble
     pshufb GF MAC, one stripe per thread) on a bounded sample of the workload:
-    ~10 s on `threads` host threads (default: every logical CPU of the box,
-    SURVEY.md §8d), then ~4 s on one core (the reference quotes ~110 us per
+    ~10 s on `threads` host threads (default: every CPU the process may use,
+    SURVEY.md §8d; the host's CPU count, quota and model are reported), then
+    ~4 s on one core (the reference quotes ~110 us per
     1 MiB block on one core, encode.rs:512)."""
     import numpy as np
     from oracle import oracle as O
@@ -314,7 +328,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(k, m, S, min(a.cpu_sample_stripes, n), a.cpu_threads or (os.cpu_count() or 1))
+        cpu = cpu_baseline(k, m, S, min(a.cpu_sample_stripes, n), a.cpu_threads or usable_cpus())
 
     if rank == 0:
         line = {
