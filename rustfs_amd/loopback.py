@@ -30,13 +30,14 @@ from __future__ import annotations
 
 import json
 import os
-from typing import List, Optional
+from typing import Iterator, List, Optional
 
 import numpy as np
 
 from . import _lib
 from .bitrot import HashAlgorithm, bitrot_shard_file_size
 from .erasure import Erasure, calc_shard_size
+from .pipeline import DEFAULT_BATCH_BLOCKS, DEFAULT_INFLIGHT_BATCHES, get_stream, put_stream
 
 
 class LocalErasureSet:
@@ -47,6 +48,8 @@ class LocalErasureSet:
         self.dirs = dirs
         self.erasure = Erasure(data_shards, parity_shards, block_size, device=device)
         self.algo = algo
+        self._put_stage = None  # page-locked PUT staging, reused across objects
+        self.last_put: dict = {}  # put_stream's counts and producer/consumer clocks
 
     @property
     def k(self) -> int:
@@ -86,9 +89,35 @@ class LocalErasureSet:
             with open(self._path(i, name), "wb") as f:
                 for r in records[i]:
                     f.write(r)
-        meta = {"size": int(data.size), "data_blocks": k, "parity_blocks": self.m, "block_size": bs,
-                "shard_size": S, "algorithm": self.algo.name}
-        for i in range(t):
+        return self._write_meta(name, int(data.size))
+
+    def put_object_stream(self, name: str, reader, size: int, batch_blocks: int = DEFAULT_BATCH_BLOCKS,
+                          inflight_batches: int = DEFAULT_INFLIGHT_BATCHES, read_threads: int = 4) -> dict:
+        """PUT of a `size`-byte body read from `reader` (``readinto``) without
+        holding it in memory: encode_batched's pipeline (encode.rs:795-919) —
+        B-block batches through page-locked staging, GPU encode + HH256S of
+        batch i overlapping the read of batch i+1 and the shard-file writes of
+        batch i-1.  Produces the same files as put_object."""
+        e, t = self.erasure, self.k + self.m
+        fds = []
+        try:
+            for i in range(t):
+                os.makedirs(os.path.dirname(self._path(i, name)), exist_ok=True)
+                fds.append(os.open(self._path(i, name), os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644))
+            info = put_stream(e, reader, size, fds, self.algo, batch_blocks, inflight_batches, self._put_stage,
+                              read_threads)
+            self._put_stage = info.pop("stage")
+            self.last_put = info
+        finally:
+            for fd in fds:
+                os.close(fd)
+        return self._write_meta(name, size)
+
+    def _write_meta(self, name: str, size: int) -> dict:
+        e = self.erasure
+        meta = {"size": int(size), "data_blocks": self.k, "parity_blocks": self.m, "block_size": e.block_size,
+                "shard_size": e.shard_size(), "algorithm": self.algo.name}
+        for i in range(self.k + self.m):
             with open(os.path.join(self.dirs[i], name, "meta.json"), "w") as f:
                 json.dump(meta, f)
         return meta
@@ -103,82 +132,44 @@ class LocalErasureSet:
                 continue
         raise FileNotFoundError(name)
 
-    def get_object(self, name: str) -> bytes:
-        meta = self._meta(name)
-        e, k, t = self.erasure, self.k, self.k + self.m
-        size, bs = meta["size"], meta["block_size"]
-        S = e.shard_size()
-        hs = self.algo.size()
-        want = e.shard_file_size(size)
-        files = []
-        for i in range(t):
+    def _open_shards(self, name: str, size: int) -> List[Optional[int]]:
+        """Shard file descriptors; a missing or wrong-length file is None
+        (the reader for that disk is unavailable)."""
+        e = self.erasure
+        want = bitrot_shard_file_size(e.shard_file_size(size), e.shard_size(), self.algo)
+        fds: List[Optional[int]] = []
+        for i in range(self.k + self.m):
             try:
-                f = open(self._path(i, name), "rb")
-                if os.fstat(f.fileno()).st_size != bitrot_shard_file_size(want, S, self.algo):
-                    f.close()
-                    f = None
+                fd = os.open(self._path(i, name), os.O_RDONLY)
             except OSError:
-                f = None
-            files.append(f)
-        out = bytearray()
-        left = size
-        nfull = size // bs
-        try:
-            if nfull:  # full blocks: one batched verify + rebuild on the GPU
-                out += self._get_full_blocks(files, nfull, S)
-                left -= nfull * bs
-            while left > 0:
-                blk = min(bs, left)
-                s_blk = calc_shard_size(blk, k)
-                shards: List[Optional[bytes]] = [None] * t
-                for i, f in enumerate(files):
-                    if f is None:
-                        continue
-                    rec = f.read(hs + s_blk)
-                    if len(rec) < hs + s_blk:
-                        files[i] = None
-                        continue
-                    h, body = rec[:hs], rec[hs:]
-                    if self.algo.hash_encode(body) != h:  # bitrot: drop this shard for the block
-                        continue
-                    shards[i] = body
-                if sum(s is not None for s in shards) < k:
-                    raise _lib.RsgError(_lib.RSG_ERR_TOO_FEW_SHARDS, f"read quorum lost for {name}")
-                e.decode_data_with_reconstruction_verification(shards)
-                block = b"".join(bytes(shards[i]) for i in range(k))
-                out += block[:blk]
-                left -= blk
-        finally:
-            for f in files:
-                if f is not None:
-                    f.close()
-        return bytes(out)
+                fds.append(None)
+                continue
+            if os.fstat(fd).st_size != want:
+                os.close(fd)
+                fd = None
+            fds.append(fd)
+        return fds
 
-    def _get_full_blocks(self, files, nfull: int, S: int) -> bytes:
-        """Read the nfull full-block records of every available shard file,
-        move them to the GPU and run the GET engine (rsg_decode_records_dev):
-        verify every record, rebuild missing data shards, check surplus parity."""
-        import torch
-        k, bs = self.k, self.erasure.block_size
-        rec = 32 + S
-        dev_files = []
-        for f in files:
-            if f is None:
-                dev_files.append(None)
-                continue
-            raw = f.read(nfull * rec)
-            if len(raw) < nfull * rec:
-                dev_files.append(None)
-                continue
-            # pageable H2D: pinning per object (hipHostMalloc) costs more than it saves at MiB sizes
-            dev_files.append(torch.frombuffer(bytearray(raw), dtype=torch.uint8).to("cuda"))
-        if sum(d is not None for d in dev_files) < k:
-            raise _lib.RsgError(_lib.RSG_ERR_TOO_FEW_SHARDS, "read quorum lost")
-        data, status = self.erasure.decode_records_batch(dev_files, S, nfull)
-        bad = [s for s in status if s != _lib.RSG_OK]
-        if bad:
-            _lib.check(bad[0], "erasure decode")
-        return data[:, :bs].contiguous().cpu().numpy().tobytes()
+    def get_object_stream(self, name: str, offset: int = 0, length: Optional[int] = None,
+                          batch_blocks: int = DEFAULT_BATCH_BLOCKS) -> Iterator[bytes]:
+        """Stream bytes [offset, offset + length) (default: to the end) of
+        `name`: decode_inner's range read (decode.rs:1702-1968) with full
+        blocks verified and rebuilt on the GPU B blocks at a time, the next
+        batch read from the shard files while this one decodes."""
+        size = self._meta(name)["size"]
+        fds = self._open_shards(name, size)
+        try:
+            yield from get_stream(self.erasure, fds, size, offset, length, self.algo, batch_blocks)
+        finally:
+            for fd in fds:
+                if fd is not None:
+                    os.close(fd)
+
+    def get_object_range(self, name: str, offset: int = 0, length: Optional[int] = None) -> bytes:
+        return b"".join(self.get_object_stream(name, offset, length))
+
+    def get_object(self, name: str) -> bytes:
+        return self.get_object_range(name)
 
     # ----------------------------------------------------------------- HEAL
     def heal_object(self, name: str, targets: List[int]) -> None:

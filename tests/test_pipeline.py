@@ -1,0 +1,170 @@
+"""Streaming PUT (encode_batched, encode.rs:795-919) and range GET
+(decode_inner, decode.rs:1702-1968) of the loopback erasure set.
+
+The streamed PUT must write byte-for-byte the shard files the CPU oracle
+predicts (the same files as put_object), whatever the batch size; the range
+GET must return exactly data[offset:offset+length] for ranges that start and
+end inside, on and across block boundaries and the short last block, with
+lost drives and corrupted records."""
+import io
+import os
+
+import numpy as np
+import pytest
+
+from rustfs_amd.pipeline import block_geometry
+
+BS = 1 << 16  # small blocks so a few MiB spans many batches
+
+
+def _ranges(size, bs):
+    rng = np.random.default_rng(size)
+    out = {(0, size), (0, 0), (size, 0), (0, 1), (size - 1, 1) if size else (0, 0)}
+    for b in (bs - 1, bs, bs + 1, 2 * bs, 3 * bs - 5):
+        if b <= size:
+            out.add((0, b))
+            out.add((b, size - b))
+    for _ in range(12):
+        o = int(rng.integers(0, size + 1))
+        out.add((o, int(rng.integers(0, size - o + 1))))
+    return sorted(out)
+
+
+def test_block_geometry_matches_brute_force():
+    """decode.rs:1767-1781: the per-block window of a range."""
+    bs = 10
+    for total in (1, 9, 10, 11, 35):
+        for off in range(total):
+            for ln in range(1, total - off + 1):
+                want = {}
+                for x in range(off, off + ln):
+                    b = x // bs
+                    o, n = want.get(b, (x % bs, 0))
+                    want[b] = (o, n + 1)
+                for b, (o, n) in want.items():
+                    assert block_geometry(off, ln, bs, b) == (o, n), (total, off, ln, b)
+
+
+def test_range_errors_before_any_io():
+    from rustfs_amd.erasure import Erasure
+    from rustfs_amd.pipeline import get_stream
+    e = Erasure(2, 2, BS)
+    with pytest.raises(ValueError, match="offset \\+ length exceeds total length"):
+        list(get_stream(e, [None] * 4, 100, 90, 11))
+    with pytest.raises(ValueError):
+        list(get_stream(e, [None] * 4, 100, -1, 1))
+    assert list(get_stream(e, [None] * 4, 100, 40, 0)) == []
+    assert list(get_stream(e, [None] * 4, 0)) == []
+
+
+def _set(tmp_path, k, m, bs=BS):
+    from rustfs_amd.loopback import LocalErasureSet
+    dirs = [str(tmp_path / f"disk{i}") for i in range(k + m)]
+    return LocalErasureSet(dirs, k, m, block_size=bs), dirs
+
+
+def _files(dirs, name):
+    return [open(os.path.join(d, name, "part.1"), "rb").read() for d in dirs]
+
+
+def _reader(kind, data, tmp_path):
+    """BytesIO (sequential readinto producer) or a regular file opened at an
+    offset (parallel pread producer)."""
+    if kind == "bytes":
+        return io.BytesIO(data)
+    p = tmp_path / "body"
+    p.write_bytes(b"HEAD" + data + b"TRAILER")
+    f = open(p, "rb")
+    f.seek(4)
+    return f
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["bytes", "file"])
+@pytest.mark.parametrize("k,m", [(2, 2), (8, 4), (5, 3)])
+@pytest.mark.parametrize("nblk,tail", [(0, 0), (0, 777), (1, 0), (7, 0), (7, 12345), (9, 1)])
+def test_put_stream_writes_put_object_files(gpu, oracle, tmp_path, kind, k, m, nblk, tail):
+    size = nblk * BS + tail
+    es, dirs = _set(tmp_path, k, m)
+    data = np.random.default_rng(size + k).integers(0, 256, size, dtype=np.uint8).tobytes()
+    r = _reader(kind, data, tmp_path)
+    es.put_object_stream("b/s", r, size, batch_blocks=3, inflight_batches=1)
+    if kind == "file":
+        assert r.read() == b"TRAILER"  # left positioned after the body
+    es.put_object("b/o", data)
+    got, want = _files(dirs, "b/s"), _files(dirs, "b/o")
+    assert got == want
+    # oracle: block by block [HH256S][shard] records
+    if size:
+        b0 = (nblk - 1) * BS if nblk else 0
+        blk = np.frombuffer(data[b0:b0 + BS], dtype=np.uint8)
+        S = -(-blk.size // k)
+        st = np.zeros((k + m, S), dtype=np.uint8)
+        st.reshape(-1)[: blk.size] = blk
+        oracle.encode(k, m, st)
+        off = (nblk - 1) * (32 + -(-BS // k)) if nblk else 0
+        for i in range(k + m):
+            assert got[i][off: off + 32 + S] == oracle.hh256s(st[i]) + st[i].tobytes(), i
+    assert es.get_object("b/s") == data
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["bytes", "file"])
+def test_put_stream_short_body_raises(gpu, tmp_path, kind):
+    es, _ = _set(tmp_path, 2, 2)
+    with pytest.raises(EOFError):
+        es.put_object_stream("b/s", _reader(kind, b"x" * (3 * BS), tmp_path), 5 * BS, batch_blocks=2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lost", [(), (0,), (0, 1), (1, 3)])
+def test_range_get(gpu, tmp_path, lost):
+    size = 11 * BS + 4321
+    es, dirs = _set(tmp_path, 2, 2)
+    data = np.random.default_rng(5).integers(0, 256, size, dtype=np.uint8).tobytes()
+    es.put_object_stream("b/o", io.BytesIO(data), size, batch_blocks=4)
+    for i in lost:
+        os.remove(os.path.join(dirs[i], "b/o", "part.1"))
+    for off, ln in _ranges(size, BS):
+        got = b"".join(es.get_object_stream("b/o", off, ln, batch_blocks=3))
+        assert got == data[off:off + ln], (off, ln)
+    with pytest.raises(ValueError):
+        es.get_object_range("b/o", size - 3, 4)
+
+
+@pytest.mark.gpu
+def test_range_get_drops_corrupted_records(gpu, tmp_path):
+    from rustfs_amd import RsgError
+    size = 6 * BS + 100
+    es, dirs = _set(tmp_path, 4, 2)
+    data = np.random.default_rng(6).integers(0, 256, size, dtype=np.uint8).tobytes()
+    es.put_object_stream("b/o", io.BytesIO(data), size, batch_blocks=2)
+    rec = 32 + BS // 4
+
+    def flip(i, off):
+        p = os.path.join(dirs[i], "b/o", "part.1")
+        raw = bytearray(open(p, "rb").read())
+        raw[off] ^= 0x40
+        open(p, "wb").write(bytes(raw))
+
+    flip(0, 3 * rec + 32 + 7)   # block 3, data shard 0 body
+    flip(5, 3 * rec + 1)        # block 3, parity shard 5 digest
+    flip(1, 6 * rec + 32 + 10)  # tail block (25-byte shards), data shard 1
+    assert es.get_object_range("b/o", 2 * BS + 10, 4 * BS) == data[2 * BS + 10: 6 * BS + 10]
+    assert es.get_object("b/o") == data
+    flip(2, 3 * rec + 40)       # a third bad record in block 3: below read quorum
+    with pytest.raises(RsgError):
+        es.get_object_range("b/o", 3 * BS, 10)
+    assert es.get_object_range("b/o", 0, 3 * BS) == data[: 3 * BS]  # other blocks still read
+
+
+@pytest.mark.gpu
+def test_stream_close_early(gpu, tmp_path):
+    size = 20 * BS
+    es, _ = _set(tmp_path, 2, 2)
+    data = np.random.default_rng(8).integers(0, 256, size, dtype=np.uint8).tobytes()
+    es.put_object_stream("b/o", io.BytesIO(data), size)
+    g = es.get_object_stream("b/o", BS // 2, batch_blocks=4)
+    assert next(g) == data[BS // 2: BS]
+    g.close()  # joins the read-ahead thread, closes the shard files
+    assert es.get_object("b/o") == data
