@@ -1,6 +1,6 @@
 """One engine call repeated (for rocprofv3 --kernel-trace --stats): GET with
 two data disks lost, or heal, RS(8,4) 1 MiB stripes, n = 4096 records.
-Usage: python tools/engine_prof.py get2|get0|heal [reps]"""
+Usage: python tools/engine_prof.py get2|get2_01|get1|get0|heal [reps]"""
 import os
 import sys
 
@@ -16,6 +16,10 @@ def main():
     S, t = 131072, 12
     rec = 32 + S
     e = Erasure(k, m, 1 << 20)
+    early = os.environ.get("EP_FILES_FIRST") == "1"  # allocate the record files and output before the staging
+    if early:
+        files = [torch.empty(n * rec, dtype=torch.uint8, device="cuda") for _ in range(t)]
+        out = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
     st = torch.zeros((n, t, S), dtype=torch.uint8, device="cuda")
     g = torch.Generator(device="cuda").manual_seed(5)
     for s0 in range(0, n, 256):
@@ -23,20 +27,23 @@ def main():
                                             generator=g)
     dig = torch.empty((n, t, 32), dtype=torch.uint8, device="cuda")
     e.encode_batch(st, dig)
-    files = []
+    if not early:
+        files = [torch.empty(n * rec, dtype=torch.uint8, device="cuda") for _ in range(t)]
     for i in range(t):
-        f = torch.empty((n, rec), dtype=torch.uint8, device="cuda")
+        f = files[i].view(n, rec)
         f[:, :32] = dig[:, i]
         f[:, 32:] = st[:, i]
-        files.append(f.reshape(-1))
     del st, dig
-    out = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
+    if os.environ.get("EP_BAD_PARITY") == "1":  # surplus parity 10 inconsistent in every stripe (compare mismatch)
+        files[10].view(n, rec)[:, 32:] ^= 0x5A
+    if not early:
+        out = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
     for _ in range(reps):
         if what == "heal":
             tg = [torch.empty(n * rec, dtype=torch.uint8, device="cuda") if i in (1, k) else None for i in range(t)]
             e.heal_records_batch([None if i in (1, k) else files[i] for i in range(t)], tg, S, n)
         else:
-            lost = (0, 3) if what == "get2" else ()
+            lost = {"get2": (0, 3), "get2_01": (0, 1), "get1": (0,)}.get(what, ())
             e.decode_records_batch([None if i in lost else files[i] for i in range(t)], S, n, out=out)
     torch.cuda.synchronize()
     print("done", what, reps)
