@@ -194,17 +194,26 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(2))) void k_g
     for (int c = 0; c < C; ++c) x[c] = ld16(sbase + p.in_off[c] + off);
     uint4 old[R];
     if constexpr (PRE) gf_preload<R>(p, obase, off, stripe, old);
-    if (PRE && p.copy_mask) {  // wave-uniform
-#pragma unroll
-        for (int c = 0; c < C; ++c)
-            if ((p.copy_mask >> c) & 1u) st16(obase + p.copy_off[c] + off, x[c]);
-    }
     uint32_t acc[R][4];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0u;
     gf_accumulate<0, C, R>(p, x, acc);
     if constexpr (PRE) gf_store<R>(p, obase, off, acc, stripe, old);
     else gf_store_late<R>(p, obase, off, acc, stripe);
+    // Copy-through last, with non-temporal stores (written once, never read
+    // back by this pass): GET with 2 data shards lost (6 copies, 2 rebuilt, 2
+    // compared) 1.85 ms with the copies among the input loads, 1.61 ms here,
+    // 1.58 ms non-temporal (tools/kbench/get_probe.hip).
+    if (PRE && p.copy_mask) {  // wave-uniform
+        // any alignment (S need not be a multiple of 16): unaligned-access mode
+        typedef uint32_t v4u_any __attribute__((ext_vector_type(4), aligned(1)));
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+            if ((p.copy_mask >> c) & 1u) {
+                const v4u_any w = {x[c].x, x[c].y, x[c].z, x[c].w};
+                __builtin_nontemporal_store(w, (v4u_any*)(obase + p.copy_off[c] + off));
+            }
+    }
 }
 
 // Rolled over the inputs in groups of G=8 (any C <= 16, R <= 8): the next

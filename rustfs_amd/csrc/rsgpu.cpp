@@ -510,6 +510,24 @@ struct rsg_ctx {
     };
     std::map<uint64_t, Job> jobs;
 
+    // page-locked mirror of the flag scratch: the verdict D2H of the record
+    // engines is a few tens of KB, where a pageable copy's staging costs more
+    // than the copy (ctx->mu held)
+    uint8_t* h_flags = nullptr;
+    size_t h_flags_cap = 0;
+
+    int ensure_host_flags(size_t bytes) {
+        if (bytes <= h_flags_cap) return RSG_OK;
+        if (h_flags) (void)hipHostFree(h_flags);
+        h_flags = nullptr;
+        h_flags_cap = 0;
+        const size_t want = std::max(bytes, (size_t)64 << 10);
+        hipError_t e = hipHostMalloc((void**)&h_flags, want, hipHostMallocDefault);
+        if (e != hipSuccess) return hip_status(e);
+        h_flags_cap = want;
+        return RSG_OK;
+    }
+
     int ensure_scratch(size_t bytes) {
         if (bytes <= scratch_cap) return RSG_OK;
         if (d_scratch) (void)hipFree(d_scratch);
@@ -679,6 +697,7 @@ void rsg_destroy(rsg_ctx* ctx) {
         (void)hipStreamDestroy(ctx->stream);
     }
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+    if (ctx->h_flags) (void)hipHostFree(ctx->h_flags);
     for (HostLane& l : ctx->lanes) {
         if (l.stream) {
             (void)hipStreamSynchronize(l.stream);
@@ -1008,8 +1027,17 @@ int launch_verify_group(const std::vector<int>& idx, const uint8_t* const* d_fil
                         uint8_t* d_out, hipStream_t s) {
     const uint64_t rec = 32 + shard_len;
     int st;
-    for (int i : idx)
-        if ((st = hip_status(hipMemsetAsync(d_flags + (size_t)i * n + lo, 1, hi - lo, s)))) return st;
+    if (lo == 0 && hi == n) {  // whole flag rows: one memset per run of consecutive files
+        for (size_t a = 0; a < idx.size();) {
+            size_t b = a + 1;
+            while (b < idx.size() && idx[b] == idx[b - 1] + 1) ++b;
+            if ((st = hip_status(hipMemsetAsync(d_flags + (size_t)idx[a] * n, 1, (b - a) * n, s)))) return st;
+            a = b;
+        }
+    } else {
+        for (int i : idx)
+            if ((st = hip_status(hipMemsetAsync(d_flags + (size_t)i * n + lo, 1, hi - lo, s)))) return st;
+    }
     for (size_t g0 = 0; g0 < idx.size(); g0 += rsg::kMaxHashBases) {
         const size_t g1 = std::min(idx.size(), g0 + (size_t)rsg::kMaxHashBases);
         rsg::HashParams h;
@@ -1030,6 +1058,17 @@ int launch_verify_group(const std::vector<int>& idx, const uint8_t* const* d_fil
         }
         if ((st = hip_status(rsg::launch_hh256(h, s)))) return st;
     }
+    return RSG_OK;
+}
+
+// Device flags -> host through the context's page-locked buffer, stream
+// synchronised on return.
+int flags_to_host(rsg_ctx* ctx, const uint8_t* d_src, size_t bytes, uint8_t* dst, hipStream_t s) {
+    int st;
+    if ((st = ctx->ensure_host_flags(bytes))) return st;
+    if ((st = hip_status(hipMemcpyAsync(ctx->h_flags, d_src, bytes, hipMemcpyDeviceToHost, s)))) return st;
+    if ((st = hip_status(hipStreamSynchronize(s)))) return st;
+    std::memcpy(dst, ctx->h_flags, bytes);
     return RSG_OK;
 }
 
@@ -1055,13 +1094,10 @@ int verify_gather(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64_t n, co
         // every stripe needs its parity (heal, or a lost data disk): all
         // present records of all stripes in one launch, data gathered
         if ((st = launch_verify_group(all_idx, d_files, d_flags, k, shard_len, n, 0, n, key, d_out, s))) return st;
-        if ((st = hip_status(hipMemcpyAsync(flags.data(), d_flags, (size_t)t * n, hipMemcpyDeviceToHost, s))))
-            return st;
-        return hip_status(hipStreamSynchronize(s));
+        return flags_to_host(ctx, d_flags, (size_t)t * n, flags.data(), s);
     }
     if ((st = launch_verify_group(data_idx, d_files, d_flags, k, shard_len, n, 0, n, key, d_out, s))) return st;
-    if ((st = hip_status(hipMemcpyAsync(flags.data(), d_flags, (size_t)k * n, hipMemcpyDeviceToHost, s)))) return st;
-    if ((st = hip_status(hipStreamSynchronize(s)))) return st;
+    if ((st = flags_to_host(ctx, d_flags, (size_t)k * n, flags.data(), s))) return st;
     uint64_t lo = n, hi = 0;
     if (all_parity) {
         lo = 0;
@@ -1078,10 +1114,7 @@ int verify_gather(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64_t n, co
     }
     if (lo >= hi || par_idx.empty()) return RSG_OK;
     if ((st = launch_verify_group(par_idx, d_files, d_flags, k, shard_len, n, lo, hi, key, nullptr, s))) return st;
-    if ((st = hip_status(hipMemcpyAsync(flags.data() + (size_t)k * n, d_flags + (size_t)k * n, (size_t)m * n,
-                                        hipMemcpyDeviceToHost, s))))
-        return st;
-    return hip_status(hipStreamSynchronize(s));
+    return flags_to_host(ctx, d_flags + (size_t)k * n, (size_t)m * n, flags.data() + (size_t)k * n, s);
 }
 
 // GET engine body (ctx->mu held): verify records, copy/rebuild the k data
@@ -1199,16 +1232,28 @@ int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64
         for (int i = 0; i < t; ++i)
             if (d_files[i]) all_idx.push_back(i);
         if ((st = launch_verify_group(all_idx, d_files, d_flags, k, shard_len, n, 0, n, key, nullptr, s))) return st;
-        flags.assign((size_t)t * n, 0);
-        if ((st = hip_status(hipMemcpyAsync(flags.data(), d_flags, (size_t)t * n, hipMemcpyDeviceToHost, s))))
+        // the verified map and the surplus verdict (adjacent in scratch) in one
+        // copy and one synchronisation; a second one only if a run is redone
+        if ((st = ctx->ensure_host_flags((size_t)(t + 1) * n))) return st;
+        if ((st = hip_status(hipMemcpyAsync(ctx->h_flags, d_flags, (size_t)(t + 1) * n, hipMemcpyDeviceToHost, s))))
             return st;
         if ((st = hip_status(hipStreamSynchronize(s)))) return st;
+        flags.assign(ctx->h_flags, ctx->h_flags + (size_t)t * n);
+        bool redone = false;
         st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) -> int {
             if (present == present0) return RSG_OK;  // the optimistic pass was right
+            redone = true;
             int e = hip_status(hipMemsetAsync(d_ok + s0, 1, s1 - s0, s));
             return e ? e : rebuild_run(s0, s1, present, true);
         });
         if (st) return st;
+        if (!redone) {
+            if (any_verify)
+                for (uint64_t x = 0; x < n; ++x)
+                    if (h_status[x] == RSG_OK && !ctx->h_flags[(size_t)t * n + x])
+                        h_status[x] = RSG_ERR_INCONSISTENT_SOURCES;
+            return RSG_OK;  // the stream was synchronised after the last launch
+        }
     } else {
         // verify the data records and gather them into d_out; parity where needed
         if ((st = verify_gather(ctx, k, m, shard_len, n, d_files, key, d_out, false, flags, s))) return st;
@@ -1218,11 +1263,11 @@ int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64
         if (st) return st;
     }
     if (any_verify) {
-        std::vector<uint8_t> ok(n, 1);
-        if ((st = hip_status(hipMemcpyAsync(ok.data(), d_ok, n, hipMemcpyDeviceToHost, s)))) return st;
+        if ((st = ctx->ensure_host_flags(n))) return st;
+        if ((st = hip_status(hipMemcpyAsync(ctx->h_flags, d_ok, n, hipMemcpyDeviceToHost, s)))) return st;
         if ((st = hip_status(hipStreamSynchronize(s)))) return st;
         for (uint64_t x = 0; x < n; ++x)
-            if (h_status[x] == RSG_OK && !ok[x]) h_status[x] = RSG_ERR_INCONSISTENT_SOURCES;
+            if (h_status[x] == RSG_OK && !ctx->h_flags[x]) h_status[x] = RSG_ERR_INCONSISTENT_SOURCES;
     }
     return hip_status(hipStreamSynchronize(s));
 }
@@ -1329,8 +1374,7 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
     if ((st = hash_records_inplace(d_targets, t, shard_len, n, key, s))) return st;
     if (any_verify) {
         std::vector<uint8_t> ok(n, 1);
-        if ((st = hip_status(hipMemcpyAsync(ok.data(), d_ok, n, hipMemcpyDeviceToHost, s)))) return st;
-        if ((st = hip_status(hipStreamSynchronize(s)))) return st;
+        if ((st = flags_to_host(ctx, d_ok, n, ok.data(), s))) return st;
         for (uint64_t x = 0; x < n; ++x)
             if (h_status[x] == RSG_OK && !ok[x]) h_status[x] = RSG_ERR_INCONSISTENT_SOURCES;
     }
@@ -1430,10 +1474,11 @@ int rsg_bitrot_verify_dev(rsg_ctx* ctx, int algo, size_t n_files, const uint8_t*
         }
     }
     std::vector<uint8_t> flags(streaming ? (size_t)recs * n_files : 0);
-    if (!flags.empty() &&
-        (st = hip_status(hipMemcpyAsync(flags.data(), ctx->d_scratch, flags.size(), hipMemcpyDeviceToHost, s))))
+    if (!flags.empty()) {
+        if ((st = flags_to_host(ctx, ctx->d_scratch, flags.size(), flags.data(), s))) return st;
+    } else if ((st = hip_status(hipStreamSynchronize(s)))) {
         return st;
-    if ((st = hip_status(hipStreamSynchronize(s)))) return st;
+    }
     // the reference reads records in order: the first bad or missing one decides
     for (size_t f = 0; f < n_files; ++f) {
         int res = RSG_OK;

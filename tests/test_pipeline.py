@@ -117,10 +117,13 @@ def test_put_stream_short_body_raises(gpu, tmp_path, kind):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("lost", [(), (0,), (0, 1), (1, 3)])
-def test_range_get(gpu, tmp_path, lost):
+@pytest.mark.parametrize("k,m,lost", [(2, 2, ()), (2, 2, (0,)), (2, 2, (0, 1)), (2, 2, (1, 3)),
+                                      (6, 3, (0, 4)), (20, 4, (1, 19)), (20, 4, (0, 21))])
+def test_range_get(gpu, tmp_path, k, m, lost):
+    """(6,3) and (20,4): shard lengths that are not multiples of 16 (the byte
+    tail and unaligned copy-through), k > 16 (chained launches, wide compare)."""
     size = 11 * BS + 4321
-    es, dirs = _set(tmp_path, 2, 2)
+    es, dirs = _set(tmp_path, k, m)
     data = np.random.default_rng(5).integers(0, 256, size, dtype=np.uint8).tobytes()
     es.put_object_stream("b/o", io.BytesIO(data), size, batch_blocks=4)
     for i in lost:

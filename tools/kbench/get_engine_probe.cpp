@@ -3,7 +3,7 @@
 // records of 1 MiB blocks per shard file, shard files as separate hipMallocs,
 // data shards `lost` absent.  Times whole calls with host clocks; run under
 // rocprofv3 --kernel-trace for per-kernel times.  Measurement code.
-// Usage: get_engine_probe [n] [lost mask] [reps]
+// Usage: get_engine_probe [n] [lost mask] [reps] [corrupt mask]
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -30,6 +30,7 @@ int main(int argc, char** argv) {
     const size_t n = argc > 1 ? atoi(argv[1]) : 4096;
     const unsigned lost = argc > 2 ? strtoul(argv[2], nullptr, 0) : 0x3;
     const int reps = argc > 3 ? atoi(argv[3]) : 5;
+    const unsigned corrupt = argc > 4 ? strtoul(argv[4], nullptr, 0) : 0;  // shard files whose bodies are inverted
     const int k = 8, m = 4, t = k + m;
     const size_t S = 131072, rec = 32 + S;
     rsg_ctx* ctx;
@@ -46,6 +47,8 @@ int main(int argc, char** argv) {
         CK(hipMemcpy2D(files[i], rec, dig + i * 32, t * 32, 32, n, hipMemcpyDeviceToDevice));
         CK(hipMemcpy2D(files[i] + 32, rec, st + i * S, t * S, S, n, hipMemcpyDeviceToDevice));
     }
+    for (int i = 0; i < t; ++i)
+        if ((corrupt >> i) & 1) k_fill<<<4096, 256>>>(files[i] + 32, n * rec - 64, 99 + i);  // rotten records
     CK(hipFree(st));
     CK(hipFree(dig));
     uint8_t* out;

@@ -20,6 +20,7 @@ using namespace rsg;
 // ORDER 0: production order (preload, copy, accumulate, store)
 // ORDER 1: copies after the rebuilt rows' stores
 // ORDER 2: compare operands loaded late (at the compare), copies first
+// ORDER 3: as 1 with non-temporal copy stores
 template <int C, int R, int WPE, int ORDER>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_get(const GfApplyParams p) {
     const uint32_t stripe = blockIdx.x / p.chunks_per_stripe;
@@ -34,7 +35,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     for (int c = 0; c < C; ++c) x[c] = ld16(sbase + p.in_off[c] + off);
     uint4 old[R];
     if (ORDER != 2) gf_preload<R>(p, obase, off, stripe, old);
-    if (ORDER != 1 && p.copy_mask) {
+    if (ORDER != 1 && ORDER != 3 && p.copy_mask) {
 #pragma unroll
         for (int c = 0; c < C; ++c)
             if ((p.copy_mask >> c) & 1u) st16(obase + p.copy_off[c] + off, x[c]);
@@ -49,6 +50,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 #pragma unroll
         for (int c = 0; c < C; ++c)
             if ((p.copy_mask >> c) & 1u) st16(obase + p.copy_off[c] + off, x[c]);
+    }
+    if (ORDER == 3 && p.copy_mask) {  // at the end, non-temporal
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+            if ((p.copy_mask >> c) & 1u) {
+                v4u w = {x[c].x, x[c].y, x[c].z, x[c].w};
+                __builtin_nontemporal_store(w, (v4u*)(obase + p.copy_off[c] + off));
+            }
     }
 }
 
@@ -118,7 +128,9 @@ int main(int argc, char** argv) {
                 auto pack = [&](int sh, int f) { uint32_t v = 0; for (int q = 0; q < 4; ++q) v |= (uint32_t)gm(co, (uint8_t)((f + q) << sh)) << (8 * q); return v; };
                 p.tab[r][c][0] = pack(0, 0); p.tab[r][c][1] = pack(0, 4); p.tab[r][c][2] = pack(3, 0); p.tab[r][c][3] = pack(3, 4); p.tab[r][c][4] = pack(6, 0);
             }
-            p.out_off[r] = (uint64_t)(file(surv[r - 2]) - out);
+            // the target: a copy of input r-2's file in parity file 8+r (distinct memory, equal bytes)
+            CK(hipMemcpy(file(8 + r) - 32, file(surv[r - 2]) - 32, (uint64_t)n * rec, hipMemcpyDeviceToDevice));
+            p.out_off[r] = (uint64_t)(file(8 + r) - out);
         }
     }
     p.C = 8; p.R = 4; p.units = S / 16; p.chunks_per_stripe = (p.units + 63) / 64;
@@ -131,6 +143,7 @@ int main(int argc, char** argv) {
         {"wpe2 order0", k_get<8, 4, 2, 0>}, {"wpe3 order0", k_get<8, 4, 3, 0>}, {"wpe4 order0", k_get<8, 4, 4, 0>},
         {"wpe2 order1", k_get<8, 4, 2, 1>}, {"wpe3 order1", k_get<8, 4, 3, 1>}, {"wpe4 order1", k_get<8, 4, 4, 1>},
         {"wpe2 order2", k_get<8, 4, 2, 2>}, {"wpe3 order2", k_get<8, 4, 3, 2>}, {"wpe4 order2", k_get<8, 4, 4, 2>},
+        {"wpe2 order3", k_get<8, 4, 2, 3>}, {"wpe3 order3", k_get<8, 4, 3, 3>},
     };
     // interleave: the engine's verify launch (10 present record files) before every GF launch
     const bool inter = argc > 3 && atoi(argv[3]);
