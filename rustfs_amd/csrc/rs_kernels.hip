@@ -90,6 +90,13 @@ __device__ __forceinline__ uint4 ld16(const uint8_t* p) {
     return v;
 }
 __device__ __forceinline__ void st16(uint8_t* p, const uint4& v) { __builtin_memcpy(p, &v, 16); }
+// Non-temporal 16-byte store at any alignment (unaligned-access mode): for
+// output that this pass never reads back (GET's gathered data).
+typedef uint32_t v4u_any __attribute__((ext_vector_type(4), aligned(1)));
+__device__ __forceinline__ void st16_nt(uint8_t* p, const uint4& v) {
+    const v4u_any w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, (v4u_any*)p);
+}
 
 // Output row r of a launch: its effective mode and address.
 __device__ __forceinline__ uint8_t* gf_dst(const GfApplyParams& p, uint8_t* obase, uint64_t off, int r, uint32_t stripe,
@@ -205,14 +212,9 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(2))) void k_g
     // compared) 1.85 ms with the copies among the input loads, 1.61 ms here,
     // 1.58 ms non-temporal (tools/kbench/get_probe.hip).
     if (PRE && p.copy_mask) {  // wave-uniform
-        // any alignment (S need not be a multiple of 16): unaligned-access mode
-        typedef uint32_t v4u_any __attribute__((ext_vector_type(4), aligned(1)));
 #pragma unroll
         for (int c = 0; c < C; ++c)
-            if ((p.copy_mask >> c) & 1u) {
-                const v4u_any w = {x[c].x, x[c].y, x[c].z, x[c].w};
-                __builtin_nontemporal_store(w, (v4u_any*)(obase + p.copy_off[c] + off));
-            }
+            if ((p.copy_mask >> c) & 1u) st16_nt(obase + p.copy_off[c] + off, x[c]);
     }
 }
 
@@ -529,7 +531,7 @@ __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
                 const uint4 v = *(const uint4*)(stg + (4 * kk + (lane >> 4)) * 256u + (lane & 15u) * 16u);
-                if (sdst[kk]) st16(sdst[kk] + t0 * 32, v);
+                if (sdst[kk]) st16_nt(sdst[kk] + t0 * 32, v);
             }
         }
     };

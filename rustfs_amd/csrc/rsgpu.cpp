@@ -1061,6 +1061,45 @@ int launch_verify_group(const std::vector<int>& idx, const uint8_t* const* d_fil
     return RSG_OK;
 }
 
+// One multi-file hash launch (per kMaxHashBases files) that verifies the
+// records of the files in `idx` (flags[i*n + s] cleared on a mismatch; the
+// caller sets the present rows to 1 first) and writes the digest header of
+// every record of every non-null target file (BitrotWriter framing).
+int launch_verify_and_digest(const std::vector<int>& idx, const uint8_t* const* d_files, uint8_t* d_flags,
+                             uint8_t* const* d_targets, int t, uint64_t shard_len, uint64_t n, const uint64_t* key,
+                             hipStream_t s) {
+    const uint64_t rec = 32 + shard_len;
+    int st;
+    for (size_t a = 0; a < idx.size();) {  // present rows to 1: one memset per run of consecutive files
+        size_t b = a + 1;
+        while (b < idx.size() && idx[b] == idx[b - 1] + 1) ++b;
+        if ((st = hip_status(hipMemsetAsync(d_flags + (size_t)idx[a] * n, 1, (b - a) * n, s)))) return st;
+        a = b;
+    }
+    std::vector<std::pair<uint8_t*, uint8_t*>> list;  // (record 0 body, flag row or null = write digest)
+    for (int i : idx) list.push_back({const_cast<uint8_t*>(d_files[i]) + 32, d_flags + (size_t)i * n});
+    for (int i = 0; i < t; ++i)
+        if (d_targets[i]) list.push_back({d_targets[i] + 32, nullptr});
+    for (size_t g0 = 0; g0 < list.size(); g0 += rsg::kMaxHashBases) {
+        const size_t g1 = std::min(list.size(), g0 + (size_t)rsg::kMaxHashBases);
+        rsg::HashParams h;
+        std::memset(&h, 0, sizeof(h));
+        h.len = shard_len;
+        h.per_base = n;
+        h.n = (g1 - g0) * n;
+        h.stripe_stride = rec;
+        std::memcpy(h.key, key, sizeof(h.key));
+        h.nbases = (uint32_t)(g1 - g0);
+        h.digest_off = -32;
+        for (size_t x = g0; x < g1; ++x) {
+            h.base[x - g0] = list[x].first;
+            h.flag_base[x - g0] = list[x].second;
+        }
+        if ((st = hip_status(rsg::launch_hh256(h, s)))) return st;
+    }
+    return RSG_OK;
+}
+
 // Device flags -> host through the context's page-locked buffer, stream
 // synchronised on return.
 int flags_to_host(rsg_ctx* ctx, const uint8_t* d_src, size_t bytes, uint8_t* dst, hipStream_t s) {
@@ -1311,23 +1350,20 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
     const uint64_t rec = 32 + shard_len, ks = (uint64_t)k * shard_len;
     hipStream_t s = pick_stream(ctx, stream);
     std::lock_guard<std::mutex> g(ctx->mu);
-    // 1. verify every source record in place (read quorum: k verified shards
-    //    per stripe); nothing is gathered
-    std::vector<uint8_t> flags;
     if ((st = ctx->ensure_scratch((size_t)(t + 1) * n))) return st;
-    if ((st = verify_gather(ctx, k, m, shard_len, n, d_files, key, nullptr, true, flags, s))) return st;
     auto cd = get_codec(k, m);
     if (!cd) return RSG_ERR_INVALID_ARG;
-    // 2. per run of stripes with one verified pattern, ONE pass over the
-    //    survivors (first k verified shards) writes every target's record
-    //    body — data rebuilt or, if verified, reproduced (identity row), parity
-    //    re-encoded — and compares every verified source parity that is not a
-    //    survivor with its re-encoded value: "inconsistent heal source shards"
-    //    (heal.rs:180-196; a survivor parity re-encodes to itself)
+    uint8_t* d_flags = ctx->d_scratch;
     uint8_t* d_ok = ctx->d_scratch + (size_t)t * n;
     if ((st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
     bool any_verify = false;
-    st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) -> int {
+    // Per run of stripes with one verified pattern, ONE pass over the
+    // survivors (first k verified shards) writes every target's record body —
+    // data rebuilt or, if verified, reproduced (identity row), parity
+    // re-encoded — and compares every verified source parity that is not a
+    // survivor with its re-encoded value: "inconsistent heal source shards"
+    // (heal.rs:180-196; a survivor parity re-encodes to itself).
+    auto heal_run = [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) -> int {
         int valid = 0;
         for (int i = 0; i < t; ++i) valid += present[i];
         for (uint64_t x = s0; x < s1; ++x) h_status[x] = valid < k ? RSG_ERR_TOO_FEW_SHARDS : RSG_OK;
@@ -1366,18 +1402,67 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
         int e = apply_rows(ps, base, ob, rec, rec, shard_len, s1 - s0, rsg::GF_MODE_STORE, nullptr, s);
         if (e || !vs.R) return e;
         return apply_rows(vs, base, ob, rec, rec, shard_len, s1 - s0, rsg::GF_MODE_COMPARE, d_ok + s0, s);
-    });
-    if (st) return st;
+    };
+    // the target records of stripes [s0, s1) get their HH256S headers
+    auto hash_targets = [&](uint64_t s0, uint64_t s1) -> int {
+        std::vector<uint8_t*> tg(t, nullptr);
+        for (int i = 0; i < t; ++i)
+            if (d_targets[i]) tg[i] = d_targets[i] + s0 * rec;
+        return hash_records_inplace(tg.data(), t, shard_len, s1 - s0, key, s);
+    };
+    std::vector<uint8_t> present0(t), flags;
+    int valid0 = 0;
+    for (int i = 0; i < t; ++i) valid0 += (present0[i] = d_files[i] ? 1 : 0);
+    bool done = false;
+    if (valid0 >= k && lost_disk_fast_enabled()) {
+        // Optimistic (replaced disks, sound sources — the common heal): the GF
+        // pass first, as if every present record verifies; then ONE hash launch
+        // verifies every present record and writes every target's digest; one
+        // copy + synchronisation brings back the verified map and the parity
+        // verdict.  Runs whose verified pattern differs are redone (targets
+        // rewritten and rehashed) from their actual valid shards.
+        if ((st = heal_run(0, n, present0))) return st;
+        if ((st = hip_status(hipMemsetAsync(d_flags, 0, (size_t)t * n, s)))) return st;
+        std::vector<int> all_idx;
+        for (int i = 0; i < t; ++i)
+            if (d_files[i]) all_idx.push_back(i);
+        if ((st = launch_verify_and_digest(all_idx, d_files, d_flags, d_targets, t, shard_len, n, key, s))) return st;
+        if ((st = ctx->ensure_host_flags((size_t)(t + 1) * n))) return st;
+        if ((st = hip_status(hipMemcpyAsync(ctx->h_flags, d_flags, (size_t)(t + 1) * n, hipMemcpyDeviceToHost, s))))
+            return st;
+        if ((st = hip_status(hipStreamSynchronize(s)))) return st;
+        flags.assign(ctx->h_flags, ctx->h_flags + (size_t)t * n);
+        std::vector<uint8_t> ok(ctx->h_flags + (size_t)t * n, ctx->h_flags + (size_t)(t + 1) * n);
+        bool redone = false;
+        st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) -> int {
+            if (present == present0) return RSG_OK;
+            redone = true;
+            int e = hip_status(hipMemsetAsync(d_ok + s0, 1, s1 - s0, s));
+            if (!e) e = heal_run(s0, s1, present);
+            return e ? e : hash_targets(s0, s1);
+        });
+        if (st) return st;
+        if (redone && any_verify && (st = flags_to_host(ctx, d_ok, n, ok.data(), s))) return st;
+        if (any_verify)
+            for (uint64_t x = 0; x < n; ++x)
+                if (h_status[x] == RSG_OK && !ok[x]) h_status[x] = RSG_ERR_INCONSISTENT_SOURCES;
+        done = true;
+    }
+    if (!done) {
+        // verify every source record in place first (read quorum: k verified
+        // shards per stripe), then the per-pattern GF passes, then the digests
+        if ((st = verify_gather(ctx, k, m, shard_len, n, d_files, key, nullptr, true, flags, s))) return st;
+        if ((st = for_each_pattern_run(t, n, flags, heal_run))) return st;
+        if ((st = hash_targets(0, n))) return st;
+        if (any_verify) {
+            std::vector<uint8_t> ok(n, 1);
+            if ((st = flags_to_host(ctx, d_ok, n, ok.data(), s))) return st;
+            for (uint64_t x = 0; x < n; ++x)
+                if (h_status[x] == RSG_OK && !ok[x]) h_status[x] = RSG_ERR_INCONSISTENT_SOURCES;
+        }
+    }
     (void)d_work;
     (void)ks;
-    // 3. every target record gets its HH256S header (BitrotWriter::write)
-    if ((st = hash_records_inplace(d_targets, t, shard_len, n, key, s))) return st;
-    if (any_verify) {
-        std::vector<uint8_t> ok(n, 1);
-        if ((st = flags_to_host(ctx, d_ok, n, ok.data(), s))) return st;
-        for (uint64_t x = 0; x < n; ++x)
-            if (h_status[x] == RSG_OK && !ok[x]) h_status[x] = RSG_ERR_INCONSISTENT_SOURCES;
-    }
     // A failed stripe's target records hold unverified bytes: their digest
     // headers are zeroed so they can never pass bitrot verification even if a
     // caller ignores h_status (the reference writes nothing for a failed heal).

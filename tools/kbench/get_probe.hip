@@ -3,7 +3,7 @@
 // in place from 12 record files, data 0 and 1 rebuilt into the output, data
 // 2..7 copied through, parity 10 and 11 re-derived and compared.  The
 // production PRE kernel against register-capped and reordered variants.
-// Measurement code.  Usage: get_probe [n] [separate files 0|1] [verify launch before each GF launch 0|1] [round file allocations to this many bytes] [compare rows match 0|1]
+// Measurement code.  Usage: get_probe [n] [separate files 0|1] [verify launch before each GF launch 0|1] [round file allocations to this many bytes] [compare rows match 0|1] [no copy-through 0|1]
 #include "../../rustfs_amd/csrc/rs_kernels.hip"
 
 #include <stdio.h>
@@ -112,7 +112,8 @@ int main(int argc, char** argv) {
     p.mode = GF_MODE_STORE_COMPARE;
     p.n_store = 2;
     p.ok_flags = ok;
-    for (int c = 0; c < 6; ++c) {
+    const bool nocopy = argc > 6 && atoi(argv[6]);  // heal shape: no copy-through
+    for (int c = 0; c < 6 && !nocopy; ++c) {
         p.copy_mask |= 1u << c;
         p.copy_off[c] = (uint64_t)(2 + c) * S;
     }
@@ -191,7 +192,7 @@ int main(int argc, char** argv) {
     std::vector<uint8_t> okh(n);
     CK(hipMemcpy(okh.data(), ok, n, hipMemcpyDeviceToHost));
     printf("ok flags of the last launch: %d of %u stripes consistent\n", (int)std::count(okh.begin(), okh.end(), 1), n);
-    const double alg = (double)n * S * (8 + 2 + 2 + 6);  // reads 8 + 2 compared, writes 2 rebuilt + 6 copied
+    const double alg = (double)n * S * (8 + 2 + 2 + (nocopy ? 0 : 6));  // reads 8 + 2 compared, writes 2 rebuilt (+ 6 copied)
     for (size_t v = 0; v < vs.size(); ++v) {
         auto& x = t[v];
         std::sort(x.begin(), x.end());
