@@ -988,13 +988,21 @@ static int vec_block() {
 // runs; default 0 = whatever their registers allow, 3 for the 163-VGPR
 // RS(8,4) encode).  Enforced with an otherwise unused dynamic LDS allocation
 // per one-wave workgroup: 160 KiB / (4 SIMDs x occ) each.
-static int vec_occupancy() {
-    static const int occ = [] {
+// Resident waves per SIMD for a vector GF launch, imposed through padding LDS
+// (0 = as many as the registers allow).  RSG_VEC_OCC=<n> forces n for every
+// launch (A/B runs, tools/ab_occ.sh).  Default: 2 for the read-heavy
+// rebuilds of one or two shards from 8 inputs, where fewer waves in flight
+// stream better (RS(8,4) n = 4096: 1 lost 0.846 -> 0.814 ms, 2 lost 0.905 ->
+// 0.888 ms; profiles/r02/ab_occ2/), else no cap.
+static int vec_occupancy(int C, int R, bool pre) {
+    static const int forced = [] {
         const char* e = std::getenv("RSG_VEC_OCC");
-        const int v = e ? std::atoi(e) : 0;
+        if (!e) return -1;
+        const int v = std::atoi(e);
         return (v < 0 || v > 8) ? 0 : v;
     }();
-    return occ;
+    if (forced >= 0) return forced;
+    return (!pre && C == 8 && R <= 2) ? 2 : 0;
 }
 
 static GfKernel pick_vec(int C, int R, bool pre) {
@@ -1017,13 +1025,14 @@ static GfKernel pick_byte(int R) {
 }
 
 hipError_t launch_gf_apply_vec(GfApplyParams p, uint64_t n_stripes, hipStream_t stream) {
-    GfKernel k = pick_vec((int)p.C, (int)p.R, p.mode != GF_MODE_STORE || p.copy_mask != 0);
+    const bool pre = p.mode != GF_MODE_STORE || p.copy_mask != 0;
+    GfKernel k = pick_vec((int)p.C, (int)p.R, pre);
     if (!k || p.units == 0 || n_stripes == 0) return hipErrorInvalidValue;
     const uint32_t B = (uint32_t)vec_block();
     p.chunks_per_stripe = (p.units + B - 1) / B;
     const uint64_t blocks = (uint64_t)p.chunks_per_stripe * n_stripes;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    const int occ = vec_occupancy();
+    const int occ = vec_occupancy((int)p.C, (int)p.R, pre);
     const size_t lds = occ ? (size_t)(160 * 1024) / (size_t)(4 * occ * (B / 64)) / 16 * 16 : 0;
     hipLaunchKernelGGL(k, dim3((uint32_t)blocks), dim3(B), lds, stream, p);
     return hipGetLastError();
