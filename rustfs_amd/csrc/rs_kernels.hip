@@ -453,10 +453,10 @@ __device__ __forceinline__ void hhq_finish(HHQuad& s, uint8_t* out, uint32_t q) 
 __device__ __forceinline__ void st64_any(uint8_t* p, uint64_t v) { __builtin_memcpy(p, &v, 8); }
 
 // Plain / per-shard batch hash: quad j hashes message j (16 messages per wave).
-// Every lane issues its own 8-byte loads.  DEEP = 0: one batch of 8 packets
-// fetched ahead; DEEP = 1: two batches (16 packets, 128 B per lane) in flight,
-// double-buffered: the next batch's loads are issued before the current batch
-// is hashed.  A launch of few messages (the GET engine's 8 data records per
+// Every lane issues its own 8-byte loads.  DEPTH = 1: one batch of 8 packets
+// fetched, then hashed; DEPTH = 2 (default): two batches (16 packets, 128 B per
+// lane) in flight, the next batch's loads issued before the current batch is
+// hashed; DEPTH = 3: three.  A launch of few messages (the GET engine's 8 data records per
 // stripe: 2 waves per SIMD at 4096 stripes) needs the deeper pipeline to keep
 // enough bytes in flight per CU.  COPY: also store the message bytes to
 // copy_base[b] + r*copy_stride (multi-file).
@@ -467,7 +467,7 @@ __device__ __forceinline__ void st64_any(uint8_t* p, uint64_t v) { __builtin_mem
 // per instruction) instead of 16 scattered 32-byte pieces of 8 B per lane.
 // The whole wave stays in the loop (a quad past n hashes message 0 and stores
 // nothing) because its lanes store other quads' bytes.
-template <int COPY, int DEEP>
+template <int COPY, int DEPTH>
 __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
     const uint64_t j0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 2;
     const uint32_t q = threadIdx.x & 3u;
@@ -536,20 +536,26 @@ __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
         }
     };
     const uint64_t nb = packets / 8;  // whole 8-packet batches
-    if constexpr (DEEP) {
+    if constexpr (DEPTH >= 2) {
+        // DEPTH register batches: batch x lives in w[x % DEPTH]; the loads of
+        // batch x + DEPTH - 1 are issued before batch x is hashed.  Loads past
+        // the last batch are clamped to it (inside the message) and unused.
         if (nb) {
-            uint64_t wa[8], wb[8];
-            fetch(wa, 0);
+            uint64_t w[DEPTH][8];
+#pragma unroll
+            for (int d = 0; d < DEPTH - 1; ++d) fetch(w[d], ((uint64_t)d < nb ? (uint64_t)d : nb - 1) * 8);
             uint64_t b = 0;
-            for (; b + 2 <= nb; b += 2) {
-                fetch(wb, (b + 1) * 8);
-                consume(wa, b * 8);
-                // clamped, so the loads stay unconditional: past the last
-                // batch this re-reads it (inside the message) and is unused
-                fetch(wa, (b + 2 < nb ? b + 2 : nb - 1) * 8);
-                consume(wb, (b + 1) * 8);
+            for (; b + DEPTH <= nb; b += DEPTH) {
+#pragma unroll
+                for (int d = 0; d < DEPTH; ++d) {
+                    const uint64_t nxt = b + d + DEPTH - 1;
+                    fetch(w[(d + DEPTH - 1) % DEPTH], (nxt < nb ? nxt : nb - 1) * 8);
+                    consume(w[d], (b + d) * 8);
+                }
             }
-            if (b < nb) consume(wa, b * 8);  // odd batch count: wa holds batch nb-1
+#pragma unroll
+            for (int d = 0; d < DEPTH - 1; ++d)  // fewer than DEPTH batches left, all fetched
+                if (b + d < nb) consume(w[d], (b + d) * 8);
             t = nb * 8;
         }
     } else {
@@ -1061,17 +1067,18 @@ hipError_t launch_hh256(const HashParams& p, hipStream_t stream) {
         const char* e = getenv("RSG_HASH_COPY");
         return e && e[0] == '1';
     }();
-    // Two batches in flight per lane (DEEP) unless the launch alone fills the
-    // GPU with waves; RSG_HASH_DEEP=0/1 forces one for A/B runs.
-    static const int force = [] {
-        const char* e = getenv("RSG_HASH_DEEP");
-        return !e ? -1 : (e[0] == '1' ? 1 : 0);
+    // Batches of 8 packets in flight per lane: 2 by default; RSG_HASH_DEPTH
+    // = 1, 2 or 3 forces one for A/B runs.
+    static const int depth = [] {
+        const char* e = getenv("RSG_HASH_DEPTH");
+        const int v = e ? atoi(e) : 2;
+        return v >= 1 && v <= 3 ? v : 2;
     }();
-    const bool deep = force >= 0 ? force == 1 : true;
     using HashKernel = void (*)(const HashParams);
-    const HashKernel k = copy ? (direct_copy ? (deep ? k_hh256_quad<1, 1> : k_hh256_quad<1, 0>)
-                                             : (deep ? k_hh256_quad<2, 1> : k_hh256_quad<2, 0>))
-                              : (deep ? k_hh256_quad<0, 1> : k_hh256_quad<0, 0>);
+    HashKernel k;
+    if (!copy) k = depth == 1 ? k_hh256_quad<0, 1> : depth == 2 ? k_hh256_quad<0, 2> : k_hh256_quad<0, 3>;
+    else if (direct_copy) k = depth == 1 ? k_hh256_quad<1, 1> : depth == 2 ? k_hh256_quad<1, 2> : k_hh256_quad<1, 3>;
+    else k = depth == 1 ? k_hh256_quad<2, 1> : depth == 2 ? k_hh256_quad<2, 2> : k_hh256_quad<2, 3>;
     hipLaunchKernelGGL(k, dim3((uint32_t)blocks), dim3(256), 0, stream, p);
     return hipGetLastError();
 }

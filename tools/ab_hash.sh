@@ -1,12 +1,16 @@
 #!/bin/bash
-# A/B of the hash kernel's prefetch depth (RSG_HASH_DEEP) on the engines that
-# are hash-bound (GET verify+gather, bitrot_verify, heal), after the GPU tests.
+# A/B of the hash kernel's prefetch depth (RSG_HASH_DEPTH = batches of 8
+# packets in flight per lane) on the record engines (bench.py extras:
+# GET, heal, bitrot_verify) and the fused-digest fallback paths.
 set -o pipefail
-TAG=${1:-abhash}
-OUT=gpurun_out/$TAG
+OUT=gpurun_out/ab_hash
 mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 \
- && RSG_HASH_DEEP=0 timeout -k 10 300 python tools/engine_bench.py > $OUT/engine_d0.json 2> $OUT/err0.log \
- && RSG_HASH_DEEP=1 timeout -k 10 300 python tools/engine_bench.py > $OUT/engine_d1.json 2> $OUT/err1.log \
- && RSG_HASH_DEEP=0 timeout -k 10 300 python tools/engine_bench.py > $OUT/engine_d0b.json 2>> $OUT/err0.log \
- && RSG_HASH_DEEP=1 timeout -k 10 300 python tools/engine_bench.py > $OUT/engine_d1b.json 2>> $OUT/err1.log
+for d in 2 3 1 2 3; do
+  RSG_HASH_DEPTH=$d timeout -k 10 120 python bench.py --steps 5 --no-cpu-baseline > $OUT/d$d.json 2>>$OUT/err.log || exit $?
+  python - $d <<'PY'
+import json, sys
+d = sys.argv[1]
+x = json.loads(open(f"gpurun_out/ab_hash/d{d}.json").read().strip().splitlines()[-1])["extras"]["engines"]
+print("depth", d, {k: v["call_ms"] for k, v in x.items()})
+PY
+done
