@@ -1,8 +1,9 @@
 // gf_bitslice.h — bit-sliced GF(2^8) matrix apply for compile-time matrices
-// (the encode matrix of a fixed (k, m) geometry).  Measurement code, not part
-// of the product: tools/kbench/bs_variants.hip (encode) and fused_bs.hip
-// (fused encode + hash) compare it with the production table kernels;
-// DESIGN.md "Measured and not shipped" has the numbers.
+// (the encode matrix of a fixed (k, m) geometry).  Used by the LDS-DMA fused
+// encode + HighwayHash kernel (rs_kernels.hip k_encode_hash_dma, RS(8,4)),
+// whose launcher checks at run time that the codec's encode rows equal
+// EncodeRows<K, M> before selecting it; tools/kbench/ (bs_variants.hip,
+// fused_bs.hip, fused_r2.hip) compare it with the table kernels.
 //
 // Multiplication by a constant c is GF(2)-linear on the 8 bits of a byte: an
 // 8x8 bit matrix B_c with column j = c * 2^j.  If 32 bytes are held as 8 bit

@@ -19,10 +19,13 @@
 // SGPRs — wave-uniform, no per-byte LDS log/antilog lookups (those cannot meet
 // the HBM op budget).
 #include <hip/hip_runtime.h>
+
+#include <array>
 #include <stdint.h>
 #include <stdlib.h>
 
 #include "rs_kernels.h"
+#include "gf_bitslice.h"
 
 namespace rsg {
 
@@ -768,6 +771,271 @@ void k_encode_hash_fused(const GfApplyParams p,
 }
 
 // ---------------------------------------------------------------------------
+// Fused RS encode + HighwayHash-256 with LDS-DMA data and bit-sliced
+// encoders, for a compile-time encode matrix (RS(8,4)).  Same output as
+// k_encode_hash_fused; 1.48-1.50 ms against 1.55-1.62 ms for RS(8,4),
+// n = 4096, 1 MiB stripes (tools/kbench/fused_r2.hip "v8 bar D3").
+//
+// One workgroup of 10 waves owns 8 stripes and walks them in 512-byte steps:
+//   data-hasher waves (K/2): each brings 8 of the step's K x 4 data-row DMA
+//     instructions (global_load_lds, 16 B per lane; an instruction carries one
+//     shard of stripes i and i + 4) into a 3-slot LDS ring two steps ahead,
+//     then hashes 16 data streams of the current step straight out of the ring;
+//   encoder waves (4): stripe group g = stripes {2g, 2g+1, 2g+4, 2g+5}, 8 B
+//     per lane of each, read from the ring, bit-transposed into planes, every
+//     parity row one compile-time XOR network (v_bitop3) over the planes,
+//     transposed back, stored to HBM and to a double-buffered parity-row area;
+//   parity-hasher waves (M/2): the parity streams one step behind.
+// One barrier per step.  The DMA writes LDS behind the compiler's back, so
+// its completion is awaited with counted vmcnt waits and the data rows are
+// read with asm ds_read_b64 (the compiler adds no vmcnt(0) for them).  Dead
+// stripes (past n) re-read stripe 0 and store stripe 0's own bytes.
+namespace dma {
+constexpr uint32_t CH = 512;          // bytes per shard per step
+constexpr uint32_t IP = 2 * CH + 32;  // LDS pitch of one DMA instruction (rows of stripes i and i+4)
+constexpr uint32_t PP = CH + 32;      // parity row pitch
+constexpr int SPW = 8, HS = 4, D = 3, NP = 2, EW = 4;
+
+// s_waitcnt vmcnt(n) only (gfx9 encoding; n <= 63)
+constexpr uint32_t vmcnt_imm(int n) {
+    return 0x0F70u | ((uint32_t)(n > 63 ? 63 : n) & 15u) | (((uint32_t)(n > 63 ? 63 : n) >> 4) & 3u) << 14;
+}
+
+// 16 packets of one stream (8 B per lane, 32 B apart) from LDS, one asm.
+__device__ __forceinline__ void read16(uint32_t a, uint64_t (&w)[16]) {
+    asm volatile(
+        "ds_read_b64 %0, %16 offset:0\n\t"
+        "ds_read_b64 %1, %16 offset:32\n\t"
+        "ds_read_b64 %2, %16 offset:64\n\t"
+        "ds_read_b64 %3, %16 offset:96\n\t"
+        "ds_read_b64 %4, %16 offset:128\n\t"
+        "ds_read_b64 %5, %16 offset:160\n\t"
+        "ds_read_b64 %6, %16 offset:192\n\t"
+        "ds_read_b64 %7, %16 offset:224\n\t"
+        "ds_read_b64 %8, %16 offset:256\n\t"
+        "ds_read_b64 %9, %16 offset:288\n\t"
+        "ds_read_b64 %10, %16 offset:320\n\t"
+        "ds_read_b64 %11, %16 offset:352\n\t"
+        "ds_read_b64 %12, %16 offset:384\n\t"
+        "ds_read_b64 %13, %16 offset:416\n\t"
+        "ds_read_b64 %14, %16 offset:448\n\t"
+        "ds_read_b64 %15, %16 offset:480\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(w[4]), "=&v"(w[5]), "=&v"(w[6]), "=&v"(w[7]),
+          "=&v"(w[8]), "=&v"(w[9]), "=&v"(w[10]), "=&v"(w[11]), "=&v"(w[12]), "=&v"(w[13]), "=&v"(w[14]),
+          "=&v"(w[15])
+        : "v"(a)
+        : "memory");
+}
+
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+}
+
+// 8x8 bit transpose of 8 dwords (bs::transpose) with two shifts and two
+// v_bfi_b32 per masked swap; its own inverse
+__device__ __forceinline__ void swap_bfi(uint32_t& lo, uint32_t& hi, int s, uint32_t mask) {
+    const uint32_t a = lo, b = hi;
+    lo = bfi(mask, a, b << s);
+    hi = bfi(mask, a >> s, b);
+}
+__device__ __forceinline__ void transpose(uint32_t (&w)[8], uint32_t m4, uint32_t m2, uint32_t m1) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) swap_bfi(w[d], w[d + 4], 4, m4);
+    swap_bfi(w[0], w[2], 2, m2);
+    swap_bfi(w[1], w[3], 2, m2);
+    swap_bfi(w[4], w[6], 2, m2);
+    swap_bfi(w[5], w[7], 2, m2);
+#pragma unroll
+    for (int d = 0; d < 8; d += 2) swap_bfi(w[d], w[d + 1], 1, m1);
+}
+
+// acc[r][i] (^)= XOR of the planes P[c][j] with bit j of mask[R0+r][C0+c][i]
+// (rows [R0, R0+RN), shards [C0, C0+NC)), folded two terms at a time by
+// the three-input XOR.
+template <int K, int M, int R0, int RN, int C0, int NC, bool FIRST>
+__device__ __forceinline__ void fold(uint32_t (&acc)[RN][8], const uint32_t (&P)[NC][8]) {
+    constexpr bs::PlaneMasks<K, M> PM{};
+#pragma unroll
+    for (int r = 0; r < RN; ++r) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            uint32_t t[1 + 8 * NC];
+            int n = 0;
+            if (!FIRST) t[n++] = acc[r][i];
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if ((PM.mask[R0 + r][C0 + c][i] >> j) & 1u) t[n++] = P[c][j];
+            uint32_t v = n ? t[0] : 0u;
+            int k = 1;
+            for (; k + 1 < n; k += 2) v = x3(v, t[k], t[k + 1]);
+            if (k < n) v ^= t[k];
+            acc[r][i] = v;
+        }
+    }
+}
+
+template <int K, int M>
+struct Shape {
+    static constexpr int NI = HS * K;                 // DMA instructions per step (1 KiB each)
+    static constexpr uint32_t DSLOT = NI * IP;        // one step of all data rows
+    static constexpr uint32_t PSLOT = SPW * M * PP;   // one step of all parity rows
+    static constexpr int DATA = (SPW * K) / 16;       // data-hasher waves
+    static constexpr int PAR = (SPW * M + 15) / 16;   // parity-hasher waves
+    static constexpr int WAVES = EW + DATA + PAR;
+};
+
+// Encoder wave: stripe group g, parity rows [R0, R0 + M/2) (two waves per group)
+template <int K, int M, int H>
+__device__ __forceinline__ void encoder(const GfApplyParams& p, uint64_t n, uint32_t steps, uint64_t s0, uint32_t g,
+                                        const uint8_t* ring, uint8_t* prow) {
+    using L = Shape<K, M>;
+    constexpr int RPW = M / 2;
+    constexpr int R0 = H * RPW;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t m4 = vgpr_const(0x0f0f0f0fu), m2 = vgpr_const(0x33333333u), m1 = vgpr_const(0x55555555u);
+    const uint32_t mys[4] = {2 * g, 2 * g + 1, 2 * g + HS, 2 * g + HS + 1};
+    uint8_t* const base = p.out_base;
+    uint64_t pdst[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pdst[j] = (s0 + mys[j] < n ? s0 + mys[j] : 0) * p.stripe_stride + lane * 8u;
+    lds_barrier();  // B(0): slot 0 landed
+#pragma unroll 1
+    for (uint32_t s = 0; s < steps; ++s) {
+        const uint8_t* slot = ring + (s % D) * L::DSLOT + 2 * g * IP + lane * 8u;
+        uint32_t acc[RPW][8];
+#pragma unroll
+        for (int c = 0; c < K; c += 2) {
+            uint32_t P[2][8];
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) {
+                const uint8_t* row = slot + HS * (c + cc) * IP;
+                const uint2 a0 = *(const uint2*)row, a1 = *(const uint2*)(row + IP);
+                const uint2 a2 = *(const uint2*)(row + CH), a3 = *(const uint2*)(row + IP + CH);
+                P[cc][0] = a0.x; P[cc][1] = a0.y; P[cc][2] = a1.x; P[cc][3] = a1.y;
+                P[cc][4] = a2.x; P[cc][5] = a2.y; P[cc][6] = a3.x; P[cc][7] = a3.y;
+                transpose(P[cc], m4, m2, m1);
+            }
+            if (c == 0) fold<K, M, R0, RPW, 0, 2, true>(acc, P);
+            else if (c == 2) fold<K, M, R0, RPW, (K > 2 ? 2 : 0), 2, false>(acc, P);
+            else if (c == 4) fold<K, M, R0, RPW, (K > 4 ? 4 : 0), 2, false>(acc, P);
+            else fold<K, M, R0, RPW, (K > 6 ? 6 : 0), 2, false>(acc, P);
+        }
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            transpose(acc[r], m4, m2, m1);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint2 v = make_uint2(acc[r][2 * j], acc[r][2 * j + 1]);
+                // a dead stripe's lanes computed stripe 0's parity from stripe
+                // 0's data and store exactly the bytes stripe 0's lanes store
+                *(uint2*)(base + pdst[j] + p.out_off[R0 + r] + (uint64_t)s * CH) = v;
+                *(uint2*)(prow + (s % NP) * L::PSLOT + ((R0 + r) * SPW + mys[j]) * PP + lane * 8u) = v;
+            }
+        }
+        lds_barrier();  // B(s+1): parity rows of step s published
+    }
+}
+}  // namespace dma
+
+template <int K, int M>
+__global__ __launch_bounds__((64 * dma::Shape<K, M>::WAVES)) void k_encode_hash_dma(const GfApplyParams p,
+                                                                                  const HashParams h) {
+    using namespace dma;
+    static_assert(K % 2 == 0 && M % 2 == 0 && K <= 8 && M <= 4 && M >= 2, "pairs of shards per wave");
+    using L = Shape<K, M>;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[D * L::DSLOT];
+    __shared__ __attribute__((aligned(16))) uint8_t prow[NP * L::PSLOT];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u, q = lane & 3u;
+    const uint64_t n = h.n;
+    const uint32_t steps = p.units;  // S / CH
+    const uint64_t s0 = (uint64_t)blockIdx.x * SPW;
+    const uint32_t ring_base = (uint32_t)(uintptr_t)ring;
+
+    if (wave < (uint32_t)EW) {
+        const uint32_t g = wave % 2;
+        if (wave < 2) encoder<K, M, 0>(p, n, steps, s0, g, ring, prow);
+        else encoder<K, M, 1>(p, n, steps, s0, g, ring, prow);
+        return;
+    }
+    // ---------------------------------- hashers ----------------------------------
+    const uint32_t hw = wave - EW, j = lane >> 2;
+    const bool is_data = hw < (uint32_t)L::DATA;
+    constexpr int NDI = 8;  // DMA instructions a data-hasher wave owns
+    uint32_t stripe_l, shard, roff;
+    if (is_data) {
+        // data hasher hw owns DMA instructions [8 hw, 8 hw + 8): it brings them
+        // into the ring D-1 steps ahead and hashes both halves of each: quad j
+        // takes instruction 8 hw + (j & 7), half j >> 3 (conflict-free
+        // ds_read_b64: the 8 quads of a 32-lane group read rows 32 B apart mod 256)
+        const uint32_t idx = NDI * hw + (j & 7u), half = j >> 3;
+        shard = idx / HS;
+        stripe_l = idx % HS + HS * half;
+        roff = idx * IP + half * CH + 8 * q;
+    } else {
+        uint32_t pi = 16 * (hw - L::DATA) + j;  // parity row index r * SPW + stripe
+        if (pi >= (uint32_t)(SPW * M)) pi = 0;  // idle quad
+        shard = K + pi / SPW;
+        stripe_l = pi % SPW;
+        roff = pi * PP + 8 * q;
+    }
+    const bool live = s0 + stripe_l < n && (is_data || 16 * (hw - L::DATA) + j < (uint32_t)(SPW * M));
+    HHQuad st;
+    hhq_init(st, h.key, q);
+    auto hash16 = [&](uint32_t a) {
+        uint64_t w[16];
+        read16(a, w);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) hhq_update(st, w[t]);
+    };
+    if (is_data) {
+        // DMA instruction 8 hw + k: shard c = (8 hw + k) / 4, stripe pair
+        // i = k % 4: lanes 0-31 stripe i, lanes 32-63 stripe i + 4
+        uint64_t dsrc[HS];
+#pragma unroll
+        for (int i = 0; i < HS; ++i) {
+            const uint64_t sg = s0 + i + (lane >> 5) * HS;
+            dsrc[i] = (sg < n ? sg : 0) * p.stripe_stride + (lane & 31u) * 16u;
+        }
+        const uint8_t* base = p.out_base;
+        auto dma = [&](uint32_t step) {
+#pragma unroll
+            for (int k = 0; k < NDI; ++k) {
+                const uint32_t c = (NDI * hw + k) / HS;  // wave-uniform
+                const uint8_t* src = base + dsrc[k % HS] + p.in_off[c] + (uint64_t)step * CH;
+                __builtin_amdgcn_global_load_lds(
+                    (const void*)src,
+                    (__attribute__((address_space(3))) void*)(ring + (step % D) * L::DSLOT + (NDI * hw + k) * IP),
+                    16, 0, 0);
+            }
+        };
+#pragma unroll
+        for (int d = 0; d < D - 1; ++d) dma(d < (int)steps ? d : steps - 1);
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm((D - 2) * NDI));  // DMA(0) landed
+        lds_barrier();  // B(0)
+#pragma unroll 1
+        for (uint32_t s = 0; s < steps; ++s) {
+            dma(s + D - 1 < steps ? s + D - 1 : steps - 1);  // into the slot step s-1 used
+            hash16(ring_base + (s % D) * L::DSLOT + roff);
+            __builtin_amdgcn_s_waitcnt(vmcnt_imm((D - 2) * NDI));  // DMA(s+1) landed
+            lds_barrier();  // B(s+1)
+        }
+    } else {
+        lds_barrier();  // B(0)
+#pragma unroll 1
+        for (uint32_t s = 0; s <= steps; ++s) {
+            if (s > 0) hash16((uint32_t)(uintptr_t)prow + ((s - 1) % NP) * L::PSLOT + roff);  // published by B(s)
+            if (s < steps) lds_barrier();  // B(s+1)
+        }
+    }
+    if (live) hhq_finish(st, h.out + ((s0 + stripe_l) * (K + M) + shard) * 32u, q);
+}
+
+// ---------------------------------------------------------------------------
 // Fused RS encode + HighwayHash-256, ring variant for batches of few large
 // stripes (config 4's 4-16 MiB stripes at 4 GiB per launch: 256-1024 stripes).
 // There the packed kernel above has too few bytes in flight (one 512-B chunk
@@ -1137,6 +1405,57 @@ bool fused_supported(int C, int R, uint64_t shard_len) {
            shard_len % kFusedChunk == 0 && shard_len / kFusedChunk <= 0xffffffffull;
 }
 
+// The DMA kernel bakes the RS(8,4) encode matrix in at compile time: it is
+// selected only when the launch's coefficient tables are exactly that
+// matrix's (an encode launch, in place, a3-style layout), 16-byte aligned
+// (LDS-DMA moves 16 B per lane) and whole 512-byte steps.
+static bool dma_tables_match(const GfApplyParams& p) {
+    static const auto want = [] {
+        constexpr bs::EncodeRows<8, 4> E{};
+        std::array<uint32_t, 4 * 8 * 5> t{};
+        for (int r = 0; r < 4; ++r)
+            for (int c = 0; c < 8; ++c) {
+                const uint8_t co = E.g[r][c];
+                auto pack = [&](int sh, int f) {
+                    uint32_t v = 0;
+                    for (int i = 0; i < 4; ++i) v |= (uint32_t)bs::gmul(co, (uint8_t)((f + i) << sh)) << (8 * i);
+                    return v;
+                };
+                uint32_t* d = &t[(r * 8 + c) * 5];
+                d[0] = pack(0, 0); d[1] = pack(0, 4); d[2] = pack(3, 0); d[3] = pack(3, 4); d[4] = pack(6, 0);
+            }
+        return t;
+    }();
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 8; ++c)
+            for (int q = 0; q < 5; ++q)
+                if (p.tab[r][c][q] != want[(r * 8 + c) * 5 + q]) return false;
+    return true;
+}
+
+static bool dma_supported(const GfApplyParams& p, uint64_t shard_len, uint64_t n_stripes) {
+    if (p.C != 8 || p.R != 4 || p.mode != GF_MODE_STORE || p.copy_mask || p.base != p.out_base ||
+        p.stripe_stride != p.out_stripe_stride || n_stripes == 0 || n_stripes > 0x7fffffffull * dma::SPW)
+        return false;
+    if (shard_len < dma::CH || shard_len % dma::CH || shard_len / dma::CH > 0xffffffffull) return false;
+    if ((uintptr_t)p.base % 16 || p.stripe_stride % 16) return false;
+    for (int c = 0; c < 8; ++c)
+        if (p.in_off[c] % 16) return false;
+    for (int r = 0; r < 4; ++r)
+        if (p.out_off[r] % 8) return false;
+    return dma_tables_match(p);
+}
+
+static hipError_t launch_encode_hash_dma(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
+                                         hipStream_t stream) {
+    p.units = (uint32_t)(shard_len / dma::CH);
+    h.n = n_stripes;
+    const uint64_t blocks = (n_stripes + dma::SPW - 1) / dma::SPW;
+    hipLaunchKernelGGL((k_encode_hash_dma<8, 4>), dim3((uint32_t)blocks), dim3(64 * dma::Shape<8, 4>::WAVES), 0,
+                       stream, p, h);
+    return hipGetLastError();
+}
+
 hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                     hipStream_t stream) {
     // Packed workgroups measured as fast or faster than one stripe per
@@ -1152,14 +1471,18 @@ hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shar
     // RSG_FUSED_KIND=packed|ring forces one for A/B runs.
     static const int kind = [] {
         const char* e = getenv("RSG_FUSED_KIND");
-        return !e ? 0 : (e[0] == 'p' ? 1 : e[0] == 'r' ? 2 : 0);
+        return !e ? 0 : (e[0] == 'p' ? 1 : e[0] == 'r' ? 2 : e[0] == 'd' ? 3 : 0);
     }();
-    if (kind != 1 && (kind == 2 || n_stripes < 2048)) {
+    if (kind != 1 && kind != 3 && (kind == 2 || n_stripes < 2048)) {
         uint32_t E = n_stripes <= 768 ? 2u : 1u;
         if (E == 2 && !ring_supported((int)p.C, (int)p.R, shard_len, E)) E = 1;
         if (ring_supported((int)p.C, (int)p.R, shard_len, E))
             return launch_encode_hash_ring(p, h, shard_len, n_stripes, E, stream);
     }
+    // RS(8,4), 2048+ stripes: the LDS-DMA bit-sliced kernel (RSG_FUSED_KIND=
+    // packed keeps the table kernel for A/B runs)
+    if (kind != 1 && (kind == 3 || n_stripes >= 2048) && dma_supported(p, shard_len, n_stripes))
+        return launch_encode_hash_dma(p, h, shard_len, n_stripes, stream);
     const FusedPick f = pick_fused((int)p.C, (int)p.R, !unpacked);
     if (!f.k || !fused_supported((int)p.C, (int)p.R, shard_len) || n_stripes == 0 || n_stripes > 0x7fffffffull)
         return hipErrorInvalidValue;

@@ -4,8 +4,9 @@ Config 2: RS(8,4) encode of 1 MiB stripes at batch 4096 (6 GiB resident).
 Config 3: RS(8,4) reconstruct of that batch with 1-4 missing shards.
 Config 4: RS(8,4) encode + fused HighwayHash256S over the 64 KiB-16 MiB stripe
 sweep at SURVEY §8(d)'s sizing (n = 4 GiB / stripe), which walks every fused
-kernel the launcher picks: packed (n >= 2048), ring E = 1 (768 < n < 2048) and
-ring E = 2 with up to 1024 chunks per shard (S = 2 MiB).
+kernel the launcher picks for RS(8,4): the LDS-DMA kernel (n >= 2048), ring
+E = 1 (768 < n < 2048) and ring E = 2 with up to 1024 chunks per shard
+(S = 2 MiB).
 
 The whole batch stays on the device; a sample of stripes (always the first and
 the last) is copied back and checked byte for byte — parity and all k+m
@@ -74,6 +75,31 @@ def test_config4_fused_sweep_at_survey_sizing(gpu, oracle, stripe_bytes):
     assert torch.equal(d2.reshape(n, k + m, 32), dig)
     del st, dig, flat, d2
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("n,S", [(2049, 512), (2055, 4096), (4093, 4096), (2049, 131072)])
+def test_fused_dma_kernel_ragged_batches(gpu, oracle, n, S):
+    """RS(8,4) with >= 2048 stripes takes the LDS-DMA bit-sliced fused kernel
+    (8 stripes per workgroup): batches that are not a multiple of 8 leave
+    dead stripes in the last workgroup, which must neither store nor hash
+    anything; one 512-byte step (S = 512) is the shortest walk."""
+    import torch
+    from rustfs_amd import Erasure, _lib
+    k, m = 8, 4
+    st = _fill(torch, n, k, m, S, seed=n + S)
+    dig = torch.zeros((n + 1, k + m, 32), dtype=torch.uint8, device="cuda")  # one guard stripe of digests
+    e = Erasure(k, m, k * S)
+    e.encode_batch(st, dig[:n])
+    torch.cuda.synchronize()
+    _check_stripes(oracle, st, dig, k, m, sorted({0, 1, 7, 8, n - 9, n - 8, n - 2, n - 1}))
+    assert bool(e.verify_batch(st).all())
+    flat = st.reshape(n * (k + m), S)
+    d2 = torch.zeros((n * (k + m), 32), dtype=torch.uint8, device="cuda")
+    _lib.check(_lib.load().rsg_hash_batch_dev(_lib.context(0).handle, _lib.RSG_HASH_HIGHWAY256S, flat.data_ptr(), S, S,
+                                              n * (k + m), d2.data_ptr(), torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    assert torch.equal(d2.reshape(n, k + m, 32), dig[:n])
+    assert not bool(dig[n].any())  # nothing written past the batch
 
 
 def test_config2_full_batch(gpu, oracle):

@@ -2,7 +2,7 @@
 // workgroup sizes 64 / 128 / 256 threads, same block -> (stripe, column)
 // order.  Measurement code.  Usage: block_probe [n] [k] [m]
 #include "../../rustfs_amd/csrc/rs_kernels.hip"
-#include "gf_bitslice.h"
+#include "../../rustfs_amd/csrc/gf_bitslice.h"
 
 #include <stdio.h>
 #include <stdlib.h>

@@ -3,7 +3,7 @@
 // byte for byte.  Not part of the product.
 // Usage: bs_variants n [iters]
 #include "../../rustfs_amd/csrc/rs_kernels.hip"
-#include "gf_bitslice.h"
+#include "../../rustfs_amd/csrc/gf_bitslice.h"
 
 #include <stdio.h>
 #include <stdlib.h>

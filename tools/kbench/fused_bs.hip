@@ -3,7 +3,7 @@
 // byte, interleaved timing in one process).  Not part of the product.
 // Usage: fused_bs n [iters]
 #include "../../rustfs_amd/csrc/rs_kernels.hip"
-#include "gf_bitslice.h"
+#include "../../rustfs_amd/csrc/gf_bitslice.h"
 
 #include <stdio.h>
 #include <stdlib.h>

@@ -4,7 +4,7 @@
 // workgroups share a CU and a 4096-stripe batch runs in two even rounds.
 // Not part of the product.  Usage: fused_deep n [iters]
 #include "../../rustfs_amd/csrc/rs_kernels.hip"
-#include "gf_bitslice.h"
+#include "../../rustfs_amd/csrc/gf_bitslice.h"
 
 #include <stdio.h>
 #include <stdlib.h>

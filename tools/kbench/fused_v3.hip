@@ -3,7 +3,7 @@
 // deep, parity rows double-buffered in LDS, data-shard hashers reading global
 // memory two chunks ahead.  Not part of the product.  Usage: fused_v3 n [iters]
 #include "../../rustfs_amd/csrc/rs_kernels.hip"
-#include "gf_bitslice.h"
+#include "../../rustfs_amd/csrc/gf_bitslice.h"
 
 #include <stdio.h>
 #include <stdlib.h>

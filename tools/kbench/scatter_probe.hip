@@ -6,7 +6,7 @@
 // every stripe advanced 1 KiB at a time, like a kernel that walks all stripes
 // in lockstep).  Measurement code.  Usage: scatter_probe [n]
 #include "../../rustfs_amd/csrc/rs_kernels.hip"
-#include "gf_bitslice.h"
+#include "../../rustfs_amd/csrc/gf_bitslice.h"
 
 #include <stdio.h>
 #include <stdlib.h>

@@ -6,7 +6,7 @@
 // offsets.  Also the production sweep-order encode kernel on the same
 // layouts.  Measurement code.  Usage: skew_probe [n]
 #include "../../rustfs_amd/csrc/rs_kernels.hip"
-#include "gf_bitslice.h"
+#include "../../rustfs_amd/csrc/gf_bitslice.h"
 
 #include <stdio.h>
 #include <stdlib.h>
