@@ -83,6 +83,11 @@ hipError_t launch_hh256(const HashParams& p, hipStream_t stream);
 // digest output [n][C+R][32].  Requires shard_len % 512 == 0, C <= 16, R <= 4
 // and 16-B aligned shards.
 bool fused_supported(int C, int R, uint64_t shard_len);
+// One-pass degraded GET for RS(8,4) over nf (8..12) present record files
+// (k_decode_records_dma): false if the shape is not supported.
+bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len);
+hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int nf, uint64_t shard_len, uint64_t n_stripes,
+                                     hipStream_t stream);
 hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                     hipStream_t stream);
 

@@ -96,6 +96,11 @@ __device__ __forceinline__ void st16(uint8_t* p, const uint4& v) { __builtin_mem
 // Non-temporal 16-byte store at any alignment (unaligned-access mode): for
 // output that this pass never reads back (GET's gathered data).
 typedef uint32_t v4u_any __attribute__((ext_vector_type(4), aligned(1)));
+__device__ __forceinline__ void st16_nt_half(uint8_t* p, const uint2& v) {  // 8 bytes, non-temporal
+    typedef uint32_t v2u_any __attribute__((ext_vector_type(2), aligned(1)));
+    const v2u_any w = {v.x, v.y};
+    __builtin_nontemporal_store(w, (v2u_any*)p);
+}
 __device__ __forceinline__ void st16_nt(uint8_t* p, const uint4& v) {
     const v4u_any w = {v.x, v.y, v.z, v.w};
     __builtin_nontemporal_store(w, (v4u_any*)p);
@@ -1036,6 +1041,170 @@ __global__ __launch_bounds__((64 * dma::Shape<K, M>::WAVES)) void k_encode_hash_
 }
 
 // ---------------------------------------------------------------------------
+// One-pass degraded GET for RS(8,4) (rsg_decode_records_dev, a data disk
+// lost): every present record of 8 stripes is verified, the missing data
+// shards rebuilt from the first 8 present (survivors), the present data
+// shards copied through and the surplus parity compared with its re-derived
+// value — reading each present record once.  The k_encode_hash_dma layout:
+// NF present files, 4 x NF LDS-DMA instructions per 512-byte step (one shard
+// of stripes i and i+4 each) into a 3-slot ring; ceil(NF/2) DMA/hash waves
+// (8 instructions each, 16 verify streams straight out of the ring) and 8
+// table-GF waves, one per stripe (survivor rows from the ring: rebuilt rows
+// stored to the output, surplus rows compared against their ring rows,
+// survivor data copied to the output).  One barrier per step.  The host
+// redoes the stripes whose verify flags differ from the assumed pattern.
+//   p: tab[r][c] over the 8 survivors (present files 0..7 of the launch),
+//      rows [0, n_store) rebuilt into out_base + s*out_stripe_stride +
+//      out_off[r], rows [n_store, R) compared with present file 8 + (r -
+//      n_store); copy_mask/copy_off: survivors copied to the output;
+//      ok_flags[s] cleared on a compare mismatch; units = S / 512.
+//   h: base[f] = body of record 0 of present file f, stripe_stride = record
+//      pitch, flag_base[f][s] cleared on a digest mismatch, key, n.
+template <int NF>
+struct GetShape {
+    static constexpr int NI = dma::HS * NF;              // DMA instructions per step
+    static constexpr uint32_t DSLOT = NI * dma::IP;
+    static constexpr int HW = (NI + 7) / 8;               // DMA/hash waves
+    static constexpr int LAST = NI - 8 * (HW - 1);        // instructions of the last one
+    static constexpr int WAVES = HW + dma::SPW;
+};
+
+template <int NF>
+__global__ __launch_bounds__((64 * GetShape<NF>::WAVES)) void k_decode_records_dma(const GfApplyParams p,
+                                                                                   const HashParams h) {
+    using namespace dma;
+    using L = GetShape<NF>;
+    constexpr int C = 8, RM = 4;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[D * L::DSLOT];
+    __shared__ __attribute__((aligned(16))) uint8_t tabs[C * RM * 32];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u, q = lane & 3u;
+    const uint64_t n = h.n;
+    const uint32_t steps = p.units;
+    const uint64_t s0 = (uint64_t)blockIdx.x * SPW;
+    const uint32_t ring_base = (uint32_t)(uintptr_t)ring;
+    for (uint32_t i = threadIdx.x; i < (uint32_t)(C * RM); i += blockDim.x) {
+        const int c = i / RM, r = i % RM;
+        *(uint4*)(tabs + i * 32) = make_uint4(p.tab[r][c][0], p.tab[r][c][1], p.tab[r][c][2], p.tab[r][c][3]);
+        *(uint32_t*)(tabs + i * 32 + 16) = p.tab[r][c][4];
+    }
+    // (the tables are published by B(0), which every wave passes before use)
+
+    if (wave >= (uint32_t)L::HW) {
+        // ------------------------- GF wave: one stripe -------------------------
+        const uint32_t e = wave - L::HW;
+        const uint64_t stripe = s0 + e;
+        const bool live = stripe < n;
+        uint8_t* ob = p.out_base + (live ? stripe : 0) * p.out_stripe_stride + lane * 8u;
+        const uint32_t R = p.R, nst = p.n_store, cmask = p.copy_mask;
+        const uint32_t m7 = vgpr_const(0x07070707u), m3 = vgpr_const(0x03030303u);
+        // row of present file f for this stripe: instruction f*HS + e%HS, half e/HS
+        const uint32_t roff = (e % HS) * IP + (e / HS) * CH + lane * 8u;
+        lds_barrier();  // B(0)
+#pragma unroll 1
+        for (uint32_t s = 0; s < steps; ++s) {
+            const uint8_t* slot = ring + (s % D) * L::DSLOT + roff;
+            uint2 x[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) x[c] = *(const uint2*)(slot + c * HS * IP);
+            uint32_t tz;  // opaque zero: table reads stay at their use
+            asm volatile("s_mov_b32 %0, 0" : "=s"(tz));
+            const uint8_t* tb = tabs + tz;
+            uint32_t acc[RM][2], pend[RM][2];
+#pragma unroll
+            for (int r = 0; r < RM; ++r) acc[r][0] = acc[r][1] = pend[r][0] = pend[r][1] = 0u;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const uint32_t s0a = x[c].x & m7, s0b = x[c].y & m7;
+                const uint32_t s1a = (x[c].x >> 3) & m7, s1b = (x[c].y >> 3) & m7;
+                const uint32_t s2a = (x[c].x >> 6) & m3, s2b = (x[c].y >> 6) & m3;
+#pragma unroll
+                for (int r = 0; r < RM; ++r) {
+                    if ((uint32_t)r >= R) break;  // wave-uniform
+                    const uint8_t* tp = tb + (c * RM + r) * 32;
+                    const uint4 t4 = *(const uint4*)tp;
+                    const uint32_t t2 = *(const uint32_t*)(tp + 16);
+                    gf_fold(c & 1, acc[r][0], pend[r][0], __builtin_amdgcn_perm(t4.y, t4.x, s0a),
+                            __builtin_amdgcn_perm(t4.w, t4.z, s1a), __builtin_amdgcn_perm(t2, t2, s2a));
+                    gf_fold(c & 1, acc[r][1], pend[r][1], __builtin_amdgcn_perm(t4.y, t4.x, s0b),
+                            __builtin_amdgcn_perm(t4.w, t4.z, s1b), __builtin_amdgcn_perm(t2, t2, s2b));
+                }
+            }
+            bool bad = false;
+#pragma unroll
+            for (int r = 0; r < RM; ++r) {
+                if ((uint32_t)r >= R) break;
+                const uint2 v = make_uint2(acc[r][0], acc[r][1]);
+                if ((uint32_t)r < nst) {
+                    if (live) st16_nt_half(ob + p.out_off[r] + (uint64_t)s * CH, v);
+                } else {
+                    const uint2 o = *(const uint2*)(slot + (C + (r - nst)) * HS * IP);
+                    bad |= ((o.x ^ v.x) | (o.y ^ v.y)) != 0u;
+                }
+            }
+            if (live) {
+#pragma unroll
+                for (int c = 0; c < C; ++c)
+                    if ((cmask >> c) & 1u) st16_nt_half(ob + p.copy_off[c] + (uint64_t)s * CH, x[c]);
+                if (bad) p.ok_flags[stripe] = 0;
+            }
+            lds_barrier();  // B(s+1): done with slot s % D
+        }
+        return;
+    }
+    // ------------------------- DMA + verify-hash wave -------------------------
+    const uint32_t hw = wave, j = lane >> 2;
+    const int ndi = (hw == (uint32_t)(L::HW - 1)) ? L::LAST : 8;  // instructions this wave owns
+    const uint32_t idx = 8 * hw + (j & 7u), half = j >> 3;
+    const bool quad_on = (int)(j & 7u) < ndi;
+    const uint32_t file = quad_on ? idx / HS : 0, stripe_l = (idx % HS) + HS * half;
+    const uint32_t roff = (quad_on ? idx : 0) * IP + half * CH + 8 * q;
+    const bool live = quad_on && s0 + stripe_l < n;
+    HHQuad st;
+    hhq_init(st, h.key, q);
+    uint64_t dsrc[HS];
+#pragma unroll
+    for (int i = 0; i < HS; ++i) {
+        const uint64_t sg = s0 + i + (lane >> 5) * HS;
+        dsrc[i] = (sg < n ? sg : 0) * h.stripe_stride + (lane & 31u) * 16u;
+    }
+    auto dma_step = [&](uint32_t step) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (k >= ndi) break;  // wave-uniform
+            const uint32_t ins = 8 * hw + k;
+            const uint8_t* src = h.base[ins / HS] + dsrc[k % HS] + (uint64_t)step * CH;
+            __builtin_amdgcn_global_load_lds(
+                (const void*)src, (__attribute__((address_space(3))) void*)(ring + (step % D) * L::DSLOT + ins * IP), 16,
+                0, 0);
+        }
+    };
+    auto wait_next = [&]() {  // DMA of the next step landed (D - 2 steps younger in flight)
+        if (ndi == 8) __builtin_amdgcn_s_waitcnt(vmcnt_imm((D - 2) * 8));
+        else __builtin_amdgcn_s_waitcnt(vmcnt_imm((D - 2) * L::LAST));
+    };
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d) dma_step(d < (int)steps ? d : steps - 1);
+    wait_next();  // DMA(0) landed
+    lds_barrier();  // B(0)
+#pragma unroll 1
+    for (uint32_t s = 0; s < steps; ++s) {
+        dma_step(s + D - 1 < steps ? s + D - 1 : steps - 1);  // into the slot step s-1 used
+        uint64_t w[16];
+        read16(ring_base + (s % D) * L::DSLOT + roff, w);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) hhq_update(st, w[t]);
+        wait_next();
+        lds_barrier();  // B(s+1)
+    }
+    __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // the clamped tail DMA has landed before the wave ends
+    if (live) {  // verify before use (split_and_verify, bitrot.rs:227-247)
+        const uint8_t* rec0 = h.base[file] + (s0 + stripe_l) * h.stripe_stride;
+        const uint64_t d = hhq_digest(st, q);
+        if (d != ld64_any(rec0 - 32 + 8 * q)) h.flag_base[file][s0 + stripe_l] = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Fused RS encode + HighwayHash-256, ring variant for batches of few large
 // stripes (config 4's 4-16 MiB stripes at 4 GiB per launch: 256-1024 stripes).
 // There the packed kernel above has too few bytes in flight (one 512-B chunk
@@ -1453,6 +1622,32 @@ static hipError_t launch_encode_hash_dma(GfApplyParams p, HashParams h, uint64_t
     const uint64_t blocks = (n_stripes + dma::SPW - 1) / dma::SPW;
     hipLaunchKernelGGL((k_encode_hash_dma<8, 4>), dim3((uint32_t)blocks), dim3(64 * dma::Shape<8, 4>::WAVES), 0,
                        stream, p, h);
+    return hipGetLastError();
+}
+
+bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len) {
+    return k == 8 && m == 4 && nf >= 8 && nf <= 12 && shard_len >= dma::CH && shard_len % dma::CH == 0 &&
+           shard_len / dma::CH <= 0xffffffffull;
+}
+
+hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int nf, uint64_t shard_len, uint64_t n_stripes,
+                                     hipStream_t stream) {
+    if (!decode_dma_supported(8, 4, nf, shard_len) || n_stripes == 0 || p.R > 4 || p.n_store > p.R)
+        return hipErrorInvalidValue;
+    for (int f = 0; f < nf; ++f)
+        if ((uintptr_t)h.base[f] % 16) return hipErrorInvalidValue;
+    if (h.stripe_stride % 16) return hipErrorInvalidValue;
+    p.units = (uint32_t)(shard_len / dma::CH);
+    h.n = n_stripes;
+    const uint64_t blocks = (n_stripes + dma::SPW - 1) / dma::SPW;
+    if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+    switch (nf) {
+        case 8: hipLaunchKernelGGL(k_decode_records_dma<8>, dim3((uint32_t)blocks), dim3(64 * GetShape<8>::WAVES), 0, stream, p, h); break;
+        case 9: hipLaunchKernelGGL(k_decode_records_dma<9>, dim3((uint32_t)blocks), dim3(64 * GetShape<9>::WAVES), 0, stream, p, h); break;
+        case 10: hipLaunchKernelGGL(k_decode_records_dma<10>, dim3((uint32_t)blocks), dim3(64 * GetShape<10>::WAVES), 0, stream, p, h); break;
+        case 11: hipLaunchKernelGGL(k_decode_records_dma<11>, dim3((uint32_t)blocks), dim3(64 * GetShape<11>::WAVES), 0, stream, p, h); break;
+        default: hipLaunchKernelGGL(k_decode_records_dma<12>, dim3((uint32_t)blocks), dim3(64 * GetShape<12>::WAVES), 0, stream, p, h); break;
+    }
     return hipGetLastError();
 }
 

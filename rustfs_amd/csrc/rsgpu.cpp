@@ -1156,6 +1156,78 @@ int verify_gather(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64_t n, co
     return flags_to_host(ctx, d_flags + (size_t)k * n, (size_t)m * n, flags.data() + (size_t)k * n, s);
 }
 
+// RSG_GET_DMA=0 keeps the two-pass lost-disk GET (A/B runs).
+bool get_dma_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("RSG_GET_DMA");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// Launch k_decode_records_dma over all stripes for the erasure pattern
+// `present`: present files in ascending order, the first k are the
+// survivors (DecodePlan order); rows = the missing data shards, then (with
+// verify_surplus) the present non-survivor parity, compared in place.
+int launch_get_one_pass(Codec& cd, const std::vector<uint8_t>& present, const std::vector<int>& files,
+                        const uint8_t* const* d_files, uint8_t* d_flags, uint8_t* d_ok, int k, uint64_t shard_len,
+                        uint64_t n, const uint64_t* key, bool verify_surplus, uint8_t* d_out, bool& any_verify,
+                        hipStream_t s) {
+    const int t = (int)present.size();
+    auto plan = cd.plan(present.data());
+    if (!plan) return RSG_ERR_TOO_FEW_SHARDS;
+    for (int c = 0; c < k; ++c)
+        if (plan->survivors[c] != files[c]) return RSG_ERR_INVALID_ARG;  // survivors = first k present
+    std::vector<uint8_t> coef;
+    rsg::GfApplyParams p;
+    std::memset(&p, 0, sizeof(p));
+    int R = 0;
+    for (int i = 0; i < k; ++i) {
+        if (present[i]) continue;
+        coef.resize((size_t)(R + 1) * k);
+        plan_row(cd, *plan, i, &coef[(size_t)R * k]);
+        p.out_off[R++] = (uint64_t)i * shard_len;
+    }
+    const int n_store = R;
+    if (verify_surplus) {
+        for (int f = k; f < (int)files.size(); ++f) {  // present non-survivors: parity, ascending
+            if (R >= rsg::kMaxR) return RSG_ERR_UNSUPPORTED;
+            coef.resize((size_t)(R + 1) * k);
+            plan_row(cd, *plan, files[f], &coef[(size_t)R * k]);
+            ++R;
+        }
+    }
+    if (R > 4 || R == 0) return RSG_ERR_UNSUPPORTED;
+    if (R > n_store) any_verify = true;
+    for (int r = 0; r < R; ++r)
+        for (int c = 0; c < k; ++c) coef_tables(coef[(size_t)r * k + c], p.tab[r][c]);
+    p.C = (uint32_t)k;
+    p.R = (uint32_t)R;
+    p.n_store = (uint32_t)n_store;
+    p.mode = rsg::GF_MODE_STORE_COMPARE;
+    p.out_base = d_out;
+    p.out_stripe_stride = (uint64_t)k * shard_len;
+    p.ok_flags = d_ok;
+    for (int c = 0; c < k; ++c)
+        if (files[c] < k) {
+            p.copy_mask |= 1u << c;
+            p.copy_off[c] = (uint64_t)files[c] * shard_len;
+        }
+    rsg::HashParams h;
+    std::memset(&h, 0, sizeof(h));
+    h.len = shard_len;
+    h.stripe_stride = 32 + shard_len;
+    std::memcpy(h.key, key, sizeof(h.key));
+    h.nbases = (uint32_t)files.size();
+    h.digest_off = -32;
+    for (size_t f = 0; f < files.size(); ++f) {
+        h.base[f] = d_files[files[f]] + 32;
+        h.flag_base[f] = d_flags + (size_t)files[f] * n;
+    }
+    (void)t;
+    return hip_status(rsg::launch_decode_records_dma(p, h, (int)files.size(), shard_len, n, s));
+}
+
 // GET engine body (ctx->mu held): verify records, copy/rebuild the k data
 // shards of every stripe into d_out (n x k*S), optional surplus-parity check.
 // Uses ctx->d_scratch[0, (t+1)*n).  `flags` returns the verified-shard map.
@@ -1264,13 +1336,33 @@ int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64
         // verified (read-only).  Stripes where a record fails are redone from
         // their actual valid shards.  Survivors are read twice (rebuild, then
         // verify) instead of three times by the general path.
-        if ((st = rebuild_run(0, n, present0, true))) return st;
         uint8_t* d_flags = ctx->d_scratch;
-        if ((st = hip_status(hipMemsetAsync(d_flags, 0, (size_t)t * n, s)))) return st;
         std::vector<int> all_idx;
         for (int i = 0; i < t; ++i)
             if (d_files[i]) all_idx.push_back(i);
-        if ((st = launch_verify_group(all_idx, d_files, d_flags, k, shard_len, n, 0, n, key, nullptr, s))) return st;
+        bool one_pass = get_dma_enabled() && rsg::decode_dma_supported(k, m, nfiles, shard_len) &&
+                        rec % 16 == 0;
+        for (int i : all_idx) one_pass = one_pass && (uintptr_t)(d_files[i] + 32) % 16 == 0;
+        if (one_pass) {
+            // RS(8,4): verify every present record, rebuild, gather and check
+            // the surplus parity in ONE pass (k_decode_records_dma)
+            if ((st = hip_status(hipMemsetAsync(d_flags, 0, (size_t)t * n, s)))) return st;
+            for (size_t a = 0; a < all_idx.size();) {
+                size_t b = a + 1;
+                while (b < all_idx.size() && all_idx[b] == all_idx[b - 1] + 1) ++b;
+                if ((st = hip_status(hipMemsetAsync(d_flags + (size_t)all_idx[a] * n, 1, (b - a) * n, s)))) return st;
+                a = b;
+            }
+            if ((st = launch_get_one_pass(*cd, present0, all_idx, d_files, d_flags, d_ok, k, shard_len, n, key,
+                                          verify_surplus, d_out, any_verify, s)))
+                return st;
+            for (uint64_t x = 0; x < n; ++x) h_status[x] = RSG_OK;
+        } else {
+            if ((st = rebuild_run(0, n, present0, true))) return st;
+            if ((st = hip_status(hipMemsetAsync(d_flags, 0, (size_t)t * n, s)))) return st;
+            if ((st = launch_verify_group(all_idx, d_files, d_flags, k, shard_len, n, 0, n, key, nullptr, s)))
+                return st;
+        }
         // the verified map and the surplus verdict (adjacent in scratch) in one
         // copy and one synchronisation; a second one only if a run is redone
         if ((st = ctx->ensure_host_flags((size_t)(t + 1) * n))) return st;

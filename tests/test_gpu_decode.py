@@ -125,3 +125,29 @@ def test_decode_records_lost_disk_inconsistent_surplus(gpu, oracle):
     assert status == [0, 0, 0, 0, _lib.RSG_ERR_INCONSISTENT_SOURCES]
     want = st[:, :k].reshape(n, k * S)
     assert torch.equal(out[:4], want[:4])
+
+
+def test_decode_records_lost_disk_many_workgroups(gpu, oracle):
+    """RS(8,4) one-pass GET kernel over many 8-stripe workgroups and a ragged
+    last one: rotten records and an inconsistent surplus parity scattered
+    over the batch are each caught for their own stripe only."""
+    import torch
+    from rustfs_amd import _lib
+    k, m, S, n = 8, 4, 4096, 2051
+    e, st, files = _records(torch, k, m, S, n, seed=17)
+    rec = 32 + S
+    want = st[:, :k].reshape(n, k * S)
+    f = [None if i in (0, 5) else files[i].clone() for i in range(k + m)]
+    f[3][2050 * rec + 32 + 9] ^= 0x02       # data record body, last stripe
+    f[k + 1][8 * rec + 1] ^= 0x80           # survivor parity digest, stripe 8
+    body = f[k + 3][1234 * rec + 32: 1235 * rec].cpu().numpy().copy()
+    body[4000] ^= 0x01                      # surplus parity of stripe 1234, re-hashed: inconsistent
+    f[k + 3][1234 * rec + 32: 1235 * rec] = torch.from_numpy(body).cuda()
+    f[k + 3][1234 * rec: 1234 * rec + 32] = torch.from_numpy(
+        np.frombuffer(oracle.hh256s(body), dtype=np.uint8).copy()).cuda()
+    out, status = e.decode_records_batch(f, S, n)
+    bad = [i for i, s in enumerate(status) if s != 0]
+    assert bad == [1234] and status[1234] == _lib.RSG_ERR_INCONSISTENT_SOURCES
+    ok = torch.ones(n, dtype=torch.bool, device="cuda")
+    ok[1234] = False
+    assert torch.equal(out[ok], want[ok])
