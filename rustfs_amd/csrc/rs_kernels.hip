@@ -1060,20 +1060,26 @@ __global__ __launch_bounds__((64 * dma::Shape<K, M>::WAVES)) void k_encode_hash_
 //      ok_flags[s] cleared on a compare mismatch; units = S / 512.
 //   h: base[f] = body of record 0 of present file f, stripe_stride = record
 //      pitch, flag_base[f][s] cleared on a digest mismatch, key, n.
-template <int NF>
+template <int NF, int G>
 struct GetShape {
-    static constexpr int NI = dma::HS * NF;              // DMA instructions per step
+    static constexpr int SPW = G, HS = G / 2;             // stripes per workgroup, per DMA half
+    static constexpr int NI = HS * NF;                    // DMA instructions per step
     static constexpr uint32_t DSLOT = NI * dma::IP;
     static constexpr int HW = (NI + 7) / 8;               // DMA/hash waves
     static constexpr int LAST = NI - 8 * (HW - 1);        // instructions of the last one
-    static constexpr int WAVES = HW + dma::SPW;
+    static constexpr int WAVES = HW + SPW;
 };
 
-template <int NF>
-__global__ __launch_bounds__((64 * GetShape<NF>::WAVES)) void k_decode_records_dma(const GfApplyParams p,
-                                                                                   const HashParams h) {
-    using namespace dma;
-    using L = GetShape<NF>;
+template <int NF, int G>
+__global__ __launch_bounds__((64 * GetShape<NF, G>::WAVES)) void k_decode_records_dma(const GfApplyParams p,
+                                                                                      const HashParams h) {
+    using dma::CH;
+    using dma::D;
+    using dma::IP;
+    using dma::read16;
+    using dma::vmcnt_imm;
+    using L = GetShape<NF, G>;
+    constexpr int SPW = L::SPW, HS = L::HS;
     constexpr int C = 8, RM = 4;
     __shared__ __attribute__((aligned(16))) uint8_t ring[D * L::DSLOT];
     __shared__ __attribute__((aligned(16))) uint8_t tabs[C * RM * 32];
@@ -1625,6 +1631,22 @@ static hipError_t launch_encode_hash_dma(GfApplyParams p, HashParams h, uint64_t
     return hipGetLastError();
 }
 
+// stripes per workgroup of the one-pass GET kernel: 8 (one workgroup of 13
+// waves per CU) or 4 (two of 7); RSG_GET_SPW for A/B runs
+static int get_spw() {
+    static const int v = [] {
+        const char* e = getenv("RSG_GET_SPW");
+        return e && atoi(e) == 4 ? 4 : 8;
+    }();
+    return v;
+}
+
+template <int NF, int G>
+static void launch_get(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
+    hipLaunchKernelGGL((k_decode_records_dma<NF, G>), dim3((uint32_t)blocks), dim3(64 * GetShape<NF, G>::WAVES), 0,
+                       stream, p, h);
+}
+
 bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len) {
     return k == 8 && m == 4 && nf >= 8 && nf <= 12 && shard_len >= dma::CH && shard_len % dma::CH == 0 &&
            shard_len / dma::CH <= 0xffffffffull;
@@ -1641,12 +1663,24 @@ hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int nf, uint
     h.n = n_stripes;
     const uint64_t blocks = (n_stripes + dma::SPW - 1) / dma::SPW;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+    if (get_spw() == 4) {
+        const uint64_t b4 = (n_stripes + 3) / 4;
+        if (b4 > 0x7fffffffull) return hipErrorInvalidValue;
+        switch (nf) {
+            case 8: launch_get<8, 4>(b4, p, h, stream); break;
+            case 9: launch_get<9, 4>(b4, p, h, stream); break;
+            case 10: launch_get<10, 4>(b4, p, h, stream); break;
+            case 11: launch_get<11, 4>(b4, p, h, stream); break;
+            default: launch_get<12, 4>(b4, p, h, stream); break;
+        }
+        return hipGetLastError();
+    }
     switch (nf) {
-        case 8: hipLaunchKernelGGL(k_decode_records_dma<8>, dim3((uint32_t)blocks), dim3(64 * GetShape<8>::WAVES), 0, stream, p, h); break;
-        case 9: hipLaunchKernelGGL(k_decode_records_dma<9>, dim3((uint32_t)blocks), dim3(64 * GetShape<9>::WAVES), 0, stream, p, h); break;
-        case 10: hipLaunchKernelGGL(k_decode_records_dma<10>, dim3((uint32_t)blocks), dim3(64 * GetShape<10>::WAVES), 0, stream, p, h); break;
-        case 11: hipLaunchKernelGGL(k_decode_records_dma<11>, dim3((uint32_t)blocks), dim3(64 * GetShape<11>::WAVES), 0, stream, p, h); break;
-        default: hipLaunchKernelGGL(k_decode_records_dma<12>, dim3((uint32_t)blocks), dim3(64 * GetShape<12>::WAVES), 0, stream, p, h); break;
+        case 8: launch_get<8, 8>(blocks, p, h, stream); break;
+        case 9: launch_get<9, 8>(blocks, p, h, stream); break;
+        case 10: launch_get<10, 8>(blocks, p, h, stream); break;
+        case 11: launch_get<11, 8>(blocks, p, h, stream); break;
+        default: launch_get<12, 8>(blocks, p, h, stream); break;
     }
     return hipGetLastError();
 }

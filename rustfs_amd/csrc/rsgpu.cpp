@@ -998,6 +998,17 @@ int hash_records_inplace(uint8_t* const* files, int count, uint64_t shard_len, u
     return RSG_OK;
 }
 
+// True when every stripe's verified map is exactly `present` (the assumed
+// pattern): present rows all ones, absent rows all zeros — a memchr per row
+// instead of the per-stripe run scan.
+bool flags_match_pattern(const uint8_t* flags, const std::vector<uint8_t>& present, uint64_t n) {
+    for (size_t i = 0; i < present.size(); ++i) {
+        const uint8_t* row = flags + i * n;
+        if (present[i] ? std::memchr(row, 0, n) != nullptr : std::memchr(row, 1, n) != nullptr) return false;
+    }
+    return true;
+}
+
 // Calls f(s0, s1, present) for each maximal run of stripes sharing one
 // verified-shard pattern (degraded stripes come in long runs: a lost disk).
 template <class F>
@@ -1369,15 +1380,17 @@ int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64
         if ((st = hip_status(hipMemcpyAsync(ctx->h_flags, d_flags, (size_t)(t + 1) * n, hipMemcpyDeviceToHost, s))))
             return st;
         if ((st = hip_status(hipStreamSynchronize(s)))) return st;
-        flags.assign(ctx->h_flags, ctx->h_flags + (size_t)t * n);
         bool redone = false;
-        st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) -> int {
-            if (present == present0) return RSG_OK;  // the optimistic pass was right
-            redone = true;
-            int e = hip_status(hipMemsetAsync(d_ok + s0, 1, s1 - s0, s));
-            return e ? e : rebuild_run(s0, s1, present, true);
-        });
-        if (st) return st;
+        if (!flags_match_pattern(ctx->h_flags, present0, n)) {
+            flags.assign(ctx->h_flags, ctx->h_flags + (size_t)t * n);
+            st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) -> int {
+                if (present == present0) return RSG_OK;  // the optimistic pass was right
+                redone = true;
+                int e = hip_status(hipMemsetAsync(d_ok + s0, 1, s1 - s0, s));
+                return e ? e : rebuild_run(s0, s1, present, true);
+            });
+            if (st) return st;
+        }
         if (!redone) {
             if (any_verify)
                 for (uint64_t x = 0; x < n; ++x)
@@ -1523,17 +1536,19 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
         if ((st = hip_status(hipMemcpyAsync(ctx->h_flags, d_flags, (size_t)(t + 1) * n, hipMemcpyDeviceToHost, s))))
             return st;
         if ((st = hip_status(hipStreamSynchronize(s)))) return st;
-        flags.assign(ctx->h_flags, ctx->h_flags + (size_t)t * n);
         std::vector<uint8_t> ok(ctx->h_flags + (size_t)t * n, ctx->h_flags + (size_t)(t + 1) * n);
         bool redone = false;
-        st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) -> int {
-            if (present == present0) return RSG_OK;
-            redone = true;
-            int e = hip_status(hipMemsetAsync(d_ok + s0, 1, s1 - s0, s));
-            if (!e) e = heal_run(s0, s1, present);
-            return e ? e : hash_targets(s0, s1);
-        });
-        if (st) return st;
+        if (!flags_match_pattern(ctx->h_flags, present0, n)) {
+            flags.assign(ctx->h_flags, ctx->h_flags + (size_t)t * n);
+            st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) -> int {
+                if (present == present0) return RSG_OK;
+                redone = true;
+                int e = hip_status(hipMemsetAsync(d_ok + s0, 1, s1 - s0, s));
+                if (!e) e = heal_run(s0, s1, present);
+                return e ? e : hash_targets(s0, s1);
+            });
+            if (st) return st;
+        }
         if (redone && any_verify && (st = flags_to_host(ctx, d_ok, n, ok.data(), s))) return st;
         if (any_verify)
             for (uint64_t x = 0; x < n; ++x)
