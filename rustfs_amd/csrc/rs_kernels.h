@@ -88,6 +88,11 @@ bool fused_supported(int C, int R, uint64_t shard_len);
 bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len);
 hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int nf, uint64_t shard_len, uint64_t n_stripes,
                                      hipStream_t stream);
+// One-pass heal for RS(8,4) (k_decode_records_dma with target hashing): nf
+// present source files, `targets` absent target files written with digests.
+bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len);
+hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int nf, int targets, uint64_t shard_len,
+                                   uint64_t n_stripes, hipStream_t stream);
 hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                     hipStream_t stream);
 

@@ -1060,29 +1060,38 @@ __global__ __launch_bounds__((64 * dma::Shape<K, M>::WAVES)) void k_encode_hash_
 //      ok_flags[s] cleared on a compare mismatch; units = S / 512.
 //   h: base[f] = body of record 0 of present file f, stripe_stride = record
 //      pitch, flag_base[f][s] cleared on a digest mismatch, key, n.
-template <int NF, int G>
+// TH > 0 is the one-pass heal (rsg_heal_records_dev): the TH stored rows are
+// target record bodies (out_stripe_stride = record pitch, no copy-through);
+// the GF waves also write them into a double-buffered LDS row area, and
+// ceil(8 TH / 16) target-hasher waves hash them one step behind and write
+// each target record's digest header (BitrotWriter::write).
+template <int NF, int G, int TH = 0>
 struct GetShape {
     static constexpr int SPW = G, HS = G / 2;             // stripes per workgroup, per DMA half
     static constexpr int NI = HS * NF;                    // DMA instructions per step
     static constexpr uint32_t DSLOT = NI * dma::IP;
     static constexpr int HW = (NI + 7) / 8;               // DMA/hash waves
     static constexpr int LAST = NI - 8 * (HW - 1);        // instructions of the last one
-    static constexpr int WAVES = HW + SPW;
+    static constexpr uint32_t TSLOT = SPW * (TH ? TH : 1) * dma::PP;  // one step of target rows
+    static constexpr int TW = (SPW * TH + 15) / 16;       // target-hasher waves
+    static constexpr int WAVES = HW + SPW + TW;
 };
 
-template <int NF, int G>
-__global__ __launch_bounds__((64 * GetShape<NF, G>::WAVES)) void k_decode_records_dma(const GfApplyParams p,
-                                                                                      const HashParams h) {
+template <int NF, int G, int TH>
+__global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_records_dma(const GfApplyParams p,
+                                                                                          const HashParams h) {
     using dma::CH;
     using dma::D;
     using dma::IP;
     using dma::read16;
     using dma::vmcnt_imm;
-    using L = GetShape<NF, G>;
+    using dma::PP;
+    using L = GetShape<NF, G, TH>;
     constexpr int SPW = L::SPW, HS = L::HS;
     constexpr int C = 8, RM = 4;
     __shared__ __attribute__((aligned(16))) uint8_t ring[D * L::DSLOT];
     __shared__ __attribute__((aligned(16))) uint8_t tabs[C * RM * 32];
+    __shared__ __attribute__((aligned(16))) uint8_t trow[TH ? 2 * L::TSLOT : 16];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u, q = lane & 3u;
     const uint64_t n = h.n;
     const uint32_t steps = p.units;
@@ -1095,6 +1104,29 @@ __global__ __launch_bounds__((64 * GetShape<NF, G>::WAVES)) void k_decode_record
     }
     // (the tables are published by B(0), which every wave passes before use)
 
+    if (TH && wave >= (uint32_t)(L::HW + SPW)) {
+        // ------------- target hasher: quad j hashes target row stream -------------
+        const uint32_t pi = 16 * (wave - L::HW - SPW) + (lane >> 2);  // r * SPW + stripe
+        const bool on = pi < (uint32_t)(SPW * TH);
+        const uint32_t r = on ? pi / SPW : 0, e = pi % SPW;
+        const bool live = on && s0 + e < n;
+        const uint32_t roff = (on ? pi : 0) * PP + 8 * q;
+        HHQuad st;
+        hhq_init(st, h.key, q);
+        lds_barrier();  // B(0)
+#pragma unroll 1
+        for (uint32_t s = 0; s <= steps; ++s) {
+            if (s > 0) {  // target rows of step s-1, published by B(s)
+                uint64_t w[16];
+                read16((uint32_t)(uintptr_t)trow + ((s - 1) & 1) * L::TSLOT + roff, w);
+#pragma unroll
+                for (int t = 0; t < 16; ++t) hhq_update(st, w[t]);
+            }
+            if (s < steps) lds_barrier();  // B(s+1)
+        }
+        if (live) hhq_finish(st, p.out_base + (s0 + e) * p.out_stripe_stride + p.out_off[r] - 32, q);
+        return;
+    }
     if (wave >= (uint32_t)L::HW) {
         // ------------------------- GF wave: one stripe -------------------------
         const uint32_t e = wave - L::HW;
@@ -1142,6 +1174,8 @@ __global__ __launch_bounds__((64 * GetShape<NF, G>::WAVES)) void k_decode_record
                 const uint2 v = make_uint2(acc[r][0], acc[r][1]);
                 if ((uint32_t)r < nst) {
                     if (live) st16_nt_half(ob + p.out_off[r] + (uint64_t)s * CH, v);
+                    if constexpr (TH > 0)
+                        *(uint2*)(trow + (s & 1) * L::TSLOT + (r * SPW + e) * PP + lane * 8u) = v;
                 } else {
                     const uint2 o = *(const uint2*)(slot + (C + (r - nst)) * HS * IP);
                     bad |= ((o.x ^ v.x) | (o.y ^ v.y)) != 0u;
@@ -1641,10 +1675,43 @@ static int get_spw() {
     return v;
 }
 
-template <int NF, int G>
+template <int NF, int G, int TH = 0>
 static void launch_get(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
-    hipLaunchKernelGGL((k_decode_records_dma<NF, G>), dim3((uint32_t)blocks), dim3(64 * GetShape<NF, G>::WAVES), 0,
-                       stream, p, h);
+    hipLaunchKernelGGL((k_decode_records_dma<NF, G, TH>), dim3((uint32_t)blocks),
+                       dim3(64 * GetShape<NF, G, TH>::WAVES), 0, stream, p, h);
+}
+
+bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len) {
+    return decode_dma_supported(k, m, nf, shard_len) && targets >= 1 && targets <= 4 && nf + targets <= 12;
+}
+
+hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int nf, int targets, uint64_t shard_len,
+                                   uint64_t n_stripes, hipStream_t stream) {
+    if (!heal_dma_supported(8, 4, nf, targets, shard_len) || n_stripes == 0 || p.R > 4 ||
+        p.n_store != (uint32_t)targets || p.copy_mask)
+        return hipErrorInvalidValue;
+    for (int f = 0; f < nf; ++f)
+        if ((uintptr_t)h.base[f] % 16) return hipErrorInvalidValue;
+    if (h.stripe_stride % 16 || p.out_stripe_stride != h.stripe_stride) return hipErrorInvalidValue;
+    p.units = (uint32_t)(shard_len / dma::CH);
+    h.n = n_stripes;
+    const uint64_t blocks = (n_stripes + 7) / 8;
+    if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+    // the present + target files are at most the k + m shards
+    switch (nf * 8 + targets) {
+        case 8 * 8 + 1: launch_get<8, 8, 1>(blocks, p, h, stream); break;
+        case 8 * 8 + 2: launch_get<8, 8, 2>(blocks, p, h, stream); break;
+        case 8 * 8 + 3: launch_get<8, 8, 3>(blocks, p, h, stream); break;
+        case 8 * 8 + 4: launch_get<8, 8, 4>(blocks, p, h, stream); break;
+        case 9 * 8 + 1: launch_get<9, 8, 1>(blocks, p, h, stream); break;
+        case 9 * 8 + 2: launch_get<9, 8, 2>(blocks, p, h, stream); break;
+        case 9 * 8 + 3: launch_get<9, 8, 3>(blocks, p, h, stream); break;
+        case 10 * 8 + 1: launch_get<10, 8, 1>(blocks, p, h, stream); break;
+        case 10 * 8 + 2: launch_get<10, 8, 2>(blocks, p, h, stream); break;
+        case 11 * 8 + 1: launch_get<11, 8, 1>(blocks, p, h, stream); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len) {

@@ -1239,6 +1239,60 @@ int launch_get_one_pass(Codec& cd, const std::vector<uint8_t>& present, const st
     return hip_status(rsg::launch_decode_records_dma(p, h, (int)files.size(), shard_len, n, s));
 }
 
+// Launch the one-pass heal (k_decode_records_dma with target hashing) for
+// the pattern `present`: survivors = the first k present files; rows = every
+// target (absent from the sources), then the present non-survivor parity,
+// compared in place (heal.rs:180-196).
+int launch_heal_one_pass(Codec& cd, const std::vector<uint8_t>& present, const std::vector<int>& files,
+                         const std::vector<int>& targets, const uint8_t* const* d_files, uint8_t* const* d_targets,
+                         uint8_t* d_flags, uint8_t* d_ok, int k, uint64_t shard_len, uint64_t n, const uint64_t* key,
+                         bool& any_verify, hipStream_t s) {
+    auto plan = cd.plan(present.data());
+    if (!plan) return RSG_ERR_TOO_FEW_SHARDS;
+    for (int c = 0; c < k; ++c)
+        if (plan->survivors[c] != files[c]) return RSG_ERR_INVALID_ARG;
+    const uint64_t rec = 32 + shard_len;
+    rsg::GfApplyParams p;
+    std::memset(&p, 0, sizeof(p));
+    std::vector<uint8_t> coef;
+    int R = 0;
+    p.out_base = d_targets[targets[0]] + 32;
+    for (int i : targets) {
+        coef.resize((size_t)(R + 1) * k);
+        plan_row(cd, *plan, i, &coef[(size_t)R * k]);
+        p.out_off[R++] = (uint64_t)(uintptr_t)(d_targets[i] + 32) - (uint64_t)(uintptr_t)p.out_base;
+    }
+    const int n_store = R;
+    for (int f = k; f < (int)files.size(); ++f) {  // present non-survivors: parity, ascending
+        if (R >= 4) return RSG_ERR_UNSUPPORTED;
+        coef.resize((size_t)(R + 1) * k);
+        plan_row(cd, *plan, files[f], &coef[(size_t)R * k]);
+        ++R;
+    }
+    if (R > n_store) any_verify = true;
+    for (int r = 0; r < R; ++r)
+        for (int c = 0; c < k; ++c) coef_tables(coef[(size_t)r * k + c], p.tab[r][c]);
+    p.C = (uint32_t)k;
+    p.R = (uint32_t)R;
+    p.n_store = (uint32_t)n_store;
+    p.mode = rsg::GF_MODE_STORE_COMPARE;
+    p.out_stripe_stride = rec;
+    p.ok_flags = d_ok;
+    rsg::HashParams h;
+    std::memset(&h, 0, sizeof(h));
+    h.len = shard_len;
+    h.stripe_stride = rec;
+    std::memcpy(h.key, key, sizeof(h.key));
+    h.nbases = (uint32_t)files.size();
+    h.digest_off = -32;
+    for (size_t f = 0; f < files.size(); ++f) {
+        h.base[f] = d_files[files[f]] + 32;
+        h.flag_base[f] = d_flags + (size_t)files[f] * n;
+    }
+    return hip_status(
+        rsg::launch_heal_records_dma(p, h, (int)files.size(), (int)targets.size(), shard_len, n, s));
+}
+
 // GET engine body (ctx->mu held): verify records, copy/rebuild the k data
 // shards of every stripe into d_out (n x k*S), optional surplus-parity check.
 // Uses ctx->d_scratch[0, (t+1)*n).  `flags` returns the verified-shard map.
@@ -1526,12 +1580,36 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
         // copy + synchronisation brings back the verified map and the parity
         // verdict.  Runs whose verified pattern differs are redone (targets
         // rewritten and rehashed) from their actual valid shards.
-        if ((st = heal_run(0, n, present0))) return st;
-        if ((st = hip_status(hipMemsetAsync(d_flags, 0, (size_t)t * n, s)))) return st;
-        std::vector<int> all_idx;
-        for (int i = 0; i < t; ++i)
+        std::vector<int> all_idx, tg_idx;
+        for (int i = 0; i < t; ++i) {
             if (d_files[i]) all_idx.push_back(i);
-        if ((st = launch_verify_and_digest(all_idx, d_files, d_flags, d_targets, t, shard_len, n, key, s))) return st;
+            if (d_targets[i]) tg_idx.push_back(i);
+        }
+        bool one_pass = get_dma_enabled() &&
+                        rsg::heal_dma_supported(k, m, (int)all_idx.size(), (int)tg_idx.size(), shard_len) &&
+                        rec % 16 == 0;
+        for (int i : all_idx) one_pass = one_pass && (uintptr_t)(d_files[i] + 32) % 16 == 0;
+        for (int i : tg_idx) one_pass = one_pass && !d_files[i] && (uintptr_t)(d_targets[i] + 32) % 8 == 0;
+        if (one_pass) {
+            // RS(8,4): verify every source record, write every target record
+            // (body + digest) and compare the surplus parity in ONE pass
+            if ((st = hip_status(hipMemsetAsync(d_flags, 0, (size_t)t * n, s)))) return st;
+            for (size_t a = 0; a < all_idx.size();) {
+                size_t b = a + 1;
+                while (b < all_idx.size() && all_idx[b] == all_idx[b - 1] + 1) ++b;
+                if ((st = hip_status(hipMemsetAsync(d_flags + (size_t)all_idx[a] * n, 1, (b - a) * n, s)))) return st;
+                a = b;
+            }
+            if ((st = launch_heal_one_pass(*cd, present0, all_idx, tg_idx, d_files, d_targets, d_flags, d_ok, k,
+                                           shard_len, n, key, any_verify, s)))
+                return st;
+            for (uint64_t x = 0; x < n; ++x) h_status[x] = RSG_OK;
+        } else {
+            if ((st = heal_run(0, n, present0))) return st;
+            if ((st = hip_status(hipMemsetAsync(d_flags, 0, (size_t)t * n, s)))) return st;
+            if ((st = launch_verify_and_digest(all_idx, d_files, d_flags, d_targets, t, shard_len, n, key, s)))
+                return st;
+        }
         if ((st = ctx->ensure_host_flags((size_t)(t + 1) * n))) return st;
         if ((st = hip_status(hipMemcpyAsync(ctx->h_flags, d_flags, (size_t)(t + 1) * n, hipMemcpyDeviceToHost, s))))
             return st;

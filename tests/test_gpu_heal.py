@@ -148,3 +148,59 @@ def test_bitrot_verify_batch(gpu, oracle, legacy):
     f2 = _shard_file(oracle, part2, S, legacy)
     assert bitrot_verify_batch([torch.tensor(list(f2), dtype=torch.uint8).cuda()], len(f2), len(part2), algo, S) == [0]
     assert bitrot_verify_batch([torch.empty(0, dtype=torch.uint8).cuda()], 0, 0, algo, S) == [0]
+
+
+@pytest.mark.parametrize("lost", [(1, 8), (0,), (0, 1, 2, 3), (9, 10, 11), (2, 5, 10)])
+def test_heal_one_pass_many_workgroups(gpu, oracle, lost):
+    """RS(8,4) heal through the one-pass kernel (verify every source record,
+    write every target record with its digest, compare the surplus parity)
+    over many 8-stripe workgroups and a ragged last one: the healed files are
+    byte-identical to the originals; a rotten source record is redone from
+    other survivors; a re-hashed inconsistent surplus parity fails its stripe
+    alone, whose target digests are zeroed."""
+    import torch
+    from rustfs_amd import Erasure, _lib
+    k, m, S, n = 8, 4, 4096, 2051
+    rec = 32 + S
+    e = Erasure(k, m, k * S)
+    g = torch.Generator(device="cuda").manual_seed(len(lost) * 7 + lost[0])
+    st = torch.zeros((n, k + m, S), dtype=torch.uint8, device="cuda")
+    st[:, :k] = torch.randint(0, 256, (n, k, S), dtype=torch.uint8, device="cuda", generator=g)
+    dig = torch.zeros((n, k + m, 32), dtype=torch.uint8, device="cuda")
+    e.encode_batch(st, dig)
+    files = [torch.cat([dig[:, i], st[:, i]], dim=1).contiguous().reshape(-1) for i in range(k + m)]
+    # the encoded records match the oracle on a sample (so "identical to the originals" is the reference's bytes)
+    for s in (0, n - 1):
+        ref = st[s].cpu().numpy().copy()
+        ref[k:] = 0
+        oracle.encode(k, m, ref)
+        assert np.array_equal(st[s].cpu().numpy(), ref)
+    src = [None if i in lost else files[i].clone() for i in range(k + m)]
+    present = [i for i in range(k + m) if i not in lost]
+    rot = present[2]
+    src[rot][700 * rec + 32 + 5] ^= 0x04            # rotten source record, stripe 700
+    bad_stripe = None
+    surplus = [i for i in present if i >= k][max(0, k - len([i for i in present if i < k])):]
+    if surplus:                                     # a surplus parity, inconsistent but re-hashed, stripe 1500
+        f = surplus[-1]
+        body = src[f][1500 * rec + 32: 1501 * rec].cpu().numpy().copy()
+        body[11] ^= 0x20
+        src[f][1500 * rec + 32: 1501 * rec] = torch.from_numpy(body).cuda()
+        src[f][1500 * rec: 1500 * rec + 32] = torch.from_numpy(
+            np.frombuffer(oracle.hh256s(body.tobytes()), dtype=np.uint8).copy()).cuda()
+        bad_stripe = 1500
+    tgt = [torch.zeros(n * rec, dtype=torch.uint8, device="cuda") if i in lost else None for i in range(k + m)]
+    status = e.heal_records_batch(src, tgt, S, n)
+    # with exactly k sources the rotten record costs stripe 700 its read quorum
+    want = {1500: _lib.RSG_ERR_INCONSISTENT_SOURCES} if bad_stripe is not None else {}
+    if len(present) == k:
+        want[700] = _lib.RSG_ERR_TOO_FEW_SHARDS
+    assert {i: x for i, x in enumerate(status) if x != 0} == want
+    for i in lost:
+        got = tgt[i].reshape(n, rec)
+        ref = files[i].reshape(n, rec)
+        ok = torch.ones(n, dtype=torch.bool, device="cuda")
+        for b in want:
+            ok[b] = False
+            assert not bool(got[b, :32].any())  # digest zeroed: never verifies
+        assert torch.equal(got[ok], ref[ok]), f"shard {i}"
