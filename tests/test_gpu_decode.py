@@ -76,6 +76,7 @@ def test_decode_records_detects_inconsistent_parity(gpu, oracle):
     (8, 4, 131072, 5, (0,)), (8, 4, 131072, 6, (0, 3)), (8, 4, 4096, 9, (1, 4, 6)), (8, 4, 4096, 7, (0, 2, 5, 7)),
     (8, 4, 4096, 7, (3, 9)), (8, 4, 4096, 5, (2, 8, 11)), (4, 2, 65536, 4, (1,)), (6, 3, 4096, 3, (0, 5, 7)),
     (2, 2, 1024, 3, (0,)), (1, 3, 512, 2, (0, 2)), (5, 4, 2048, 9, (4,)),
+    (8, 4, 512, 17, (0,)), (8, 4, 512, 3, (1, 2, 3, 4)), (8, 4, 1024, 8, (7, 8, 9)), (8, 4, 4608, 11, (6,)),
 ])
 def test_decode_records_lost_disk_one_pass(gpu, oracle, k, m, S, n, lost):
     """A lost disk (whole data shard files missing) takes the one-pass GET

@@ -150,6 +150,23 @@ def test_bitrot_verify_batch(gpu, oracle, legacy):
     assert bitrot_verify_batch([torch.empty(0, dtype=torch.uint8).cuda()], 0, 0, algo, S) == [0]
 
 
+@pytest.mark.parametrize("k,m,S,n", [(8, 4, 512, 9), (8, 4, 4608, 3), (8, 4, 1024, 1)])
+def test_heal_one_pass_short_walks(gpu, oracle, k, m, S, n):
+    """One-pass heal over a single 512-byte step, a step count that is not a
+    power of two, and a single stripe (seven dead stripes in the workgroup)."""
+    import torch
+    from rustfs_amd import Erasure
+    shards, recs, files = _records(torch, oracle, k, m, S, n, seed=S + n)
+    e = Erasure(k, m, k * S)
+    rec = 32 + S
+    for lost in ((3,), (0, 11), (1, 2, 9, 10)):
+        src = [None if i in lost else files[i] for i in range(k + m)]
+        tgt = [torch.zeros(n * rec, dtype=torch.uint8, device="cuda") if i in lost else None for i in range(k + m)]
+        assert e.heal_records_batch(src, tgt, S, n) == [0] * n
+        for i in lost:
+            assert np.array_equal(tgt[i].cpu().numpy().reshape(n, rec), recs[i]), (lost, i)
+
+
 @pytest.mark.parametrize("lost", [(1, 8), (0,), (0, 1, 2, 3), (9, 10, 11), (2, 5, 10)])
 def test_heal_one_pass_many_workgroups(gpu, oracle, lost):
     """RS(8,4) heal through the one-pass kernel (verify every source record,
