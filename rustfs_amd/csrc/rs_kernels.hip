@@ -962,12 +962,14 @@ __global__ __launch_bounds__((64 * dma::Shape<K, M>::WAVES)) void k_encode_hash_
     const uint32_t ring_base = (uint32_t)(uintptr_t)ring;
 
     if (wave < (uint32_t)EW) {
+        if (p.byte_begin & 2) __builtin_amdgcn_s_setprio(2);  // RSG_ENC_PRIO A/B knob
         const uint32_t g = wave % 2;
         if (wave < 2) encoder<K, M, 0>(p, n, steps, s0, g, ring, prow);
         else encoder<K, M, 1>(p, n, steps, s0, g, ring, prow);
         return;
     }
     // ---------------------------------- hashers ----------------------------------
+    if (p.byte_begin & 1) __builtin_amdgcn_s_setprio(2);
     const uint32_t hw = wave - EW, j = lane >> 2;
     const bool is_data = hw < (uint32_t)L::DATA;
     constexpr int NDI = 8;  // DMA instructions a data-hasher wave owns
@@ -1065,6 +1067,20 @@ __global__ __launch_bounds__((64 * dma::Shape<K, M>::WAVES)) void k_encode_hash_
 // the GF waves also write them into a double-buffered LDS row area, and
 // ceil(8 TH / 16) target-hasher waves hash them one step behind and write
 // each target record's digest header (BitrotWriter::write).
+// Issue priority of the wave roles in the DMA kernels (passed in an unused
+// kernel-argument field): bit 0 raises the hash waves, bit 1 the GF /
+// encoder waves.  Default 2: the GF waves of the one-pass GET/heal run ahead
+// of the latency-bound hash chains instead of queueing behind them (RS(8,4),
+// n = 4096: GET 2 lost 2.44 -> 2.18 ms, heal 1.92 -> 1.69 ms;
+// profiles/r02/ab_prio/).  RSG_DMA_PRIO=<0..3> overrides for A/B runs.
+static uint64_t dma_prio() {
+    static const uint64_t v = [] {
+        const char* e = getenv("RSG_DMA_PRIO");
+        return e ? (uint64_t)(atoi(e) & 3) : 2ull;
+    }();
+    return v;
+}
+
 template <int NF, int G, int TH = 0>
 struct GetShape {
     static constexpr int SPW = G, HS = G / 2;             // stripes per workgroup, per DMA half
@@ -1106,6 +1122,7 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_re
 
     if (TH && wave >= (uint32_t)(L::HW + SPW)) {
         // ------------- target hasher: quad j hashes target row stream -------------
+        if (p.byte_begin & 1) __builtin_amdgcn_s_setprio(2);
         const uint32_t pi = 16 * (wave - L::HW - SPW) + (lane >> 2);  // r * SPW + stripe
         const bool on = pi < (uint32_t)(SPW * TH);
         const uint32_t r = on ? pi / SPW : 0, e = pi % SPW;
@@ -1129,6 +1146,7 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_re
     }
     if (wave >= (uint32_t)L::HW) {
         // ------------------------- GF wave: one stripe -------------------------
+        if (p.byte_begin & 2) __builtin_amdgcn_s_setprio(2);  // A/B knob (RSG_DMA_PRIO)
         const uint32_t e = wave - L::HW;
         const uint64_t stripe = s0 + e;
         const bool live = stripe < n;
@@ -1192,6 +1210,7 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_re
         return;
     }
     // ------------------------- DMA + verify-hash wave -------------------------
+    if (p.byte_begin & 1) __builtin_amdgcn_s_setprio(2);  // A/B knob (RSG_DMA_PRIO)
     const uint32_t hw = wave, j = lane >> 2;
     const int ndi = (hw == (uint32_t)(L::HW - 1)) ? L::LAST : 8;  // instructions this wave owns
     const uint32_t idx = 8 * hw + (j & 7u), half = j >> 3;
@@ -1657,6 +1676,12 @@ static bool dma_supported(const GfApplyParams& p, uint64_t shard_len, uint64_t n
 
 static hipError_t launch_encode_hash_dma(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                          hipStream_t stream) {
+    // RSG_ENC_PRIO = 1 (hashers), 2 (encoders), 3: wave priorities for A/B runs
+    static const uint64_t prio = [] {
+        const char* e = getenv("RSG_ENC_PRIO");
+        return e ? (uint64_t)(atoi(e) & 3) : 0ull;
+    }();
+    p.byte_begin = prio;
     p.units = (uint32_t)(shard_len / dma::CH);
     h.n = n_stripes;
     const uint64_t blocks = (n_stripes + dma::SPW - 1) / dma::SPW;
@@ -1687,6 +1712,7 @@ bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len) {
 
 hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int nf, int targets, uint64_t shard_len,
                                    uint64_t n_stripes, hipStream_t stream) {
+    p.byte_begin = dma_prio();
     if (!heal_dma_supported(8, 4, nf, targets, shard_len) || n_stripes == 0 || p.R > 4 ||
         p.n_store != (uint32_t)targets || p.copy_mask)
         return hipErrorInvalidValue;
@@ -1721,6 +1747,7 @@ bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len) {
 
 hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int nf, uint64_t shard_len, uint64_t n_stripes,
                                      hipStream_t stream) {
+    p.byte_begin = dma_prio();
     if (!decode_dma_supported(8, 4, nf, shard_len) || n_stripes == 0 || p.R > 4 || p.n_store > p.R)
         return hipErrorInvalidValue;
     for (int f = 0; f < nf; ++f)
