@@ -1168,12 +1168,17 @@ int verify_gather(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64_t n, co
 }
 
 // RSG_GET_DMA=0 keeps the two-pass lost-disk GET (A/B runs).
-bool get_dma_enabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("RSG_GET_DMA");
-        return !(e && e[0] == '0');
-    }();
-    return on;
+// One-pass GET/heal (k_decode_records_dma) for a batch of n stripes.  A
+// workgroup walks its 8 stripes front to back (~0.6 ms for 1 MiB RS(8,4)
+// stripes), so below ~1024 stripes, where the grid does not fill the CUs,
+// the two-pass path (GF pass spread over every column, then one verify
+// launch) returns sooner: n = 8 takes 0.67 ms one-pass.  RSG_GET_DMA=0 never,
+// =1 always (tests, A/B runs); read per call.
+bool get_dma_enabled(uint64_t n) {
+    const char* e = std::getenv("RSG_GET_DMA");
+    if (e && e[0] == '0') return false;
+    if (e && e[0] == '1') return true;
+    return n >= 1024;
 }
 
 // Launch k_decode_records_dma over all stripes for the erasure pattern
@@ -1405,7 +1410,7 @@ int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64
         std::vector<int> all_idx;
         for (int i = 0; i < t; ++i)
             if (d_files[i]) all_idx.push_back(i);
-        bool one_pass = get_dma_enabled() && rsg::decode_dma_supported(k, m, nfiles, shard_len) &&
+        bool one_pass = get_dma_enabled(n) && rsg::decode_dma_supported(k, m, nfiles, shard_len) &&
                         rec % 16 == 0;
         for (int i : all_idx) one_pass = one_pass && (uintptr_t)(d_files[i] + 32) % 16 == 0;
         if (one_pass) {
@@ -1585,7 +1590,7 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
             if (d_files[i]) all_idx.push_back(i);
             if (d_targets[i]) tg_idx.push_back(i);
         }
-        bool one_pass = get_dma_enabled() &&
+        bool one_pass = get_dma_enabled(n) &&
                         rsg::heal_dma_supported(k, m, (int)all_idx.size(), (int)tg_idx.size(), shard_len) &&
                         rec % 16 == 0;
         for (int i : all_idx) one_pass = one_pass && (uintptr_t)(d_files[i] + 32) % 16 == 0;

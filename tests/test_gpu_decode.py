@@ -5,7 +5,16 @@ bitrot.rs:227-247, erasure.rs:935-973)."""
 import numpy as np
 import pytest
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("engine_path")]
+
+
+@pytest.fixture(params=["one_pass", "two_pass"], autouse=False)
+def engine_path(request, monkeypatch):
+    """Every test runs through both lost-disk engines: the one-pass RS(8,4)
+    kernel (forced at any batch size) and the two-pass path (librsgpu reads
+    RSG_GET_DMA per call; by default the one-pass kernel takes >= 1024 stripes)."""
+    monkeypatch.setenv("RSG_GET_DMA", "1" if request.param == "one_pass" else "0")
+    return request.param
 
 
 def _records(torch, k, m, S, n, seed):
