@@ -49,6 +49,8 @@ __device__ __forceinline__ uint32_t gf_mul_word(const uint32_t* t, uint32_t s0, 
 __device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
+#include "rs84_xornet.h"  // generated (tools/gen_xornet.py); uses x3
+
 // odd: input index parity (a compile-time constant in the unrolled loops)
 __device__ __forceinline__ void gf_fold(bool odd, uint32_t& acc, uint32_t& pend, uint32_t a, uint32_t b, uint32_t c) {
     if (odd) {
@@ -884,14 +886,15 @@ __device__ __forceinline__ void fold(uint32_t (&acc)[RN][8], const uint32_t (&P)
     }
 }
 
-template <int K, int M>
+template <int K, int M, int NE = EW>
 struct Shape {
     static constexpr int NI = HS * K;                 // DMA instructions per step (1 KiB each)
     static constexpr uint32_t DSLOT = NI * IP;        // one step of all data rows
     static constexpr uint32_t PSLOT = SPW * M * PP;   // one step of all parity rows
     static constexpr int DATA = (SPW * K) / 16;       // data-hasher waves
     static constexpr int PAR = (SPW * M + 15) / 16;   // parity-hasher waves
-    static constexpr int WAVES = EW + DATA + PAR;
+    static constexpr int ENC = NE;                    // encoder waves: 2 per stripe group (EW) or 1 (XOR network)
+    static constexpr int WAVES = NE + DATA + PAR;
 };
 
 // Encoder wave: stripe group g, parity rows [R0, R0 + M/2) (two waves per group)
@@ -945,14 +948,67 @@ __device__ __forceinline__ void encoder(const GfApplyParams& p, uint64_t n, uint
         lds_barrier();  // B(s+1): parity rows of step s published
     }
 }
+
+// One encoder wave per stripe group computing all four RS(8,4) parity rows:
+// the 64 input planes go through the generated common-subexpression XOR
+// network (rs84_xornet.h: 239 three-input XORs instead of 504), and each data
+// shard is bit-transposed once per group instead of once per row pair
+// (per group and step: 8 + 4 transposes + 239 XORs, against 2 x (8 + 2)
+// transposes + 504 XORs for two encoder() waves).
+template <int K, int M>
+__device__ __forceinline__ void encoder_net(const GfApplyParams& p, uint64_t n, uint32_t steps, uint64_t s0,
+                                            uint32_t g, const uint8_t* ring, uint8_t* prow) {
+    static_assert(K == 8 && M == 4, "the XOR network is RS(8,4)'s");
+    using L = Shape<K, M, 2>;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t m4 = vgpr_const(0x0f0f0f0fu), m2 = vgpr_const(0x33333333u), m1 = vgpr_const(0x55555555u);
+    const uint32_t mys[4] = {2 * g, 2 * g + 1, 2 * g + HS, 2 * g + HS + 1};
+    uint8_t* const base = p.out_base;
+    uint64_t pdst[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pdst[j] = (s0 + mys[j] < n ? s0 + mys[j] : 0) * p.stripe_stride + lane * 8u;
+    lds_barrier();  // B(0): slot 0 landed
+#pragma unroll 1
+    for (uint32_t s = 0; s < steps; ++s) {
+        const uint8_t* slot = ring + (s % D) * L::DSLOT + 2 * g * IP + lane * 8u;
+        uint32_t P[64];
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            const uint8_t* row = slot + HS * c * IP;
+            const uint2 a0 = *(const uint2*)row, a1 = *(const uint2*)(row + IP);
+            const uint2 a2 = *(const uint2*)(row + CH), a3 = *(const uint2*)(row + IP + CH);
+            uint32_t w[8] = {a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y};
+            transpose(w, m4, m2, m1);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) P[8 * c + j] = w[j];
+        }
+        uint32_t O[32];
+        xn::rs84_encode_planes(P, O);
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            uint32_t w[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) w[i] = O[8 * r + i];
+            transpose(w, m4, m2, m1);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint2 v = make_uint2(w[2 * j], w[2 * j + 1]);
+                *(uint2*)(base + pdst[j] + p.out_off[r] + (uint64_t)s * CH) = v;
+                *(uint2*)(prow + (s % NP) * L::PSLOT + (r * SPW + mys[j]) * PP + lane * 8u) = v;
+            }
+        }
+        lds_barrier();  // B(s+1): parity rows of step s published
+    }
+}
 }  // namespace dma
 
-template <int K, int M>
-__global__ __launch_bounds__((64 * dma::Shape<K, M>::WAVES)) void k_encode_hash_dma(const GfApplyParams p,
-                                                                                  const HashParams h) {
+template <int K, int M, int NE = dma::EW>
+__global__ __launch_bounds__((64 * dma::Shape<K, M, NE>::WAVES)) void k_encode_hash_dma(const GfApplyParams p,
+                                                                                      const HashParams h) {
     using namespace dma;
     static_assert(K % 2 == 0 && M % 2 == 0 && K <= 8 && M <= 4 && M >= 2, "pairs of shards per wave");
-    using L = Shape<K, M>;
+    static_assert(NE == 4 || NE == 2, "two encoder waves per stripe group, or one with the XOR network");
+    using L = Shape<K, M, NE>;
     __shared__ __attribute__((aligned(16))) uint8_t ring[D * L::DSLOT];
     __shared__ __attribute__((aligned(16))) uint8_t prow[NP * L::PSLOT];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u, q = lane & 3u;
@@ -961,16 +1017,17 @@ __global__ __launch_bounds__((64 * dma::Shape<K, M>::WAVES)) void k_encode_hash_
     const uint64_t s0 = (uint64_t)blockIdx.x * SPW;
     const uint32_t ring_base = (uint32_t)(uintptr_t)ring;
 
-    if (wave < (uint32_t)EW) {
+    if (wave < (uint32_t)NE) {
         if (p.byte_begin & 2) __builtin_amdgcn_s_setprio(2);  // RSG_ENC_PRIO A/B knob
         const uint32_t g = wave % 2;
-        if (wave < 2) encoder<K, M, 0>(p, n, steps, s0, g, ring, prow);
+        if constexpr (NE == 2) encoder_net<K, M>(p, n, steps, s0, g, ring, prow);
+        else if (wave < 2) encoder<K, M, 0>(p, n, steps, s0, g, ring, prow);
         else encoder<K, M, 1>(p, n, steps, s0, g, ring, prow);
         return;
     }
     // ---------------------------------- hashers ----------------------------------
     if (p.byte_begin & 1) __builtin_amdgcn_s_setprio(2);
-    const uint32_t hw = wave - EW, j = lane >> 2;
+    const uint32_t hw = wave - NE, j = lane >> 2;
     const bool is_data = hw < (uint32_t)L::DATA;
     constexpr int NDI = 8;  // DMA instructions a data-hasher wave owns
     uint32_t stripe_l, shard, roff;
@@ -1681,12 +1738,22 @@ static hipError_t launch_encode_hash_dma(GfApplyParams p, HashParams h, uint64_t
         const char* e = getenv("RSG_ENC_PRIO");
         return e ? (uint64_t)(atoi(e) & 3) : 0ull;
     }();
+    // RSG_DMA_EW = 4: two encoder waves per stripe group (per-row XOR folds),
+    // else one per group running the generated XOR network (A/B runs)
+    static const int ew = [] {
+        const char* e = getenv("RSG_DMA_EW");
+        return e && atoi(e) == 4 ? 4 : 2;
+    }();
     p.byte_begin = prio;
     p.units = (uint32_t)(shard_len / dma::CH);
     h.n = n_stripes;
     const uint64_t blocks = (n_stripes + dma::SPW - 1) / dma::SPW;
-    hipLaunchKernelGGL((k_encode_hash_dma<8, 4>), dim3((uint32_t)blocks), dim3(64 * dma::Shape<8, 4>::WAVES), 0,
-                       stream, p, h);
+    if (ew == 4)
+        hipLaunchKernelGGL((k_encode_hash_dma<8, 4, 4>), dim3((uint32_t)blocks),
+                           dim3(64 * dma::Shape<8, 4, 4>::WAVES), 0, stream, p, h);
+    else
+        hipLaunchKernelGGL((k_encode_hash_dma<8, 4, 2>), dim3((uint32_t)blocks),
+                           dim3(64 * dma::Shape<8, 4, 2>::WAVES), 0, stream, p, h);
     return hipGetLastError();
 }
 
