@@ -955,7 +955,7 @@ __device__ __forceinline__ void encoder(const GfApplyParams& p, uint64_t n, uint
 // shard is bit-transposed once per group instead of once per row pair
 // (per group and step: 8 + 4 transposes + 239 XORs, against 2 x (8 + 2)
 // transposes + 504 XORs for two encoder() waves).
-template <int K, int M>
+template <int K, int M, int NT>
 __device__ __forceinline__ void encoder_net(const GfApplyParams& p, uint64_t n, uint32_t steps, uint64_t s0,
                                             uint32_t g, const uint8_t* ring, uint8_t* prow) {
     static_assert(K == 8 && M == 4, "the XOR network is RS(8,4)'s");
@@ -993,7 +993,8 @@ __device__ __forceinline__ void encoder_net(const GfApplyParams& p, uint64_t n, 
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const uint2 v = make_uint2(w[2 * j], w[2 * j + 1]);
-                *(uint2*)(base + pdst[j] + p.out_off[r] + (uint64_t)s * CH) = v;
+                if constexpr (NT & 2) st16_nt_half(base + pdst[j] + p.out_off[r] + (uint64_t)s * CH, v);
+                else *(uint2*)(base + pdst[j] + p.out_off[r] + (uint64_t)s * CH) = v;
                 *(uint2*)(prow + (s % NP) * L::PSLOT + (r * SPW + mys[j]) * PP + lane * 8u) = v;
             }
         }
@@ -1002,7 +1003,7 @@ __device__ __forceinline__ void encoder_net(const GfApplyParams& p, uint64_t n, 
 }
 }  // namespace dma
 
-template <int K, int M, int NE = dma::EW>
+template <int K, int M, int NE = dma::EW, int NT = 0>
 __global__ __launch_bounds__((64 * dma::Shape<K, M, NE>::WAVES)) void k_encode_hash_dma(const GfApplyParams p,
                                                                                       const HashParams h) {
     using namespace dma;
@@ -1020,7 +1021,7 @@ __global__ __launch_bounds__((64 * dma::Shape<K, M, NE>::WAVES)) void k_encode_h
     if (wave < (uint32_t)NE) {
         if (p.byte_begin & 2) __builtin_amdgcn_s_setprio(2);  // RSG_ENC_PRIO A/B knob
         const uint32_t g = wave % 2;
-        if constexpr (NE == 2) encoder_net<K, M>(p, n, steps, s0, g, ring, prow);
+        if constexpr (NE == 2) encoder_net<K, M, NT>(p, n, steps, s0, g, ring, prow);
         else if (wave < 2) encoder<K, M, 0>(p, n, steps, s0, g, ring, prow);
         else encoder<K, M, 1>(p, n, steps, s0, g, ring, prow);
         return;
@@ -1074,7 +1075,7 @@ __global__ __launch_bounds__((64 * dma::Shape<K, M, NE>::WAVES)) void k_encode_h
                 __builtin_amdgcn_global_load_lds(
                     (const void*)src,
                     (__attribute__((address_space(3))) void*)(ring + (step % D) * L::DSLOT + (NDI * hw + k) * IP),
-                    16, 0, 0);
+                    16, 0, (NT & 1) ? 2 : 0);  // NT bit 0: non-temporal data loads
             }
         };
 #pragma unroll
@@ -1748,12 +1749,21 @@ static hipError_t launch_encode_hash_dma(GfApplyParams p, HashParams h, uint64_t
     p.units = (uint32_t)(shard_len / dma::CH);
     h.n = n_stripes;
     const uint64_t blocks = (n_stripes + dma::SPW - 1) / dma::SPW;
+    // Non-temporal data loads and parity stores (default 3): 1.30 -> 1.28 ms
+    // at n = 4096 (profiles/r02/ab_nt/); RSG_DMA_NT = bit 0 loads, bit 1
+    // stores, for A/B runs
+    static const int nt = [] {
+        const char* e = getenv("RSG_DMA_NT");
+        return e ? atoi(e) & 3 : 3;
+    }();
+    const dim3 grid((uint32_t)blocks), blk2(64 * dma::Shape<8, 4, 2>::WAVES);
     if (ew == 4)
-        hipLaunchKernelGGL((k_encode_hash_dma<8, 4, 4>), dim3((uint32_t)blocks),
-                           dim3(64 * dma::Shape<8, 4, 4>::WAVES), 0, stream, p, h);
-    else
-        hipLaunchKernelGGL((k_encode_hash_dma<8, 4, 2>), dim3((uint32_t)blocks),
-                           dim3(64 * dma::Shape<8, 4, 2>::WAVES), 0, stream, p, h);
+        hipLaunchKernelGGL((k_encode_hash_dma<8, 4, 4>), grid, dim3(64 * dma::Shape<8, 4, 4>::WAVES), 0, stream, p,
+                           h);
+    else if (nt == 1) hipLaunchKernelGGL((k_encode_hash_dma<8, 4, 2, 1>), grid, blk2, 0, stream, p, h);
+    else if (nt == 2) hipLaunchKernelGGL((k_encode_hash_dma<8, 4, 2, 2>), grid, blk2, 0, stream, p, h);
+    else if (nt == 3) hipLaunchKernelGGL((k_encode_hash_dma<8, 4, 2, 3>), grid, blk2, 0, stream, p, h);
+    else hipLaunchKernelGGL((k_encode_hash_dma<8, 4, 2>), grid, blk2, 0, stream, p, h);
     return hipGetLastError();
 }
 
