@@ -86,6 +86,14 @@ int rsg_device_count(int *count);
 int rsg_create(int device, rsg_ctx **out);
 void rsg_destroy(rsg_ctx *ctx);
 
+/* Measurement hook (no reference counterpart; bench.py): with timing on, the
+ * record engines (rsg_decode_records_dev, rsg_heal_records_dev) record HIP
+ * events around their kernel launches on the call's stream;
+ * rsg_last_kernel_ms returns the summed kernel time of the last such call
+ * (-1 if none was timed).  Off by default. */
+int rsg_set_kernel_timing(rsg_ctx *ctx, int on);
+int rsg_last_kernel_ms(rsg_ctx *ctx, float *ms);
+
 /* Encoding matrix ((k+m) x k, row-major) as reed_solomon_erasure::ReedSolomon::new
  * builds it (erasure.rs:448-470 cached_modern_reed_solomon).  Host only. */
 int rsg_matrix(int k, int m, uint8_t *out);

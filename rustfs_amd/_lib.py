@@ -55,7 +55,7 @@ EXPORTED = (
     "rsg_hash", "rsg_encode_batch_dev", "rsg_reconstruct_batch_dev", "rsg_verify_batch_dev",
     "rsg_hash_batch_dev", "rsg_sync", "rsg_encode_batch_host", "rsg_pin", "rsg_unpin",
     "rsg_decode_records_dev", "rsg_heal_records_dev", "rsg_bitrot_verify_dev",
-    "rsg_encode_batch_host_submit", "rsg_poll", "rsg_wait",
+    "rsg_encode_batch_host_submit", "rsg_poll", "rsg_wait", "rsg_set_kernel_timing", "rsg_last_kernel_ms",
 )
 
 
@@ -114,6 +114,8 @@ def load():
         L.rsg_bitrot_verify_dev.argtypes = [P, I, S, P, P, S, S, S, P, P]
         L.rsg_pin.argtypes = [P, S]
         L.rsg_unpin.argtypes = [P]
+        L.rsg_set_kernel_timing.argtypes = [P, I]
+        L.rsg_last_kernel_ms.argtypes = [P, ctypes.POINTER(ctypes.c_float)]
         _lib = L
         return L
 
@@ -122,8 +124,7 @@ def status_list(status, n: int) -> list:
     """Per-stripe status codes of a ctypes int array as a list, in one C-level
     pass (indexing the ctypes array element by element costs ~0.1 us each:
     0.4 ms per 4096-stripe call, a fifth of a GET call's kernel time)."""
-    import numpy as np
-    return np.frombuffer(status, dtype=np.int32, count=n).tolist() if n else []
+    return memoryview(status).cast("B").cast("i")[:n].tolist() if n else []
 
 
 def strerror(code: int) -> str:

@@ -1213,6 +1213,7 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_re
         const uint32_t m7 = vgpr_const(0x07070707u), m3 = vgpr_const(0x03030303u);
         // row of present file f for this stripe: instruction f*HS + e%HS, half e/HS
         const uint32_t roff = (e % HS) * IP + (e / HS) * CH + lane * 8u;
+        bool bad = false;  // this lane saw a surplus-parity mismatch
         lds_barrier();  // B(0)
 #pragma unroll 1
         for (uint32_t s = 0; s < steps; ++s) {
@@ -1243,7 +1244,6 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_re
                             __builtin_amdgcn_perm(t4.w, t4.z, s1b), __builtin_amdgcn_perm(t2, t2, s2b));
                 }
             }
-            bool bad = false;
 #pragma unroll
             for (int r = 0; r < RM; ++r) {
                 if ((uint32_t)r >= R) break;
@@ -1261,10 +1261,12 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_re
 #pragma unroll
                 for (int c = 0; c < C; ++c)
                     if ((cmask >> c) & 1u) st16_nt_half(ob + p.copy_off[c] + (uint64_t)s * CH, x[c]);
-                if (bad) p.ok_flags[stripe] = 0;
             }
             lds_barrier();  // B(s+1): done with slot s % D
         }
+        // the stripe's surplus verdict, written whole (no memset before the launch)
+        const bool any_bad = __builtin_amdgcn_ballot_w64(bad) != 0;
+        if (live && nst < R && lane == 0) p.ok_flags[stripe] = any_bad ? 0 : 1;
         return;
     }
     // ------------------------- DMA + verify-hash wave -------------------------
@@ -1314,11 +1316,13 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_re
         lds_barrier();  // B(s+1)
     }
     __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // the clamped tail DMA has landed before the wave ends
-    if (live) {  // verify before use (split_and_verify, bitrot.rs:227-247)
-        const uint8_t* rec0 = h.base[file] + (s0 + stripe_l) * h.stripe_stride;
-        const uint64_t d = hhq_digest(st, q);
-        if (d != ld64_any(rec0 - 32 + 8 * q)) h.flag_base[file][s0 + stripe_l] = 0;
-    }
+    // verify before use (split_and_verify, bitrot.rs:227-247): lane 0 of each
+    // live quad writes its record's flag whole (no memset before the launch)
+    const uint64_t d = hhq_digest(st, q);
+    bool mis = false;
+    if (live) mis = d != ld64_any(h.base[file] + (s0 + stripe_l) * h.stripe_stride - 32 + 8 * q);
+    const uint64_t bal = __builtin_amdgcn_ballot_w64(mis);
+    if (live && q == 0) h.flag_base[file][s0 + stripe_l] = ((bal >> lane) & 0xFull) ? 0 : 1;
 }
 
 // ---------------------------------------------------------------------------

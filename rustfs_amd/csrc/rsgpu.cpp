@@ -528,6 +528,35 @@ struct rsg_ctx {
         return RSG_OK;
     }
 
+    // Measurement hook (rsg_set_kernel_timing, bench.py): HIP event pairs
+    // around the record engines' kernel launches on the call's stream, summed
+    // after the call's last synchronisation (ctx->mu held).
+    bool timing = false;
+    std::vector<hipEvent_t> tev;
+    size_t tev_used = 0;
+    float last_kernel_ms = -1.f;
+
+    void tmark(hipStream_t s) {
+        if (!timing) return;
+        if (tev_used == tev.size()) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return;
+            tev.push_back(e);
+        }
+        (void)hipEventRecord(tev[tev_used++], s);
+    }
+    // after the stream has been synchronised
+    void tcollect() {
+        if (!timing) return;
+        float sum = 0.f;
+        for (size_t i = 0; i + 1 < tev_used; i += 2) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, tev[i], tev[i + 1]) == hipSuccess) sum += ms;
+        }
+        last_kernel_ms = tev_used >= 2 ? sum : -1.f;
+        tev_used = 0;
+    }
+
     int ensure_scratch(size_t bytes) {
         if (bytes <= scratch_cap) return RSG_OK;
         if (d_scratch) (void)hipFree(d_scratch);
@@ -714,6 +743,7 @@ void rsg_destroy(rsg_ctx* ctx) {
     }
     for (auto& j : ctx->jobs)
         for (hipEvent_t e : j.second.done) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ctx->tev) (void)hipEventDestroy(e);
     delete ctx;
 }
 
@@ -1143,10 +1173,14 @@ int verify_gather(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64_t n, co
     if (all_parity || (int)data_idx.size() < k) {
         // every stripe needs its parity (heal, or a lost data disk): all
         // present records of all stripes in one launch, data gathered
+        ctx->tmark(s);
         if ((st = launch_verify_group(all_idx, d_files, d_flags, k, shard_len, n, 0, n, key, d_out, s))) return st;
+        ctx->tmark(s);
         return flags_to_host(ctx, d_flags, (size_t)t * n, flags.data(), s);
     }
+    ctx->tmark(s);
     if ((st = launch_verify_group(data_idx, d_files, d_flags, k, shard_len, n, 0, n, key, d_out, s))) return st;
+    ctx->tmark(s);
     if ((st = flags_to_host(ctx, d_flags, (size_t)k * n, flags.data(), s))) return st;
     uint64_t lo = n, hi = 0;
     if (all_parity) {
@@ -1163,7 +1197,9 @@ int verify_gather(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64_t n, co
         }
     }
     if (lo >= hi || par_idx.empty()) return RSG_OK;
+    ctx->tmark(s);
     if ((st = launch_verify_group(par_idx, d_files, d_flags, k, shard_len, n, lo, hi, key, nullptr, s))) return st;
+    ctx->tmark(s);
     return flags_to_host(ctx, d_flags + (size_t)k * n, (size_t)m * n, flags.data() + (size_t)k * n, s);
 }
 
@@ -1309,7 +1345,6 @@ int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64
     int st;
     if ((st = ctx->ensure_scratch((size_t)(t + 1) * n))) return st;
     uint8_t* d_ok = ctx->d_scratch + (size_t)t * n;  // surplus-parity verdict per stripe
-    if ((st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
     auto cd = m > 0 ? get_codec(k, m) : nullptr;
     if (m > 0 && !cd) return RSG_ERR_INVALID_ARG;
     bool any_verify = false;
@@ -1415,23 +1450,26 @@ int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64
         for (int i : all_idx) one_pass = one_pass && (uintptr_t)(d_files[i] + 32) % 16 == 0;
         if (one_pass) {
             // RS(8,4): verify every present record, rebuild, gather and check
-            // the surplus parity in ONE pass (k_decode_records_dma)
-            if ((st = hip_status(hipMemsetAsync(d_flags, 0, (size_t)t * n, s)))) return st;
-            for (size_t a = 0; a < all_idx.size();) {
-                size_t b = a + 1;
-                while (b < all_idx.size() && all_idx[b] == all_idx[b - 1] + 1) ++b;
-                if ((st = hip_status(hipMemsetAsync(d_flags + (size_t)all_idx[a] * n, 1, (b - a) * n, s)))) return st;
-                a = b;
-            }
+            // the surplus parity in ONE pass (k_decode_records_dma); the kernel
+            // writes every present file's flags and, with surplus rows, every
+            // stripe's verdict whole (no memsets before it)
+            ctx->tmark(s);
             if ((st = launch_get_one_pass(*cd, present0, all_idx, d_files, d_flags, d_ok, k, shard_len, n, key,
                                           verify_surplus, d_out, any_verify, s)))
                 return st;
+            ctx->tmark(s);
+            if (!any_verify && (st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
             for (uint64_t x = 0; x < n; ++x) h_status[x] = RSG_OK;
         } else {
+            if ((st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
+            ctx->tmark(s);
             if ((st = rebuild_run(0, n, present0, true))) return st;
+            ctx->tmark(s);
             if ((st = hip_status(hipMemsetAsync(d_flags, 0, (size_t)t * n, s)))) return st;
+            ctx->tmark(s);
             if ((st = launch_verify_group(all_idx, d_files, d_flags, k, shard_len, n, 0, n, key, nullptr, s)))
                 return st;
+            ctx->tmark(s);
         }
         // the verified map and the surplus verdict (adjacent in scratch) in one
         // copy and one synchronisation; a second one only if a run is redone
@@ -1439,6 +1477,9 @@ int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64
         if ((st = hip_status(hipMemcpyAsync(ctx->h_flags, d_flags, (size_t)(t + 1) * n, hipMemcpyDeviceToHost, s))))
             return st;
         if ((st = hip_status(hipStreamSynchronize(s)))) return st;
+        if (one_pass)  // absent files' rows were never written on the device
+            for (int i = 0; i < t; ++i)
+                if (!d_files[i]) std::memset(ctx->h_flags + (size_t)i * n, 0, n);
         bool redone = false;
         if (!flags_match_pattern(ctx->h_flags, present0, n)) {
             flags.assign(ctx->h_flags, ctx->h_flags + (size_t)t * n);
@@ -1459,6 +1500,7 @@ int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64
         }
     } else {
         // verify the data records and gather them into d_out; parity where needed
+        if ((st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
         if ((st = verify_gather(ctx, k, m, shard_len, n, d_files, key, d_out, false, flags, s))) return st;
         st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) {
             return rebuild_run(s0, s1, present, false);
@@ -1493,7 +1535,29 @@ int rsg_decode_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t 
     }
     hipStream_t s = pick_stream(ctx, stream);
     std::lock_guard<std::mutex> g(ctx->mu);
-    return decode_records_locked(ctx, k, m, shard_len, n, d_files, key, verify_surplus != 0, d_out, h_status, s);
+    ctx->tev_used = 0;
+    st = decode_records_locked(ctx, k, m, shard_len, n, d_files, key, verify_surplus != 0, d_out, h_status, s);
+    if (!st) ctx->tcollect();  // every path returns with the stream synchronised
+    return st;
+}
+
+int rsg_set_kernel_timing(rsg_ctx* ctx, int on) {
+    int st = enter(ctx);
+    if (st) return st;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    ctx->timing = on != 0;
+    ctx->tev_used = 0;
+    ctx->last_kernel_ms = -1.f;
+    return RSG_OK;
+}
+
+int rsg_last_kernel_ms(rsg_ctx* ctx, float* ms) {
+    int st = enter(ctx);
+    if (st) return st;
+    if (!ms) return RSG_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    *ms = ctx->last_kernel_ms;
+    return RSG_OK;
 }
 
 // Heal (Erasure::heal, heal.rs:112-206) over n stripes of bitrot records.
@@ -1519,7 +1583,7 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
     if (!cd) return RSG_ERR_INVALID_ARG;
     uint8_t* d_flags = ctx->d_scratch;
     uint8_t* d_ok = ctx->d_scratch + (size_t)t * n;
-    if ((st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
+    ctx->tev_used = 0;
     bool any_verify = false;
     // Per run of stripes with one verified pattern, ONE pass over the
     // survivors (first k verified shards) writes every target's record body —
@@ -1598,27 +1662,33 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
         if (one_pass) {
             // RS(8,4): verify every source record, write every target record
             // (body + digest) and compare the surplus parity in ONE pass
-            if ((st = hip_status(hipMemsetAsync(d_flags, 0, (size_t)t * n, s)))) return st;
-            for (size_t a = 0; a < all_idx.size();) {
-                size_t b = a + 1;
-                while (b < all_idx.size() && all_idx[b] == all_idx[b - 1] + 1) ++b;
-                if ((st = hip_status(hipMemsetAsync(d_flags + (size_t)all_idx[a] * n, 1, (b - a) * n, s)))) return st;
-                a = b;
-            }
+            // (the kernel writes every source's flags and, with surplus rows,
+            // every stripe's verdict whole: no memsets before it)
+            ctx->tmark(s);
             if ((st = launch_heal_one_pass(*cd, present0, all_idx, tg_idx, d_files, d_targets, d_flags, d_ok, k,
                                            shard_len, n, key, any_verify, s)))
                 return st;
+            ctx->tmark(s);
+            if (!any_verify && (st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
             for (uint64_t x = 0; x < n; ++x) h_status[x] = RSG_OK;
         } else {
+            if ((st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
+            ctx->tmark(s);
             if ((st = heal_run(0, n, present0))) return st;
+            ctx->tmark(s);
             if ((st = hip_status(hipMemsetAsync(d_flags, 0, (size_t)t * n, s)))) return st;
+            ctx->tmark(s);
             if ((st = launch_verify_and_digest(all_idx, d_files, d_flags, d_targets, t, shard_len, n, key, s)))
                 return st;
+            ctx->tmark(s);
         }
         if ((st = ctx->ensure_host_flags((size_t)(t + 1) * n))) return st;
         if ((st = hip_status(hipMemcpyAsync(ctx->h_flags, d_flags, (size_t)(t + 1) * n, hipMemcpyDeviceToHost, s))))
             return st;
         if ((st = hip_status(hipStreamSynchronize(s)))) return st;
+        if (one_pass)  // absent files' rows were never written on the device
+            for (int i = 0; i < t; ++i)
+                if (!d_files[i]) std::memset(ctx->h_flags + (size_t)i * n, 0, n);
         std::vector<uint8_t> ok(ctx->h_flags + (size_t)t * n, ctx->h_flags + (size_t)(t + 1) * n);
         bool redone = false;
         if (!flags_match_pattern(ctx->h_flags, present0, n)) {
@@ -1641,6 +1711,7 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
     if (!done) {
         // verify every source record in place first (read quorum: k verified
         // shards per stripe), then the per-pattern GF passes, then the digests
+        if ((st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
         if ((st = verify_gather(ctx, k, m, shard_len, n, d_files, key, nullptr, true, flags, s))) return st;
         if ((st = for_each_pattern_run(t, n, flags, heal_run))) return st;
         if ((st = hash_targets(0, n))) return st;
@@ -1669,7 +1740,9 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
                 return st;
         s0 = s1;
     }
-    return hip_status(hipStreamSynchronize(s));
+    if ((st = hip_status(hipStreamSynchronize(s)))) return st;
+    ctx->tcollect();
+    return RSG_OK;
 }
 
 // Whole-shard-file verification (bitrot_verify, bitrot.rs:616-655) of n files.

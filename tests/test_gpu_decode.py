@@ -161,3 +161,31 @@ def test_decode_records_lost_disk_many_workgroups(gpu, oracle):
     ok = torch.ones(n, dtype=torch.bool, device="cuda")
     ok[1234] = False
     assert torch.equal(out[ok], want[ok])
+
+
+def test_kernel_timing_hook(gpu, oracle, engine_path):
+    """rsg_set_kernel_timing / rsg_last_kernel_ms (bench.py's measurement
+    hook): off by default (-1), a positive kernel time after a timed GET with
+    a lost disk and after an all-present GET, unchanged results."""
+    import ctypes
+    import torch
+    from rustfs_amd import _lib
+    k, m, S, n = 8, 4, 4096, 16
+    e, st, files = _records(torch, k, m, S, n, seed=77)
+    want = st[:, :k].reshape(n, k * S)
+    L, ctx = _lib.load(), _lib.context(0).handle
+    v = ctypes.c_float(0)
+    _lib.check(L.rsg_set_kernel_timing(ctx, 0))
+    e.decode_records_batch(files, S, n)
+    _lib.check(L.rsg_last_kernel_ms(ctx, ctypes.byref(v)))
+    assert v.value == -1.0
+    _lib.check(L.rsg_set_kernel_timing(ctx, 1))
+    try:
+        for lost in ((), (0, 3)):
+            fl = [None if i in lost else files[i] for i in range(k + m)]
+            out, status = e.decode_records_batch(fl, S, n)
+            assert status == [0] * n and torch.equal(out, want)
+            _lib.check(L.rsg_last_kernel_ms(ctx, ctypes.byref(v)))
+            assert v.value > 0, lost
+    finally:
+        _lib.check(L.rsg_set_kernel_timing(ctx, 0))
