@@ -886,8 +886,9 @@ __device__ __forceinline__ void fold(uint32_t (&acc)[RN][8], const uint32_t (&P)
     }
 }
 
-template <int K, int M, int NE = EW>
+template <int K, int M, int NE = EW, int SP = SPW>
 struct Shape {
+    static constexpr int SPW = SP, HS = SP / 2;       // stripes per workgroup, per DMA half
     static constexpr int NI = HS * K;                 // DMA instructions per step (1 KiB each)
     static constexpr uint32_t DSLOT = NI * IP;        // one step of all data rows
     static constexpr uint32_t PSLOT = SPW * M * PP;   // one step of all parity rows
@@ -955,11 +956,12 @@ __device__ __forceinline__ void encoder(const GfApplyParams& p, uint64_t n, uint
 // shard is bit-transposed once per group instead of once per row pair
 // (per group and step: 8 + 4 transposes + 239 XORs, against 2 x (8 + 2)
 // transposes + 504 XORs for two encoder() waves).
-template <int K, int M, int NT>
+template <int K, int M, int NT, int SP>
 __device__ __forceinline__ void encoder_net(const GfApplyParams& p, uint64_t n, uint32_t steps, uint64_t s0,
                                             uint32_t g, const uint8_t* ring, uint8_t* prow) {
     static_assert(K == 8 && M == 4, "the XOR network is RS(8,4)'s");
-    using L = Shape<K, M, 2>;
+    using L = Shape<K, M, SP / 4, SP>;
+    constexpr int SPW = L::SPW, HS = L::HS;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t m4 = vgpr_const(0x0f0f0f0fu), m2 = vgpr_const(0x33333333u), m1 = vgpr_const(0x55555555u);
     const uint32_t mys[4] = {2 * g, 2 * g + 1, 2 * g + HS, 2 * g + HS + 1};
@@ -1003,13 +1005,14 @@ __device__ __forceinline__ void encoder_net(const GfApplyParams& p, uint64_t n, 
 }
 }  // namespace dma
 
-template <int K, int M, int NE = dma::EW, int NT = 0>
-__global__ __launch_bounds__((64 * dma::Shape<K, M, NE>::WAVES)) void k_encode_hash_dma(const GfApplyParams p,
-                                                                                      const HashParams h) {
+template <int K, int M, int NE = dma::EW, int NT = 0, int SP = dma::SPW>
+__global__ __launch_bounds__((64 * dma::Shape<K, M, NE, SP>::WAVES)) void k_encode_hash_dma(const GfApplyParams p,
+                                                                                          const HashParams h) {
     using namespace dma;
     static_assert(K % 2 == 0 && M % 2 == 0 && K <= 8 && M <= 4 && M >= 2, "pairs of shards per wave");
-    static_assert(NE == 4 || NE == 2, "two encoder waves per stripe group, or one with the XOR network");
-    using L = Shape<K, M, NE>;
+    static_assert((NE == 4 && SP == 8) || NE == SP / 4, "two encoder waves per stripe group, or one with the XOR network");
+    using L = Shape<K, M, NE, SP>;
+    constexpr int SPW = L::SPW, HS = L::HS;
     __shared__ __attribute__((aligned(16))) uint8_t ring[D * L::DSLOT];
     __shared__ __attribute__((aligned(16))) uint8_t prow[NP * L::PSLOT];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u, q = lane & 3u;
@@ -1021,7 +1024,7 @@ __global__ __launch_bounds__((64 * dma::Shape<K, M, NE>::WAVES)) void k_encode_h
     if (wave < (uint32_t)NE) {
         if (p.byte_begin & 2) __builtin_amdgcn_s_setprio(2);  // RSG_ENC_PRIO A/B knob
         const uint32_t g = wave % 2;
-        if constexpr (NE == 2) encoder_net<K, M, NT>(p, n, steps, s0, g, ring, prow);
+        if constexpr (NE == SP / 4) encoder_net<K, M, NT, SP>(p, n, steps, s0, g, ring, prow);
         else if (wave < 2) encoder<K, M, 0>(p, n, steps, s0, g, ring, prow);
         else encoder<K, M, 1>(p, n, steps, s0, g, ring, prow);
         return;
@@ -1760,7 +1763,19 @@ static hipError_t launch_encode_hash_dma(GfApplyParams p, HashParams h, uint64_t
         const char* e = getenv("RSG_DMA_NT");
         return e ? atoi(e) & 3 : 3;
     }();
+    // RSG_DMA_SPW = 4 (A/B only): four stripes per workgroup, two workgroups
+    // per CU — measured slower (n = 4096: 1.39 vs 1.25 ms; 4 MiB stripes,
+    // n = 1024: 2.00 ms vs 1.70 ms for the ring kernel; profiles/r02/ab_spw/)
+    static const int spw = [] {
+        const char* e = getenv("RSG_DMA_SPW");
+        return e && atoi(e) == 4 ? 4 : 8;
+    }();
     const dim3 grid((uint32_t)blocks), blk2(64 * dma::Shape<8, 4, 2>::WAVES);
+    if (spw == 4 && ew != 4 && (n_stripes + 3) / 4 <= 0x7fffffffull) {
+        const dim3 g4((uint32_t)((n_stripes + 3) / 4)), b4(64 * dma::Shape<8, 4, 1, 4>::WAVES);
+        hipLaunchKernelGGL((k_encode_hash_dma<8, 4, 1, 3, 4>), g4, b4, 0, stream, p, h);
+        return hipGetLastError();
+    }
     if (ew == 4)
         hipLaunchKernelGGL((k_encode_hash_dma<8, 4, 4>), grid, dim3(64 * dma::Shape<8, 4, 4>::WAVES), 0, stream, p,
                            h);
