@@ -17,8 +17,6 @@ enum GfMode : uint32_t {
     // rows r >= n_store: COMPARE at out_base + s*cmp_stripe_stride + out_off[r]
     // (GET: rebuild missing data and check surplus parity in one pass)
     GF_MODE_STORE_COMPARE = 3,
-    // one-pass RS(8,4) GET/heal with syndrome-form GF waves (syn_* fields)
-    GF_MODE_SYNDROME = 4,
 };
 
 // Passed by value: lands in the kernel-argument segment (SGPR-loaded).
@@ -42,21 +40,7 @@ struct GfApplyParams {
     // shards are gathered by the same pass that rebuilds the missing ones)
     uint32_t copy_mask;
     uint64_t copy_off[kMaxC];
-    // one-pass RS(8,4) GET/heal in syndrome form (k_decode_records_dma SYN):
-    // LDS row offset (from a ring slot) of data shard c's / parity j's present
-    // file for stripe group 0, or kSynAbsent; syn_mask bit j: parity j's
-    // syndrome is a GF input (tab[r][8 + j]); row r adds V_j (syn_base[r] = j) or
-    // nothing (kSynAbsent), V_j = encode_j(present data) ^ parity j (present)
-    // or encode_j(present data) (absent)
-    uint32_t syn_drow[8], syn_prow[4];
-    uint32_t syn_mask;
-    uint32_t syn_base[4];
-    uint32_t syn_copy_mask;  // bit d: present data shard d copied to copy_off[8 + d] (GET)
 };
-constexpr uint32_t kSynAbsent = 0xffffffffu;
-// LDS bytes between present files' rows in the one-pass GET ring (4 DMA
-// instructions of 2 x 512 + 32 bytes per file and step: dma::IP, HS = 4)
-constexpr uint32_t kSynFileRow = 4u * (2u * 512u + 32u);
 
 constexpr int kMaxHashBases = 32;
 

@@ -1142,179 +1142,49 @@ static uint64_t dma_prio() {
     return v;
 }
 
-template <int NF, int G, int TH = 0, bool SYN = false>
+template <int NF, int G, int TH = 0>
 struct GetShape {
     static constexpr int SPW = G, HS = G / 2;             // stripes per workgroup, per DMA half
-    static constexpr int GW = SYN ? G / 4 : G;            // GF waves: per 4-stripe group, or per stripe
     static constexpr int NI = HS * NF;                    // DMA instructions per step
     static constexpr uint32_t DSLOT = NI * dma::IP;
     static constexpr int HW = (NI + 7) / 8;               // DMA/hash waves
     static constexpr int LAST = NI - 8 * (HW - 1);        // instructions of the last one
     static constexpr uint32_t TSLOT = SPW * (TH ? TH : 1) * dma::PP;  // one step of target rows
     static constexpr int TW = (SPW * TH + 15) / 16;       // target-hasher waves
-    static constexpr int WAVES = HW + GW + TW;
+    static constexpr int WAVES = HW + SPW + TW;
 };
 
-// Syndrome-form GF wave of the one-pass GET/heal (RS(8,4), SYN): stripe group
-// g = stripes {2g, 2g+1, 2g+HS, 2g+HS+1}, 8 B of each per lane (the
-// encoder_net tiling).  Per 512-byte step: the present data shards (absent
-// ones read as zeros) are bit-transposed and run through the RS(8,4) encode
-// network (rs84_xornet.h); V_j = encode_j ^ parity j where parity j is
-// present (its syndrome), encode_j where it is absent.  With the first e
-// present parities as the survivors beside the present data (the
-// reference's first-k-present rule), every output is a GF combination of
-// those e syndromes: a lost data shard d is plan_row(d) restricted to them,
-// a lost parity j (heal target) V_j ^ the same for j, and a surplus parity
-// is consistent iff V_j equals its combination — bit-identical to decoding
-// from the survivors (the present-data terms are exactly what the network
-// added).  Run-time tables cover only e <= 4 syndrome inputs instead of 8
-// survivors; the fixed part is the compile-time network.
-template <int HS, int SPW, int TH, int D, uint32_t DSLOT, uint32_t TSLOT>
-__device__ __forceinline__ void get_syn_wave(const GfApplyParams& p, uint64_t n, uint32_t steps, uint64_t s0,
-                                             uint32_t g, const uint8_t* ring, const uint8_t* zrow, const uint8_t* tabs,
-                                             uint8_t* trow) {
-    using dma::CH;
-    using dma::IP;
-    using dma::PP;
-    constexpr int RM = 4;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t m4 = vgpr_const(0x0f0f0f0fu), m2 = vgpr_const(0x33333333u), m1 = vgpr_const(0x55555555u);
-    const uint32_t m7 = vgpr_const(0x07070707u), m3 = vgpr_const(0x03030303u);
-    const uint32_t mys[4] = {2 * g, 2 * g + 1, 2 * g + HS, 2 * g + HS + 1};
-    bool live[4];
-    uint64_t obase[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        live[j] = s0 + mys[j] < n;  // wave-uniform
-        obase[j] = (live[j] ? s0 + mys[j] : 0) * p.out_stripe_stride + lane * 8u;
-    }
-    const uint32_t R = p.R, nst = p.n_store, cmask = p.syn_copy_mask, smask = p.syn_mask;
-    bool bad[4] = {false, false, false, false};
-    lds_barrier();  // B(0)
-#pragma unroll 1
-    for (uint32_t s = 0; s < steps; ++s) {
-        const uint8_t* slot = ring + (s % D) * DSLOT + 2 * g * IP + lane * 8u;
-        uint32_t P[64];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const uint32_t ro = p.syn_drow[c];  // wave-uniform
-            const uint8_t* row = ro == kSynAbsent ? zrow + lane * 8u : slot + ro;
-            const uint2 a0 = *(const uint2*)row, a1 = *(const uint2*)(row + IP);
-            const uint2 a2 = *(const uint2*)(row + CH), a3 = *(const uint2*)(row + IP + CH);
-            if ((cmask >> c) & 1u) {  // present data shard copied through (GET)
-                const uint2 a[4] = {a0, a1, a2, a3};
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (live[j]) st16_nt_half(p.out_base + obase[j] + p.copy_off[8 + c] + (uint64_t)s * CH, a[j]);
-            }
-            uint32_t w[8] = {a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y};
-            dma::transpose(w, m4, m2, m1);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) P[8 * c + j] = w[j];
-        }
-        uint32_t O[32];
-        xn::rs84_encode_planes(P, O);
-        uint32_t V[4][8];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) V[j][i] = O[8 * j + i];
-            dma::transpose(V[j], m4, m2, m1);
-            const uint32_t ro = p.syn_prow[j];
-            if (ro != kSynAbsent) {  // present parity: its syndrome
-                const uint8_t* row = slot + ro;
-                const uint2 a0 = *(const uint2*)row, a1 = *(const uint2*)(row + IP);
-                const uint2 a2 = *(const uint2*)(row + CH), a3 = *(const uint2*)(row + IP + CH);
-                V[j][0] ^= a0.x; V[j][1] ^= a0.y; V[j][2] ^= a1.x; V[j][3] ^= a1.y;
-                V[j][4] ^= a2.x; V[j][5] ^= a2.y; V[j][6] ^= a3.x; V[j][7] ^= a3.y;
-            }
-        }
-        uint32_t tz;  // opaque zero: table reads stay at their use
-        asm volatile("s_mov_b32 %0, 0" : "=s"(tz));
-        const uint8_t* tb = tabs + tz;
-#pragma unroll
-        for (int r = 0; r < RM; ++r) {
-            if ((uint32_t)r >= R) break;  // wave-uniform
-            uint32_t acc[8];
-            const uint32_t b = p.syn_base[r];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) acc[i] = 0u;
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (b == (uint32_t)j)
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) acc[i] = V[j][i];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if (!((smask >> j) & 1u)) continue;  // wave-uniform
-                const uint8_t* tp = tb + (j * RM + r) * 32;
-                const uint4 t4 = *(const uint4*)tp;
-                const uint32_t t2 = *(const uint32_t*)(tp + 16);
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const uint32_t x = V[j][i];
-                    acc[i] = x3(acc[i], __builtin_amdgcn_perm(t4.y, t4.x, x & m7),
-                                __builtin_amdgcn_perm(t4.w, t4.z, (x >> 3) & m7)) ^
-                             __builtin_amdgcn_perm(t2, t2, (x >> 6) & m3);
-                }
-            }
-            if ((uint32_t)r < nst) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint2 v = make_uint2(acc[2 * j], acc[2 * j + 1]);
-                    if (live[j]) st16_nt_half(p.out_base + obase[j] + p.out_off[r] + (uint64_t)s * CH, v);
-                    if constexpr (TH > 0)
-                        *(uint2*)(trow + (s & 1) * TSLOT + (r * SPW + mys[j]) * PP + lane * 8u) = v;
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) bad[j] |= (acc[2 * j] | acc[2 * j + 1]) != 0u;
-            }
-        }
-        lds_barrier();  // B(s+1): done with slot s % D
-    }
-    // each stripe's surplus verdict, written whole (no memset before the launch)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const bool any_bad = __builtin_amdgcn_ballot_w64(bad[j]) != 0;
-        if (live[j] && nst < R && lane == 0) p.ok_flags[s0 + mys[j]] = any_bad ? 0 : 1;
-    }
-}
-
-template <int NF, int G, int TH, bool SYN>
-__global__ __launch_bounds__((64 * GetShape<NF, G, TH, SYN>::WAVES)) void k_decode_records_dma(
-    const GfApplyParams p, const HashParams h) {
+template <int NF, int G, int TH>
+__global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_records_dma(const GfApplyParams p,
+                                                                                          const HashParams h) {
     using dma::CH;
     using dma::D;
     using dma::IP;
     using dma::read16;
     using dma::vmcnt_imm;
     using dma::PP;
-    using L = GetShape<NF, G, TH, SYN>;
+    using L = GetShape<NF, G, TH>;
     constexpr int SPW = L::SPW, HS = L::HS;
     constexpr int C = 8, RM = 4;
     __shared__ __attribute__((aligned(16))) uint8_t ring[D * L::DSLOT];
     __shared__ __attribute__((aligned(16))) uint8_t tabs[C * RM * 32];
     __shared__ __attribute__((aligned(16))) uint8_t trow[TH ? 2 * L::TSLOT : 16];
-    __shared__ __attribute__((aligned(16))) uint8_t zrow[SYN ? 2 * IP : 16];  // an absent data shard reads zeros
-    if constexpr (SYN)
-        for (uint32_t i = threadIdx.x; i < 2 * IP / 16; i += blockDim.x) *(uint4*)(zrow + 16 * i) = make_uint4(0, 0, 0, 0);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u, q = lane & 3u;
     const uint64_t n = h.n;
     const uint32_t steps = p.units;
     const uint64_t s0 = (uint64_t)blockIdx.x * SPW;
     const uint32_t ring_base = (uint32_t)(uintptr_t)ring;
     for (uint32_t i = threadIdx.x; i < (uint32_t)(C * RM); i += blockDim.x) {
-        const int c = i / RM + (SYN ? 8 : 0), r = i % RM;  // SYN: syndrome tables in columns 8..11
+        const int c = i / RM, r = i % RM;
         *(uint4*)(tabs + i * 32) = make_uint4(p.tab[r][c][0], p.tab[r][c][1], p.tab[r][c][2], p.tab[r][c][3]);
         *(uint32_t*)(tabs + i * 32 + 16) = p.tab[r][c][4];
     }
     // (the tables are published by B(0), which every wave passes before use)
 
-    if (TH && wave >= (uint32_t)(L::HW + L::GW)) {
+    if (TH && wave >= (uint32_t)(L::HW + SPW)) {
         // ------------- target hasher: quad j hashes target row stream -------------
         if (p.byte_begin & 1) __builtin_amdgcn_s_setprio(2);
-        const uint32_t pi = 16 * (wave - L::HW - L::GW) + (lane >> 2);  // r * SPW + stripe
+        const uint32_t pi = 16 * (wave - L::HW - SPW) + (lane >> 2);  // r * SPW + stripe
         const bool on = pi < (uint32_t)(SPW * TH);
         const uint32_t r = on ? pi / SPW : 0, e = pi % SPW;
         const bool live = on && s0 + e < n;
@@ -1335,12 +1205,7 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH, SYN>::WAVES)) void k_deco
         if (live) hhq_finish(st, p.out_base + (s0 + e) * p.out_stripe_stride + p.out_off[r] - 32, q);
         return;
     }
-    if (SYN && wave >= (uint32_t)L::HW) {
-        if (p.byte_begin & 2) __builtin_amdgcn_s_setprio(2);  // A/B knob (RSG_DMA_PRIO)
-        get_syn_wave<HS, SPW, TH, D, L::DSLOT, L::TSLOT>(p, n, steps, s0, wave - L::HW, ring, zrow, tabs, trow);
-        return;
-    }
-    if (!SYN && wave >= (uint32_t)L::HW) {
+    if (wave >= (uint32_t)L::HW) {
         // ------------------------- GF wave: one stripe -------------------------
         if (p.byte_begin & 2) __builtin_amdgcn_s_setprio(2);  // A/B knob (RSG_DMA_PRIO)
         const uint32_t e = wave - L::HW;
@@ -1933,15 +1798,8 @@ static int get_spw() {
 
 template <int NF, int G, int TH = 0>
 static void launch_get(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
-    if constexpr (G == 8) {
-        if (p.mode == GF_MODE_SYNDROME) {
-            hipLaunchKernelGGL((k_decode_records_dma<NF, G, TH, true>), dim3((uint32_t)blocks),
-                               dim3(64 * GetShape<NF, G, TH, true>::WAVES), 0, stream, p, h);
-            return;
-        }
-    }
-    hipLaunchKernelGGL((k_decode_records_dma<NF, G, TH, false>), dim3((uint32_t)blocks),
-                       dim3(64 * GetShape<NF, G, TH, false>::WAVES), 0, stream, p, h);
+    hipLaunchKernelGGL((k_decode_records_dma<NF, G, TH>), dim3((uint32_t)blocks),
+                       dim3(64 * GetShape<NF, G, TH>::WAVES), 0, stream, p, h);
 }
 
 bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len) {

@@ -645,7 +645,7 @@ uint8_t* pinned_view(const uint8_t* p, size_t len, int device) {
 bool lost_disk_fast_enabled() {
     static const bool on = [] {
         const char* e = std::getenv("RSG_LOST_DISK_FAST");
-        return e && e[0] == '1';  // measured slower: off by default
+        return !(e && e[0] == '0');
     }();
     return on;
 }
@@ -654,7 +654,7 @@ bool lost_disk_fast_enabled() {
 bool zero_copy_enabled() {
     static const bool on = [] {
         const char* e = std::getenv("RSG_ZERO_COPY");
-        return e && e[0] == '1';  // measured slower: off by default
+        return !(e && e[0] == '0');
     }();
     return on;
 }
@@ -1217,55 +1217,6 @@ bool get_dma_enabled(uint64_t n) {
     return n >= 1024;
 }
 
-// RSG_GET_SYN=0 keeps the survivor-table GF waves of the one-pass GET/heal
-// (A/B runs); read per call.
-bool get_syn_enabled() {
-    const char* e = std::getenv("RSG_GET_SYN");
-    return e && e[0] == '1';  // measured slower: off by default
-}
-
-// Syndrome form of a one-pass RS(8,4) launch (GF_MODE_SYNDROME,
-// k_decode_records_dma SYN): the GF waves encode the present data with the
-// compile-time network and take the syndromes of the present parities; row r
-// (shard row_shard[r]: a lost data shard, a heal target parity or a compared
-// surplus parity) is plan_row(row_shard[r]) restricted to the survivor
-// parities (the first e present parities) applied to their syndromes, plus
-// V_j for a parity row.  Same bytes as the survivor form (rs_kernels.hip
-// get_syn_wave derives it).
-void syndrome_params(const Codec& cd, const DecodePlan& plan, const std::vector<int>& files,
-                     const std::vector<int>& row_shard, rsg::GfApplyParams& p) {
-    const int k = cd.k;
-    for (int c = 0; c < 8; ++c) p.syn_drow[c] = rsg::kSynAbsent;
-    for (int j = 0; j < 4; ++j) p.syn_prow[j] = p.syn_base[j] = rsg::kSynAbsent;
-    for (size_t f = 0; f < files.size(); ++f) {
-        if (files[f] < k) p.syn_drow[files[f]] = (uint32_t)f * rsg::kSynFileRow;
-        else p.syn_prow[files[f] - k] = (uint32_t)f * rsg::kSynFileRow;
-    }
-    p.syn_mask = 0;
-    for (int c = 0; c < k; ++c)
-        if (plan.survivors[c] >= k) p.syn_mask |= 1u << (plan.survivors[c] - k);
-    // copy-through by data shard (the survivor form's copy_mask is by survivor position)
-    p.syn_copy_mask = 0;
-    for (int c = 0; c < k; ++c)
-        if ((p.copy_mask >> c) & 1u) {
-            const int d = plan.survivors[c];
-            p.syn_copy_mask |= 1u << d;
-            p.copy_off[8 + d] = p.copy_off[c];
-        }
-    std::vector<uint8_t> row(k);
-    for (size_t r = 0; r < row_shard.size(); ++r) {
-        const int x = row_shard[r];
-        plan_row(cd, plan, x, row.data());
-        // columns 8 + j (the survivor-form tables in columns 0..7 stay intact
-        // for a launch that takes the survivor-form kernel)
-        for (int j = 0; j < 4; ++j) coef_tables(0, p.tab[r][8 + j]);
-        for (int c = 0; c < k; ++c)
-            if (plan.survivors[c] >= k) coef_tables(row[c], p.tab[r][8 + plan.survivors[c] - k]);
-        p.syn_base[r] = x >= k ? (uint32_t)(x - k) : rsg::kSynAbsent;
-    }
-    p.mode = rsg::GF_MODE_SYNDROME;
-}
-
 // Launch k_decode_records_dma over all stripes for the erasure pattern
 // `present`: present files in ascending order, the first k are the
 // survivors (DecodePlan order); rows = the missing data shards, then (with
@@ -1280,7 +1231,6 @@ int launch_get_one_pass(Codec& cd, const std::vector<uint8_t>& present, const st
     for (int c = 0; c < k; ++c)
         if (plan->survivors[c] != files[c]) return RSG_ERR_INVALID_ARG;  // survivors = first k present
     std::vector<uint8_t> coef;
-    std::vector<int> row_shard;
     rsg::GfApplyParams p;
     std::memset(&p, 0, sizeof(p));
     int R = 0;
@@ -1288,7 +1238,6 @@ int launch_get_one_pass(Codec& cd, const std::vector<uint8_t>& present, const st
         if (present[i]) continue;
         coef.resize((size_t)(R + 1) * k);
         plan_row(cd, *plan, i, &coef[(size_t)R * k]);
-        row_shard.push_back(i);
         p.out_off[R++] = (uint64_t)i * shard_len;
     }
     const int n_store = R;
@@ -1297,7 +1246,6 @@ int launch_get_one_pass(Codec& cd, const std::vector<uint8_t>& present, const st
             if (R >= rsg::kMaxR) return RSG_ERR_UNSUPPORTED;
             coef.resize((size_t)(R + 1) * k);
             plan_row(cd, *plan, files[f], &coef[(size_t)R * k]);
-            row_shard.push_back(files[f]);
             ++R;
         }
     }
@@ -1317,7 +1265,6 @@ int launch_get_one_pass(Codec& cd, const std::vector<uint8_t>& present, const st
             p.copy_mask |= 1u << c;
             p.copy_off[c] = (uint64_t)files[c] * shard_len;
         }
-    if (get_syn_enabled()) syndrome_params(cd, *plan, files, row_shard, p);
     rsg::HashParams h;
     std::memset(&h, 0, sizeof(h));
     h.len = shard_len;
@@ -1349,13 +1296,11 @@ int launch_heal_one_pass(Codec& cd, const std::vector<uint8_t>& present, const s
     rsg::GfApplyParams p;
     std::memset(&p, 0, sizeof(p));
     std::vector<uint8_t> coef;
-    std::vector<int> row_shard;
     int R = 0;
     p.out_base = d_targets[targets[0]] + 32;
     for (int i : targets) {
         coef.resize((size_t)(R + 1) * k);
         plan_row(cd, *plan, i, &coef[(size_t)R * k]);
-        row_shard.push_back(i);
         p.out_off[R++] = (uint64_t)(uintptr_t)(d_targets[i] + 32) - (uint64_t)(uintptr_t)p.out_base;
     }
     const int n_store = R;
@@ -1363,7 +1308,6 @@ int launch_heal_one_pass(Codec& cd, const std::vector<uint8_t>& present, const s
         if (R >= 4) return RSG_ERR_UNSUPPORTED;
         coef.resize((size_t)(R + 1) * k);
         plan_row(cd, *plan, files[f], &coef[(size_t)R * k]);
-        row_shard.push_back(files[f]);
         ++R;
     }
     if (R > n_store) any_verify = true;
@@ -1373,7 +1317,6 @@ int launch_heal_one_pass(Codec& cd, const std::vector<uint8_t>& present, const s
     p.R = (uint32_t)R;
     p.n_store = (uint32_t)n_store;
     p.mode = rsg::GF_MODE_STORE_COMPARE;
-    if (get_syn_enabled()) syndrome_params(cd, *plan, files, row_shard, p);
     p.out_stripe_stride = rec;
     p.ok_flags = d_ok;
     rsg::HashParams h;
