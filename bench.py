@@ -30,8 +30,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--k", type=int, default=8)
-    ap.add_argument("--m", type=int, default=4)
+    # --data-shards / --parity-shards: the same as --k / --m, for launches
+    # through torch.distributed.run, whose parser takes "--m" for its own
+    # options (ambiguous abbreviation)
+    ap.add_argument("--k", "--data-shards", dest="k", type=int, default=8)
+    ap.add_argument("--m", "--parity-shards", dest="m", type=int, default=4)
     ap.add_argument("--stripe-bytes", type=int, default=1 << 20)
     ap.add_argument("--batch", type=int, default=4096, help="stripes per GPU (weak scaling)")
     ap.add_argument("--total-batch", type=int, default=0,
