@@ -48,3 +48,18 @@ def test_bitrot_shard_file_size():
     assert bitrot_shard_file_size(1025, 1024, h) == 1025 + 64
     assert bitrot_shard_file_size(524288, 524288, h) == 524288 + 32
     assert bitrot_shard_file_size(1000, 100, HashAlgorithm.NONE) == 1000
+
+
+def test_bench_geometry_flags(monkeypatch):
+    """bench.py takes the geometry as --k/--m or, through torchrun (whose
+    parser claims a bare --m), as --data-shards/--parity-shards."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--data-shards", "16", "--parity-shards", "4", "--total-batch", "8"])
+    a = bench.parse()
+    assert (a.k, a.m, a.total_batch) == (16, 4, 8)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--k", "6", "--m", "3"])
+    a = bench.parse()
+    assert (a.k, a.m) == (6, 3)
