@@ -37,7 +37,7 @@ import numpy as np
 from . import _lib
 from .bitrot import HashAlgorithm, bitrot_shard_file_size
 from .erasure import Erasure, calc_shard_size
-from .pipeline import DEFAULT_BATCH_BLOCKS, DEFAULT_INFLIGHT_BATCHES, get_stream, put_stream
+from .pipeline import DEFAULT_BATCH_BLOCKS, DEFAULT_INFLIGHT_BATCHES, GetStage, get_stream, put_stream
 
 
 class LocalErasureSet:
@@ -49,6 +49,7 @@ class LocalErasureSet:
         self.erasure = Erasure(data_shards, parity_shards, block_size, device=device)
         self.algo = algo
         self._put_stage = None  # page-locked PUT staging, reused across objects
+        self._get_stage = GetStage()  # page-locked GET staging + device buffers, reused across objects
         self.last_put: dict = {}  # put_stream's counts and producer/consumer clocks
 
     @property
@@ -159,7 +160,7 @@ class LocalErasureSet:
         size = self._meta(name)["size"]
         fds = self._open_shards(name, size)
         try:
-            yield from get_stream(self.erasure, fds, size, offset, length, self.algo, batch_blocks)
+            yield from get_stream(self.erasure, fds, size, offset, length, self.algo, batch_blocks, self._get_stage)
         finally:
             for fd in fds:
                 if fd is not None:

@@ -222,11 +222,12 @@ def block_geometry(offset: int, length: int, block_size: int, block: int):
 
 def get_stream(erasure: Erasure, fds: List[Optional[int]], total_length: int, offset: int = 0,
                length: Optional[int] = None, algo: HashAlgorithm = HashAlgorithm.HighwayHash256S,
-               batch_blocks: int = DEFAULT_BATCH_BLOCKS) -> Iterator[bytes]:
+               batch_blocks: int = DEFAULT_BATCH_BLOCKS, stage: Optional[GetStage] = None) -> Iterator[bytes]:
     """Yield bytes [offset, offset + length) of an object whose shard files
     are open at `fds` (None: disk unavailable), verifying every record
     before use and rebuilding missing data on the GPU.  Range errors follow
-    decode_inner (decode.rs:1716-1742)."""
+    decode_inner (decode.rs:1716-1742).  `stage`: reusable buffers
+    (GetStage), else allocated for this call."""
     if length is None:
         length = total_length - offset
     if offset < 0 or length < 0 or offset + length > total_length:
@@ -244,7 +245,7 @@ def get_stream(erasure: Erasure, fds: List[Optional[int]], total_length: int, of
     start, end = offset // bs, (offset + length - 1) // bs
     full_end = min(end, nfull - 1)  # last full block in the range
     if start <= full_end:
-        yield from _get_full(erasure, fds, start, full_end, offset, length, algo, batch_blocks)
+        yield from _get_full(erasure, fds, start, full_end, offset, length, algo, batch_blocks, stage)
     if end >= nfull:  # the short last block: host path, verify-before-use
         tl = total_length - nfull * bs
         s_blk = calc_shard_size(tl, k)
@@ -263,7 +264,40 @@ def get_stream(erasure: Erasure, fds: List[Optional[int]], total_length: int, of
         yield blk[o:o + n]
 
 
-def _get_full(erasure, fds, start, full_end, offset, length, algo, batch_blocks):
+class GetStage:
+    """Reusable buffers of the GET pipeline: two page-locked record stages
+    per shard file, the device record files and decode output, the
+    page-locked output and the read pool.  Page-locking megabytes costs more
+    than a whole 1 MiB-object GET (the loopback set's per-object calls), so a
+    LocalErasureSet keeps one; a call that finds it busy (another thread's
+    GET) allocates its own."""
+
+    def __init__(self):
+        self.lock = threading.Lock()
+        self.key = None
+        self.cnt = 0
+        self.pool = None
+
+    def ensure(self, t: int, k: int, S: int, bs: int, cnt_max: int, dev) -> None:
+        import torch
+        rec = 32 + S
+        key = (t, k, S, bs, str(dev))
+        if self.key != key or self.cnt < cnt_max:
+            self.stage = [[_pinned(cnt_max * rec) for _ in range(t)] for _ in range(2)]
+            self.files_dev = [torch.empty(cnt_max * rec, dtype=torch.uint8, device=dev) for _ in range(t)]
+            self.out = torch.empty((cnt_max, k * S), dtype=torch.uint8, device=dev)
+            self.host_out = _pinned((cnt_max, bs))
+            self.key, self.cnt = key, cnt_max
+        if self.pool is None:
+            self.pool = ThreadPoolExecutor(max_workers=min(t, 8))
+
+    def close(self) -> None:
+        if self.pool is not None:
+            self.pool.shutdown()
+            self.pool = None
+
+
+def _get_full(erasure, fds, start, full_end, offset, length, algo, batch_blocks, reuse=None):
     """Full blocks start..full_end: B-block batches, read-ahead of batch i+1
     into the other page-locked stage while batch i is decoded on the GPU."""
     import torch
@@ -272,15 +306,28 @@ def _get_full(erasure, fds, start, full_end, offset, length, algo, batch_blocks)
     rec = 32 + S
     dev = torch.device("cuda", erasure._device or 0)
     cnt_max = max(1, min(batch_blocks, full_end - start + 1))
-    stage = [[_pinned(cnt_max * rec) if fd is not None else None for fd in fds] for _ in range(2)]
-    files_dev = [torch.empty(cnt_max * rec, dtype=torch.uint8, device=dev) if fd is not None else None
-                 for fd in fds]
-    out = torch.empty((cnt_max, k * S), dtype=torch.uint8, device=dev)
-    host_out = _pinned((cnt_max, bs))
+    own = reuse is None or not reuse.lock.acquire(blocking=False)
+    gs = GetStage() if own else reuse
+    if own:
+        gs.lock.acquire()
+    try:
+        gs.ensure(t, k, S, bs, cnt_max, dev)
+        yield from _get_batches(erasure, fds, start, full_end, offset, length, algo, cnt_max, gs)
+    finally:
+        gs.lock.release()
+        if own:
+            gs.close()
+
+
+def _get_batches(erasure, fds, start, full_end, offset, length, algo, cnt_max, gs):
+    import torch
+    k, t = erasure.data_shards, erasure.total_shard_count()
+    bs, S = erasure.block_size, erasure.shard_size()
+    rec = 32 + S
+    dev = torch.device("cuda", erasure._device or 0)
+    stage, files_dev, out, host_out, pool = gs.stage, gs.files_dev, gs.out, gs.host_out, gs.pool
     batches = [(b0, min(cnt_max, full_end + 1 - b0)) for b0 in range(start, full_end + 1, cnt_max)]
     got: dict = {}
-
-    pool = ThreadPoolExecutor(max_workers=min(t, 8))
 
     def fetch(j):  # one pread per shard file per batch, files in parallel; a failed read = shard missing
         b0, cnt = batches[j]
@@ -325,4 +372,3 @@ def _get_full(erasure, fds, start, full_end, offset, length, algo, batch_blocks)
                 yield host_out[b, o:o + n].tobytes()
     finally:
         th.join()
-        pool.shutdown()
