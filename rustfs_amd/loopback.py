@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import json
 import os
+import threading
 from typing import Iterator, List, Optional
 
 import numpy as np
@@ -37,7 +38,7 @@ import numpy as np
 from . import _lib
 from .bitrot import HashAlgorithm, bitrot_shard_file_size
 from .erasure import Erasure, calc_shard_size
-from .pipeline import DEFAULT_BATCH_BLOCKS, DEFAULT_INFLIGHT_BATCHES, GetStage, get_stream, put_stream
+from .pipeline import DEFAULT_BATCH_BLOCKS, DEFAULT_INFLIGHT_BATCHES, GetStage, PutStage, get_stream, put_stream
 
 
 class LocalErasureSet:
@@ -49,6 +50,7 @@ class LocalErasureSet:
         self.erasure = Erasure(data_shards, parity_shards, block_size, device=device)
         self.algo = algo
         self._put_stage = None  # page-locked PUT staging, reused across objects
+        self._stage_lock = threading.Lock()  # put_object's use of _put_stage
         self._get_stage = GetStage()  # page-locked GET staging + device buffers, reused across objects
         self.last_put: dict = {}  # put_stream's counts and producer/consumer clocks
 
@@ -71,26 +73,51 @@ class LocalErasureSet:
         S = e.shard_size()
         nfull = data.size // bs
         tail = data.size - nfull * bs
-        records: List[List[bytes]] = [[] for _ in range(t)]
-        if nfull:
-            st = np.zeros((nfull, t, S), dtype=np.uint8)
-            flat = st.reshape(nfull, t * S)
-            flat[:, :bs] = data[: nfull * bs].reshape(nfull, bs)  # zero-pad to k*S (erasure.rs:863)
-            dig = np.zeros((nfull, t, 32), dtype=np.uint8)
-            e.encode_batch_host(st, dig, algo=self.algo.value)
-            for b in range(nfull):
-                for i in range(t):
-                    records[i].append(dig[b, i].tobytes() + st[b, i].tobytes())
-        if tail:
-            shards = e.encode_data(data[nfull * bs:])
+        records: List[list] = [[] for _ in range(t)]  # buffers written with one writev per shard file
+        staged = bool(nfull) and self._stage_lock.acquire(blocking=False)
+        try:
+            if nfull:
+                if staged:
+                    # page-locked (n, k+m, S) stripes + digests reused across
+                    # objects (PutStage: the pad between a block's end and k*S
+                    # is never written, so it stays zero, erasure.rs:858-866)
+                    if self._put_stage is None or not self._put_stage.fits(1, nfull, t, S):
+                        self._put_stage = PutStage(1, nfull, t, S)
+                    st = self._put_stage.stripes[0][:nfull]
+                    dig = self._put_stage.digests[0][:nfull]
+                else:  # another thread's PUT holds the stage
+                    st = np.zeros((nfull, t, S), dtype=np.uint8)
+                    dig = np.zeros((nfull, t, 32), dtype=np.uint8)
+                st.reshape(nfull, t * S)[:, :bs] = data[: nfull * bs].reshape(nfull, bs)
+                e.encode_batch_host(st, dig, algo=self.algo.value)
+                for b in range(nfull):
+                    for i in range(t):
+                        records[i] += [dig[b, i], st[b, i]]
+            self._write_records(name, records, data[nfull * bs:] if tail else None)
+        finally:
+            if staged:
+                self._stage_lock.release()
+        return self._write_meta(name, int(data.size))
+
+    def _write_records(self, name: str, records: List[list], tail) -> None:
+        e, t = self.erasure, self.k + self.m
+        if tail is not None:
+            shards = e.encode_data(tail)
             for i in range(t):
-                records[i].append(self.algo.hash_encode(shards[i]) + shards[i])
+                records[i] += [self.algo.hash_encode(shards[i]), shards[i]]
         for i in range(t):
             os.makedirs(os.path.dirname(self._path(i, name)), exist_ok=True)
-            with open(self._path(i, name), "wb") as f:
-                for r in records[i]:
-                    f.write(r)
-        return self._write_meta(name, int(data.size))
+            fd = os.open(self._path(i, name), os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+            try:
+                for c0 in range(0, len(records[i]), 512):  # IOV_MAX is 1024 on Linux
+                    chunk = records[i][c0:c0 + 512]
+                    done = os.writev(fd, chunk)
+                    if done != sum(memoryview(r).nbytes for r in chunk):  # short write: finish plainly
+                        rest = b"".join(bytes(r) for r in chunk)[done:]
+                        while rest:
+                            rest = rest[os.write(fd, rest):]
+            finally:
+                os.close(fd)
 
     def put_object_stream(self, name: str, reader, size: int, batch_blocks: int = DEFAULT_BATCH_BLOCKS,
                           inflight_batches: int = DEFAULT_INFLIGHT_BATCHES, read_threads: int = 4) -> dict:
@@ -101,15 +128,20 @@ class LocalErasureSet:
         batch i-1.  Produces the same files as put_object."""
         e, t = self.erasure, self.k + self.m
         fds = []
+        staged = self._stage_lock.acquire(blocking=False)  # else another PUT holds the stage
         try:
             for i in range(t):
                 os.makedirs(os.path.dirname(self._path(i, name)), exist_ok=True)
                 fds.append(os.open(self._path(i, name), os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644))
-            info = put_stream(e, reader, size, fds, self.algo, batch_blocks, inflight_batches, self._put_stage,
-                              read_threads)
-            self._put_stage = info.pop("stage")
+            info = put_stream(e, reader, size, fds, self.algo, batch_blocks, inflight_batches,
+                              self._put_stage if staged else None, read_threads)
+            stage = info.pop("stage")
+            if staged:
+                self._put_stage = stage
             self.last_put = info
         finally:
+            if staged:
+                self._stage_lock.release()
             for fd in fds:
                 os.close(fd)
         return self._write_meta(name, size)
