@@ -143,3 +143,44 @@ def test_config5_geometry_full_batch_per_gpu(gpu, oracle):
     assert bool(e.verify_batch(st).all())
     del st
     torch.cuda.empty_cache()
+
+
+_VARIANT_SNIPPET = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, {root!r})
+from rustfs_amd import Erasure
+from oracle import oracle as O
+k, m, S, n = 8, 4, 4096, {n}
+g = torch.Generator(device="cuda").manual_seed(n)
+st = torch.zeros((n, k + m, S), dtype=torch.uint8, device="cuda")
+st[:, :k] = torch.randint(0, 256, (n, k, S), dtype=torch.uint8, device="cuda", generator=g)
+dig = torch.zeros((n, k + m, 32), dtype=torch.uint8, device="cuda")
+Erasure(k, m, k * S).encode_batch(st, dig)
+torch.cuda.synchronize()
+for s in sorted({{0, 1, 5, n // 2, n - 2, n - 1}}):
+    got = st[s].cpu().numpy(); ref = got.copy(); ref[k:] = 0
+    O.encode(k, m, ref)
+    assert np.array_equal(got[k:], ref[k:]), s
+    d = dig[s].cpu().numpy()
+    for i in range(k + m):
+        assert d[i].tobytes() == O.hh256s(ref[i]), (s, i)
+print("ok")
+"""
+
+
+@pytest.mark.parametrize("env", [{"RSG_DMA_SPW": "4"}, {"RSG_DMA_EW": "4"}, {"RSG_DMA_NT": "0"},
+                                 {"RSG_ENC_PRIO": "3"}])
+def test_dma_kernel_ab_variants(gpu, oracle, env):
+    """The fused DMA kernel's A/B knobs (read once per process, so each runs
+    in its own process): four stripes per workgroup, the two-wave encoder,
+    cached loads/stores, raised priorities — parity and digests vs the oracle
+    on a ragged batch (n = 2051) and a 4-aligned one."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for n in (2051, 2052):
+        r = subprocess.run([sys.executable, "-c", _VARIANT_SNIPPET.format(root=root, n=n)],
+                           env={**os.environ, **env, "RSG_FUSED_KIND": "dma"}, capture_output=True, text=True,
+                           timeout=150)
+        assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (env, n, r.stdout[-500:], r.stderr[-2000:])
