@@ -6,9 +6,20 @@ encode pass over the whole batch (one rsg_encode_batch_dev call).  value =
 payload (data) GiB/s over all ranks, the reference benches' convention
 (crates/ecstore/benches/erasure_benchmark.rs:112 Throughput::Bytes(data_size)).
 
-Multi-GPU: one process per GPU (torch.distributed.run), independent stripes,
-no data-path collective ("scaling": "weak"); a gloo barrier brackets the timed
-region and the elapsed time is the max over ranks.
+Multi-GPU: one process per GPU, independent stripes, no data-path collective
+("scaling": "weak"); a gloo barrier brackets the timed region and the elapsed
+time is the max over ranks.  `python bench.py --gpus N` starts the N rank
+processes itself (before anything touches the GPU) and relays rank 0's line;
+under torch.distributed.run the ranks come from the environment and must
+number exactly --gpus.  Ranks never share a device unless
+--allow-shared-device (a rehearsal on a smaller box) says so.
+
+Besides the headline encode, the line's extras time, in the same process:
+config 3 (reconstruct with 1-4 lost data shards), config 4 (RS(8,4) encode +
+fused HighwayHash-256 digests, the PUT path's kernel, encode.rs:601-628),
+config 5's per-GPU share (RS(16,4) encode, S = 65536, 8192 stripes) and the
+GET / heal / bitrot_verify engines — each with its kernel time, algorithmic
+bytes and roofline fraction.
 """
 from __future__ import annotations
 
@@ -25,7 +36,7 @@ GiB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -48,10 +59,69 @@ def parse():
     ap.add_argument("--no-engines", action="store_true", help="skip the GET / heal / bitrot_verify measurements")
     ap.add_argument("--warm-seconds", type=float, default=0.5,
                     help="keep warming (untimed) until the device has been busy this long (clock ramp)")
-    return ap.parse_args()
+    ap.add_argument("--allow-shared-device", action="store_true",
+                    help="rehearsal only: let ranks share GPUs when fewer are visible than ranks")
+    ap.add_argument("--no-config-extras", action="store_true",
+                    help="skip the config 4 (fused digests) and config 5 (RS(16,4)) encode extras")
+    return ap.parse_args(argv)
 
 
-def dist_init():
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(a, argv, script=None, devices=None) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes of this
+    script (rank r on device r), relay rank 0's JSON line, return the first
+    failing rank's exit code.  Nothing here touches the GPU: counting devices
+    with torch.cuda.device_count() does not initialise it on this image, and
+    the ranks are fresh child processes, not an exec of this one.  (`script`
+    and `devices` let the CPU tests drive the launcher with a stand-in rank.)"""
+    import subprocess
+    from rustfs_amd.dispatch import check_world, rank_plan
+    if devices is None:
+        import torch
+        devices = torch.cuda.device_count()
+    why = check_world(a.gpus, a.gpus, devices, a.allow_shared_device)
+    if why:
+        print(f"bench.py: {why}", file=sys.stderr, flush=True)
+        return 2
+    procs = []
+    script = script or os.path.abspath(__file__)
+    for r, env in enumerate(rank_plan(a.gpus, free_port(), os.environ)):
+        # rank 0's stdout is this process's (its JSON line); the others' go to stderr
+        procs.append(subprocess.Popen([sys.executable, "-u", script] + list(argv), env=env,
+                                      stdout=None if r == 0 else sys.stderr))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 1
+                    print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the others",
+                          file=sys.stderr, flush=True)
+                    for o in live:
+                        o.kill()
+            time.sleep(0.05)
+    finally:
+        for p in procs:  # exact PIDs this launcher started
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
+def dist_init(a):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -151,6 +221,80 @@ def cpu_baseline(k, m, S, stripes, threads):
                             f"(reference: ~110 us per 1 MiB block on one core, encode.rs:512)"}
 
 
+def random_stripes(dev, k, m, S, n, seed):
+    """n synthetic stripes in the a3 layout (n, k+m, S), data bytes uniform
+    random, resident in HBM."""
+    import torch
+    st = torch.empty((n, k + m, S), dtype=torch.uint8, device=dev)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    step = max(1, (384 << 20) // (k * S))
+    for s0 in range(0, n, step):
+        s1 = min(n, s0 + step)
+        st[s0:s1, :k] = torch.randint(0, 256, (s1 - s0, k, S), dtype=torch.uint8, device=dev, generator=g)
+    return st
+
+
+def time_encode(e, stripes, digests, stream, reps, warm=3):
+    """Average device time (ms) of one rsg_encode_batch_dev over `reps`
+    launches: HIP events on the launch stream around each."""
+    import torch
+    for _ in range(warm):
+        e.encode_batch(stripes, digests, stream=stream)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for s, t in ev:
+        s.record(stream)
+        e.encode_batch(stripes, digests, stream=stream)
+        t.record(stream)
+    torch.cuda.synchronize()
+    ms = [s.elapsed_time(t) for s, t in ev]
+    return sum(ms) / len(ms), min(ms)
+
+
+def encode_extra(name_workload, e, stripes, digests, k, m, S, n, stream, reps):
+    """One encode configuration priced like the headline: algorithmic bytes =
+    k*S read + m*S written per stripe (+ 32*(k+m) digest bytes with fused
+    digests), over the average launch time."""
+    avg, mn = time_encode(e, stripes, digests, stream, reps)
+    alg = n * (k + m) * S + (n * (k + m) * 32 if digests is not None else 0)
+    return {"workload": name_workload, "k": k, "m": m, "shard_bytes": S, "stripes": n,
+            "kernel_ms": round(avg, 4), "kernel_ms_min": round(mn, 4), "launches": reps,
+            "GiB_s_payload": round(n * k * S / (avg * 1e-3) / GiB, 2),
+            "alg_bytes": alg, "achieved_GB_s": round(alg / (avg * 1e-3) / 1e9, 1),
+            "frac": round(alg / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+def config_extras(a, e_main, stripes, k, m, dev, stream, rank):
+    """BASELINE configs 4 and 5 at their per-GPU sizes, timed beside the
+    headline so the driver's default run carries them."""
+    import torch
+    from rustfs_amd import Erasure
+    out = {}
+    reps = max(10, a.steps)
+    # config 4: RS(8,4) 1 MiB stripes, n = 4096, parity + all 12 HH256S
+    # digests in one pass (the PUT path's kernel, bitrot.rs:496-502)
+    n4, k4, m4 = 4096, 8, 4
+    S4 = -(-(1 << 20) // k4)
+    if (k, m, a.stripe_bytes, stripes.shape[0]) == (k4, m4, 1 << 20, n4):
+        st4, e4 = stripes, e_main
+    else:
+        st4, e4 = random_stripes(dev, k4, m4, S4, n4, 2000 + rank), Erasure(k4, m4, 1 << 20, device=dev.index)
+    dig = torch.empty((n4, k4 + m4, 32), dtype=torch.uint8, device=dev)
+    out["encode_fused_hh256s"] = encode_extra("RS(8,4) encode + fused HighwayHash-256S digests, 1 MiB stripes, "
+                                              "batch 4096 (config 4)", e4, st4, dig, k4, m4, S4, n4, stream, reps)
+    del dig, st4
+    # config 5, one GPU's share: RS(16,4), S = 65536, 8192 stripes
+    n5, k5, m5 = 8192, 16, 4
+    S5 = -(-(1 << 20) // k5)
+    st5 = random_stripes(dev, k5, m5, S5, n5, 3000 + rank)
+    e5 = Erasure(k5, m5, 1 << 20, device=dev.index)
+    out["encode_rs16_4"] = encode_extra("RS(16,4) encode, 1 MiB stripes, 8192 stripes per GPU (config 5)",
+                                        e5, st5, None, k5, m5, S5, n5, stream, reps)
+    del st5
+    torch.cuda.empty_cache()
+    return out
+
+
 def engine_extras(e, stripes, k, m, S, n, stream):
     """SURVEY §8(f) engines on the same device-resident batch, as BitrotWriter
     record files ([HH256S][S bytes] per block): GET all present, GET with two
@@ -239,15 +383,24 @@ def engine_extras(e, stripes, k, m, S, n, stream):
     return res
 
 
-def main():
-    a = parse()
-    rank, world, local = dist_init()
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return launch_ranks(a, argv)  # before anything touches the GPU
     import torch
-    from rustfs_amd import Erasure, RSG_RECONSTRUCT_MISSING, _lib
+    from rustfs_amd.dispatch import check_world, device_for_rank
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    why = check_world(a.gpus, world_env, torch.cuda.device_count(), a.allow_shared_device)
+    if why:
+        print(f"bench.py: {why}", file=sys.stderr, flush=True)
+        return 2
+    rank, world, local = dist_init(a)
+    from rustfs_amd import Erasure, RSG_RECONSTRUCT_MISSING, _lib  # noqa: F401
 
-    # one process per GPU; on a box with fewer GPUs than ranks (a rehearsal)
-    # ranks share devices round-robin
-    local = local % max(1, torch.cuda.device_count())
+    # one process per GPU: rank r on device LOCAL_RANK (shared only in a
+    # --allow-shared-device rehearsal)
+    local = device_for_rank(local, torch.cuda.device_count(), a.allow_shared_device)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     k, m = a.k, a.m
@@ -259,11 +412,7 @@ def main():
     e = Erasure(k, m, a.stripe_bytes, device=local)
 
     # synthetic stripes, a3 layout (n, k+m, S), data random, resident in HBM
-    stripes = torch.empty((n, k + m, S), dtype=torch.uint8, device=dev)
-    g = torch.Generator(device=dev).manual_seed(1000 + rank)
-    for s0 in range(0, n, 256):
-        s1 = min(n, s0 + 256)
-        stripes[s0:s1, :k] = torch.randint(0, 256, (s1 - s0, k, S), dtype=torch.uint8, device=dev, generator=g)
+    stripes = random_stripes(dev, k, m, S, n, 1000 + rank)
     digests = torch.empty((n, k + m, 32), dtype=torch.uint8, device=dev) if a.digests else None
     stream = torch.cuda.current_stream(dev)
 
@@ -300,11 +449,17 @@ def main():
     elapsed = max_over_ranks(elapsed, world)
     kern_ms = sorted(s.elapsed_time(t) for s, t in ev)
     avg_ms = sum(kern_ms) / len(kern_ms)
-    rank_ms = [avg_ms]
+    mine = {"rank": rank, "device": local, "pci_bus": None, "kernel_ms": avg_ms}
+    try:
+        mine["pci_bus"] = torch.cuda.get_device_properties(local).pci_bus_id
+    except Exception:
+        pass
+    ranks = [mine]
     if world > 1:
         import torch.distributed as dist
-        rank_ms = [None] * world
-        dist.all_gather_object(rank_ms, avg_ms)
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+    rank_ms = [r["kernel_ms"] for r in ranks]
 
     payload = n * k * S
     total_stripes = a.total_batch if a.total_batch else n * world
@@ -340,6 +495,8 @@ def main():
         extras["verify_all_ok_after_reconstruct"] = bool(ok.all().item())
         if not a.no_engines and world == 1 and not a.digests:
             extras["engines"] = engine_extras(e, stripes, k, m, S, n, stream)
+        if not a.no_config_extras and world == 1:
+            extras.update(config_extras(a, e, stripes, k, m, dev, stream, rank))
 
     traffic = None
     prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -379,7 +536,10 @@ def main():
                          "kernel_ms_avg": round(avg_ms, 4), "kernel_ms_min": round(kern_ms[0], 4),
                          "alg_bytes_per_launch": alg_bytes,
                          "per_rank_kernel_ms": [round(x, 4) for x in rank_ms],
-                         "per_rank_frac": [round(alg_bytes / (x * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) for x in rank_ms]},
+                         "per_rank_frac": [round(alg_bytes / (x * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) for x in rank_ms],
+                         "per_rank_device": [r["device"] for r in ranks],
+                         "per_rank_pci_bus": [r["pci_bus"] for r in ranks],
+                         "shared_device": len(set(r["device"] for r in ranks)) < world},
             "cpu_baseline": cpu,
             "extras": extras,
         }
@@ -387,7 +547,8 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

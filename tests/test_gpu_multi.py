@@ -86,3 +86,28 @@ def test_device_count_and_context_per_device(gpu):
     assert n >= 1
     h = ctypes.c_void_p()
     assert _lib.load().rsg_create(n, ctypes.byref(h)) == _lib.RSG_ERR_NO_DEVICE  # ordinal past the last device
+
+
+def test_bench_self_launch_two_ranks_rehearsal(gpu):
+    """`bench.py --gpus 2` starts its two ranks itself (no torch.distributed.run)
+    and reports n_gpus 2 with each rank's device; on a one-GPU box only as an
+    explicit --allow-shared-device rehearsal, which the line says it was."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--allow-shared-device", "--batch", "256",
+           "--steps", "2", "--warmup", "1", "--warm-seconds", "0", "--no-cpu-baseline", "--no-extras"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=150)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["total_stripes"] == 512
+    import torch
+    ndev = torch.cuda.device_count()
+    assert line["roofline"]["per_rank_device"] == [0, 1 % ndev]
+    assert line["roofline"]["shared_device"] == (ndev < 2)
+    assert len(line["roofline"]["per_rank_kernel_ms"]) == 2

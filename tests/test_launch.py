@@ -1,0 +1,98 @@
+"""CPU tests of bench.py's multi-GPU launch: `bench.py --gpus
+N` starts N rank processes itself, each bound to its own device, and refuses
+(non-zero, with a message) any run that would time fewer GPUs than it reports.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+import bench
+from rustfs_amd.dispatch import check_world, device_for_rank, rank_plan
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_rank_plan_env():
+    plans = rank_plan(4, 29555, {"PATH": "/bin", "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    assert len(plans) == 4
+    for r, env in enumerate(plans):
+        assert env["RANK"] == env["LOCAL_RANK"] == str(r)
+        assert env["WORLD_SIZE"] == env["LOCAL_WORLD_SIZE"] == "4"
+        assert env["MASTER_ADDR"] == "127.0.0.1" and env["MASTER_PORT"] == "29555"
+        assert env["PATH"] == "/bin" and env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    with pytest.raises(ValueError):
+        rank_plan(0, 1, {})
+
+
+def test_check_world_refusals():
+    assert check_world(8, 8, 8, False) is None
+    assert check_world(1, 1, 1, False) is None
+    assert "launched" in check_world(8, 1, 8, False)        # --gpus 8, one rank
+    assert "launched" in check_world(1, 2, 8, False)        # torchrun 2 ranks, --gpus 1
+    assert "only 1 are visible" in check_world(2, 2, 1, False)
+    assert check_world(2, 2, 1, True) is None               # explicit rehearsal
+    assert "no GPU" in check_world(1, 1, 0, True)
+
+
+def test_device_for_rank():
+    assert [device_for_rank(r, 8, False) for r in range(8)] == list(range(8))
+    assert [device_for_rank(r, 1, True) for r in range(3)] == [0, 0, 0]
+    with pytest.raises(ValueError):
+        device_for_rank(1, 1, False)
+
+
+STAND_IN = r'''
+import json, os, sys
+r = int(os.environ["RANK"])
+if "--fail-rank" in sys.argv and str(r) == sys.argv[sys.argv.index("--fail-rank") + 1]:
+    sys.exit(3)
+if r == 0:
+    print(json.dumps({"rank": r, "world": os.environ["WORLD_SIZE"], "local": os.environ["LOCAL_RANK"],
+                      "master": os.environ["MASTER_ADDR"], "argv": sys.argv[1:]}), flush=True)
+'''
+
+
+def test_launcher_relays_rank0_line(tmp_path, capfd):
+    script = tmp_path / "rank.py"
+    script.write_text(STAND_IN)
+    argv = ["--gpus", "3", "--steps", "2"]
+    a = bench.parse(argv)
+    assert bench.launch_ranks(a, argv, script=str(script), devices=3) == 0
+    out = capfd.readouterr().out.strip().splitlines()
+    assert len(out) == 1
+    line = json.loads(out[0])
+    assert line == {"rank": 0, "world": "3", "local": "0", "master": "127.0.0.1", "argv": argv}
+
+
+def test_launcher_propagates_rank_failure(tmp_path, capfd):
+    script = tmp_path / "rank.py"
+    script.write_text(STAND_IN)
+    argv = ["--gpus", "2"]
+    a = bench.parse(argv)
+    assert bench.launch_ranks(a, argv + ["--fail-rank", "1"], script=str(script), devices=2) == 3
+    assert "rank 1 exited with 3" in capfd.readouterr().err
+
+
+def test_launcher_refuses_too_few_devices(tmp_path, capfd):
+    script = tmp_path / "rank.py"
+    script.write_text(STAND_IN)
+    a = bench.parse(["--gpus", "8"])
+    assert bench.launch_ranks(a, ["--gpus", "8"], script=str(script), devices=1) == 2
+    assert "only 1 are visible" in capfd.readouterr().err
+
+
+def test_bench_refuses_without_gpu_or_matching_world():
+    """The real script, no GPU in this container: --gpus 2 must fail loudly
+    (not time one rank), and so must a torchrun-style world that differs
+    from --gpus.  Neither touches a device."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 2 and "no GPU visible" in p.stderr and p.stdout == ""
+    env.update(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 2 and "2 rank(s) were launched" in p.stderr and p.stdout == ""
