@@ -11,11 +11,15 @@
  * reed_solomon_erasure::galois_8::ReedSolomon used by rustfs and MinIO;
  * docs/architecture/erasure-coding.md:41-50).  Outputs are bit-exact with it.
  *
- * Threading: every function is thread-safe.  A context owns one device, a
- * stream and per-geometry coefficient caches; concurrent host-buffer calls on
- * one context are serialised internally (the reference calls encode from many
+ * Threading: every function is thread-safe.  A context owns one device and
+ * per-geometry coefficient caches.  Host-buffer calls (rsg_encode,
+ * rsg_reconstruct, rsg_verify, rsg_hash) run on one of the context's 8 lanes
+ * (own stream and device buffer), so up to 8 concurrent callers overlap and
+ * further ones wait for a free lane (the reference calls encode from many
  * tokio workers concurrently, encode.rs:511-526).  Device-batch calls are
- * asynchronous on the caller's stream.
+ * asynchronous on the caller's stream; the record engines (decode / heal /
+ * bitrot_verify) share the context's scratch and run one at a time.
+ * Host-batch tickets may be polled or waited on from several threads.
  *
  * Errors: functions return an rsg_status; rsg_strerror() gives the message
  * fragment the reference uses for the same condition (erasure.rs:87-121,
@@ -31,7 +35,7 @@
 extern "C" {
 #endif
 
-#define RSG_ABI_VERSION 3
+#define RSG_ABI_VERSION 4
 #define RSG_MAX_TOTAL_SHARDS 256 /* galois_8::Field::ORDER, erasure.rs:72 */
 #define RSG_DIGEST_BYTES 32      /* HighwayHash-256 */
 
@@ -93,6 +97,18 @@ void rsg_destroy(rsg_ctx *ctx);
  * (-1 if none was timed).  Off by default. */
 int rsg_set_kernel_timing(rsg_ctx *ctx, int on);
 int rsg_last_kernel_ms(rsg_ctx *ctx, float *ms);
+
+/* Record-engine path of rsg_decode_records_dev / rsg_heal_records_dev (no
+ * reference counterpart; tests and A/B runs).  AUTO (default): the one-pass
+ * kernel from 1024 stripes where the geometry has one, else the two-pass
+ * path; ONE_PASS / TWO_PASS force a path where the geometry allows it.  Both
+ * paths produce identical bytes and statuses. */
+typedef enum rsg_record_engine {
+    RSG_RECORD_ENGINE_AUTO = 0,
+    RSG_RECORD_ENGINE_ONE_PASS = 1,
+    RSG_RECORD_ENGINE_TWO_PASS = 2
+} rsg_record_engine;
+int rsg_set_record_engine(rsg_ctx *ctx, int engine);
 
 /* Encoding matrix ((k+m) x k, row-major) as reed_solomon_erasure::ReedSolomon::new
  * builds it (erasure.rs:448-470 cached_modern_reed_solomon).  Host only. */
@@ -171,7 +187,8 @@ int rsg_decode_records_dev(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t 
  * decode_data_and_parity, erasure.rs:917, per block).  Sources as in
  * rsg_decode_records_dev (d_files[i] == NULL: no reader; every record is
  * verified before use).  d_targets[i] != NULL marks shard i as a heal target
- * (a writer, not aliasing any source): it receives n BitrotWriter records
+ * (a writer; a target range overlapping any source or another target is
+ * RSG_ERR_INVALID_ARG): it receives n BitrotWriter records
  * [HH256S][shard_len bytes] (stride 32+shard_len) of the rebuilt shard i (data
  * shards as read/rebuilt, parity re-encoded), computed in one pass over the
  * survivors.  Every verified source parity is compared with the parity
@@ -221,8 +238,12 @@ int rsg_sync(rsg_ctx *ctx, void *stream);
  * must stay alive and untouched until the ticket completes.
  * rsg_poll sets *done = 1 (and releases the ticket) when the job has finished,
  * returning its status; rsg_wait blocks until then.  An unknown or already
- * released ticket is RSG_ERR_INVALID_ARG.  rsg_encode_batch_host = submit +
- * wait. */
+ * released ticket is RSG_ERR_INVALID_ARG.  Several threads may poll or wait
+ * on one ticket; all of them see it finish.  If submit returns an error, no
+ * ticket is issued and none of the job's copies is still in flight: the
+ * sub-batches it had already queued are drained before it returns, so the
+ * caller may reuse or free h_stripes / h_digests at once (their contents are
+ * then unspecified).  rsg_encode_batch_host = submit + wait. */
 int rsg_encode_batch_host(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t n, uint8_t *h_stripes,
                           size_t shard_pitch, size_t stripe_stride, uint8_t *h_digests, int algo);
 int rsg_encode_batch_host_submit(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t n, uint8_t *h_stripes,

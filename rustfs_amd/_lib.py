@@ -48,6 +48,10 @@ RSG_RECONSTRUCT_DATA = 0
 RSG_RECONSTRUCT_MISSING = 1
 RSG_RECONSTRUCT_REENCODE_PARITY = 2
 
+RSG_RECORD_ENGINE_AUTO = 0
+RSG_RECORD_ENGINE_ONE_PASS = 1
+RSG_RECORD_ENGINE_TWO_PASS = 2
+
 # Every symbol include/rsgpu.h declares (checked by tests/test_abi.py).
 EXPORTED = (
     "rsg_abi_version", "rsg_strerror", "rsg_device_count", "rsg_create", "rsg_destroy",
@@ -56,6 +60,7 @@ EXPORTED = (
     "rsg_hash_batch_dev", "rsg_sync", "rsg_encode_batch_host", "rsg_pin", "rsg_unpin",
     "rsg_decode_records_dev", "rsg_heal_records_dev", "rsg_bitrot_verify_dev",
     "rsg_encode_batch_host_submit", "rsg_poll", "rsg_wait", "rsg_set_kernel_timing", "rsg_last_kernel_ms",
+    "rsg_set_record_engine",
 )
 
 
@@ -116,6 +121,7 @@ def load():
         L.rsg_unpin.argtypes = [P]
         L.rsg_set_kernel_timing.argtypes = [P, I]
         L.rsg_last_kernel_ms.argtypes = [P, ctypes.POINTER(ctypes.c_float)]
+        L.rsg_set_record_engine.argtypes = [P, I]
         _lib = L
         return L
 

@@ -1,0 +1,336 @@
+// rs_decode.hip — the one-pass GET / heal kernel (k_decode_records_dma) and
+// its launchers, in its own translation unit so its instantiations (four
+// survivor counts x present-file counts x heal targets) compile in parallel
+// with rs_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include "rs_device.h"
+
+namespace rsg {
+
+// ---------------------------------------------------------------------------
+// One-pass degraded GET (rsg_decode_records_dev, a data disk lost) for
+// RS(k, m) with k in {2, 4, 8, 16} and m <= 4: every present record of G
+// stripes is verified, the missing data shards rebuilt from the first C = k
+// present (survivors), the present data shards copied through and the
+// surplus parity compared with its re-derived value — reading each present
+// record once.  The k_encode_hash_dma layout: NF present files, G/2 x NF
+// LDS-DMA instructions per 512-byte step (one shard of stripes i and i+G/2
+// each) into a 3-slot ring; ceil(G NF / 16) DMA/hash waves (8 instructions
+// each, 16 verify streams straight out of the ring) and G table-GF waves,
+// one per stripe (survivor rows from the ring: rebuilt rows stored to the
+// output, surplus rows compared against their ring rows, survivor data
+// copied to the output).  One barrier per step.  The host redoes the stripes
+// whose verify flags differ from the assumed pattern.  At most m <= 4 rows
+// (missing data + surplus parity, or heal targets + surplus) are ever needed.
+//   p: tab[r][c] over the C survivors (present files 0..C-1 of the launch),
+//      rows [0, n_store) rebuilt into out_base + s*out_stripe_stride +
+//      out_off[r], rows [n_store, R) compared with present file 8 + (r -
+//      n_store); copy_mask/copy_off: survivors copied to the output;
+//      ok_flags[s] cleared on a compare mismatch; units = S / 512.
+//   h: base[f] = body of record 0 of present file f, stripe_stride = record
+//      pitch, flag_base[f][s] cleared on a digest mismatch, key, n.
+// TH > 0 is the one-pass heal (rsg_heal_records_dev): the TH stored rows are
+// target record bodies (out_stripe_stride = record pitch, no copy-through);
+// the GF waves also write them into a double-buffered LDS row area, and
+// ceil(8 TH / 16) target-hasher waves hash them one step behind and write
+// each target record's digest header (BitrotWriter::write).
+// Issue priority of the wave roles in the DMA kernels (GfApplyParams::
+// wave_prio): kPrioHash raises the hash waves, kPrioGf the GF / encoder
+// waves.  Default kPrioGf: the GF waves of the one-pass GET/heal run ahead
+// of the latency-bound hash chains instead of queueing behind them (RS(8,4),
+// n = 4096: GET 2 lost 2.44 -> 2.18 ms, heal 1.92 -> 1.69 ms;
+// profiles/r02/ab_prio/).  Tuning::get_prio overrides it for A/B runs.
+static uint32_t dma_prio() { return (uint32_t)tuning().get_prio; }
+
+template <int NF, int G, int TH = 0>
+struct GetShape {
+    static constexpr int SPW = G, HS = G / 2;             // stripes per workgroup, per DMA half
+    static constexpr int NI = HS * NF;                    // DMA instructions per step
+    static constexpr uint32_t DSLOT = NI * dma::IP;
+    static constexpr int HW = (NI + 7) / 8;               // DMA/hash waves
+    static constexpr int LAST = NI - 8 * (HW - 1);        // instructions of the last one
+    static constexpr uint32_t TSLOT = SPW * (TH ? TH : 1) * dma::PP;  // one step of target rows
+    static constexpr int TW = (SPW * TH + 15) / 16;       // target-hasher waves
+    static constexpr int WAVES = HW + SPW + TW;
+};
+
+template <int C, int NF, int G, int TH>
+__global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_records_dma(const GfApplyParams p,
+                                                                                          const HashParams h) {
+    static_assert(C >= 1 && C <= kMaxC && NF >= C && NF <= C + 4 && TH <= 4 && NF + TH <= C + 4, "RS(C, <= 4)");
+    using dma::CH;
+    using dma::D;
+    using dma::IP;
+    using dma::read16;
+    using dma::vmcnt_imm;
+    using dma::PP;
+    using L = GetShape<NF, G, TH>;
+    constexpr int SPW = L::SPW, HS = L::HS;
+    constexpr int RM = 4;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[D * L::DSLOT];
+    __shared__ __attribute__((aligned(16))) uint8_t tabs[C * RM * 32];
+    __shared__ __attribute__((aligned(16))) uint8_t trow[TH ? 2 * L::TSLOT : 16];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u, q = lane & 3u;
+    const uint64_t n = h.n;
+    const uint32_t steps = p.units;
+    const uint64_t s0 = (uint64_t)blockIdx.x * SPW;
+    const uint32_t ring_base = (uint32_t)(uintptr_t)ring;
+    for (uint32_t i = threadIdx.x; i < (uint32_t)(C * RM); i += blockDim.x) {
+        const int c = i / RM, r = i % RM;
+        *(uint4*)(tabs + i * 32) = make_uint4(p.tab[r][c][0], p.tab[r][c][1], p.tab[r][c][2], p.tab[r][c][3]);
+        *(uint32_t*)(tabs + i * 32 + 16) = p.tab[r][c][4];
+    }
+    // (the tables are published by B(0), which every wave passes before use)
+
+    if (TH && wave >= (uint32_t)(L::HW + SPW)) {
+        // ------------- target hasher: quad j hashes target row stream -------------
+        if (p.wave_prio & kPrioHash) __builtin_amdgcn_s_setprio(2);
+        const uint32_t pi = 16 * (wave - L::HW - SPW) + (lane >> 2);  // r * SPW + stripe
+        const bool on = pi < (uint32_t)(SPW * TH);
+        const uint32_t r = on ? pi / SPW : 0, e = pi % SPW;
+        const bool live = on && s0 + e < n;
+        const uint32_t roff = (on ? pi : 0) * PP + 8 * q;
+        HHQuad st;
+        hhq_init(st, h.key, q);
+        lds_barrier();  // B(0)
+#pragma unroll 1
+        for (uint32_t s = 0; s <= steps; ++s) {
+            if (s > 0) {  // target rows of step s-1, published by B(s)
+                uint64_t w[16];
+                read16((uint32_t)(uintptr_t)trow + ((s - 1) & 1) * L::TSLOT + roff, w);
+#pragma unroll
+                for (int t = 0; t < 16; ++t) hhq_update(st, w[t]);
+            }
+            if (s < steps) lds_barrier();  // B(s+1)
+        }
+        if (live) hhq_finish(st, p.out_base + (s0 + e) * p.out_stripe_stride + p.out_off[r] - 32, q);
+        return;
+    }
+    if (wave >= (uint32_t)L::HW) {
+        // ------------------------- GF wave: one stripe -------------------------
+        if (p.wave_prio & kPrioGf) __builtin_amdgcn_s_setprio(2);
+        const uint32_t e = wave - L::HW;
+        const uint64_t stripe = s0 + e;
+        const bool live = stripe < n;
+        uint8_t* ob = p.out_base + (live ? stripe : 0) * p.out_stripe_stride + lane * 8u;
+        const uint32_t R = p.R, nst = p.n_store, cmask = p.copy_mask;
+        const uint32_t m7 = vgpr_const(0x07070707u), m3 = vgpr_const(0x03030303u);
+        // row of present file f for this stripe: instruction f*HS + e%HS, half e/HS
+        const uint32_t roff = (e % HS) * IP + (e / HS) * CH + lane * 8u;
+        bool bad = false;  // this lane saw a surplus-parity mismatch
+        lds_barrier();  // B(0)
+#pragma unroll 1
+        for (uint32_t s = 0; s < steps; ++s) {
+            const uint8_t* slot = ring + (s % D) * L::DSLOT + roff;
+            uint2 x[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) x[c] = *(const uint2*)(slot + c * HS * IP);
+            uint32_t tz;  // opaque zero: table reads stay at their use
+            asm volatile("s_mov_b32 %0, 0" : "=s"(tz));
+            const uint8_t* tb = tabs + tz;
+            uint32_t acc[RM][2], pend[RM][2];
+#pragma unroll
+            for (int r = 0; r < RM; ++r) acc[r][0] = acc[r][1] = pend[r][0] = pend[r][1] = 0u;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const uint32_t s0a = x[c].x & m7, s0b = x[c].y & m7;
+                const uint32_t s1a = (x[c].x >> 3) & m7, s1b = (x[c].y >> 3) & m7;
+                const uint32_t s2a = (x[c].x >> 6) & m3, s2b = (x[c].y >> 6) & m3;
+#pragma unroll
+                for (int r = 0; r < RM; ++r) {
+                    if ((uint32_t)r >= R) break;  // wave-uniform
+                    const uint8_t* tp = tb + (c * RM + r) * 32;
+                    const uint4 t4 = *(const uint4*)tp;
+                    const uint32_t t2 = *(const uint32_t*)(tp + 16);
+                    gf_fold(c & 1, acc[r][0], pend[r][0], __builtin_amdgcn_perm(t4.y, t4.x, s0a),
+                            __builtin_amdgcn_perm(t4.w, t4.z, s1a), __builtin_amdgcn_perm(t2, t2, s2a));
+                    gf_fold(c & 1, acc[r][1], pend[r][1], __builtin_amdgcn_perm(t4.y, t4.x, s0b),
+                            __builtin_amdgcn_perm(t4.w, t4.z, s1b), __builtin_amdgcn_perm(t2, t2, s2b));
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < RM; ++r) {
+                if ((uint32_t)r >= R) break;
+                const uint2 v = make_uint2(acc[r][0], acc[r][1]);
+                if ((uint32_t)r < nst) {
+                    if (live) st16_nt_half(ob + p.out_off[r] + (uint64_t)s * CH, v);
+                    if constexpr (TH > 0)
+                        *(uint2*)(trow + (s & 1) * L::TSLOT + (r * SPW + e) * PP + lane * 8u) = v;
+                } else {
+                    const uint2 o = *(const uint2*)(slot + (C + (r - nst)) * HS * IP);
+                    bad |= ((o.x ^ v.x) | (o.y ^ v.y)) != 0u;
+                }
+            }
+            if (live) {
+#pragma unroll
+                for (int c = 0; c < C; ++c)
+                    if ((cmask >> c) & 1u) st16_nt_half(ob + p.copy_off[c] + (uint64_t)s * CH, x[c]);
+            }
+            lds_barrier();  // B(s+1): done with slot s % D
+        }
+        // the stripe's surplus verdict, written whole (no memset before the launch)
+        const bool any_bad = __builtin_amdgcn_ballot_w64(bad) != 0;
+        if (live && nst < R && lane == 0) p.ok_flags[stripe] = any_bad ? 0 : 1;
+        return;
+    }
+    // ------------------------- DMA + verify-hash wave -------------------------
+    if (p.wave_prio & kPrioHash) __builtin_amdgcn_s_setprio(2);
+    const uint32_t hw = wave, j = lane >> 2;
+    const int ndi = (hw == (uint32_t)(L::HW - 1)) ? L::LAST : 8;  // instructions this wave owns
+    const uint32_t idx = 8 * hw + (j & 7u), half = j >> 3;
+    const bool quad_on = (int)(j & 7u) < ndi;
+    const uint32_t file = quad_on ? idx / HS : 0, stripe_l = (idx % HS) + HS * half;
+    const uint32_t roff = (quad_on ? idx : 0) * IP + half * CH + 8 * q;
+    const bool live = quad_on && s0 + stripe_l < n;
+    HHQuad st;
+    hhq_init(st, h.key, q);
+    uint64_t dsrc[HS];
+#pragma unroll
+    for (int i = 0; i < HS; ++i) {
+        const uint64_t sg = s0 + i + (lane >> 5) * HS;
+        dsrc[i] = (sg < n ? sg : 0) * h.stripe_stride + (lane & 31u) * 16u;
+    }
+    auto dma_step = [&](uint32_t step) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (k >= ndi) break;  // wave-uniform
+            const uint32_t ins = 8 * hw + k;
+            const uint8_t* src = h.base[ins / HS] + dsrc[k % HS] + (uint64_t)step * CH;
+            __builtin_amdgcn_global_load_lds(
+                (const void*)src, (__attribute__((address_space(3))) void*)(ring + (step % D) * L::DSLOT + ins * IP), 16,
+                0, 0);
+        }
+    };
+    auto wait_next = [&]() {  // DMA of the next step landed (D - 2 steps younger in flight)
+        if (ndi == 8) __builtin_amdgcn_s_waitcnt(vmcnt_imm((D - 2) * 8));
+        else __builtin_amdgcn_s_waitcnt(vmcnt_imm((D - 2) * L::LAST));
+    };
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d) dma_step(d < (int)steps ? d : steps - 1);
+    wait_next();  // DMA(0) landed
+    lds_barrier();  // B(0)
+#pragma unroll 1
+    for (uint32_t s = 0; s < steps; ++s) {
+        dma_step(s + D - 1 < steps ? s + D - 1 : steps - 1);  // into the slot step s-1 used
+        uint64_t w[16];
+        read16(ring_base + (s % D) * L::DSLOT + roff, w);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) hhq_update(st, w[t]);
+        wait_next();
+        lds_barrier();  // B(s+1)
+    }
+    __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // the clamped tail DMA has landed before the wave ends
+    // verify before use (split_and_verify, bitrot.rs:227-247): lane 0 of each
+    // live quad writes its record's flag whole (no memset before the launch)
+    const uint64_t d = hhq_digest(st, q);
+    bool mis = false;
+    if (live) mis = d != ld64_any(h.base[file] + (s0 + stripe_l) * h.stripe_stride - 32 + 8 * q);
+    const uint64_t bal = __builtin_amdgcn_ballot_w64(mis);
+    if (live && q == 0) h.flag_base[file][s0 + stripe_l] = ((bal >> lane) & 0xFull) ? 0 : 1;
+}
+
+// Stripes per workgroup of the one-pass GET/heal kernel for C survivors: 8
+// (one workgroup of 13 waves per CU at RS(8,4)) while the ring of 3 x G/2 x
+// NF KiB-rows fits the LDS, 4 for C = 16 (RS(16,4): up to 19 present files).
+// (Four stripes per workgroup at RS(8,4) — two workgroups of 7 waves per CU —
+// measured no faster, profiles/r02/ab_eng/.)
+constexpr int get_group(int C) { return C > 8 ? 4 : 8; }
+static_assert(dma::D * (get_group(16) / 2) * 19 * dma::IP + 16 * 4 * 32 + 2 * 4 * 4 * dma::PP <= 160 * 1024,
+              "RS(16,4) one-pass ring fits the LDS");
+static_assert(dma::D * (get_group(8) / 2) * 11 * dma::IP + 8 * 4 * 32 <= 160 * 1024, "RS(8,4) ring fits the LDS");
+
+template <int C, int NF, int G, int TH = 0>
+static void launch_get(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
+    hipLaunchKernelGGL((k_decode_records_dma<C, NF, G, TH>), dim3((uint32_t)blocks),
+                       dim3(64 * GetShape<NF, G, TH>::WAVES), 0, stream, p, h);
+}
+
+// nf present files -> the k_decode_records_dma<C, NF, G, TH> instantiation
+template <int C, int G, int TH, int NF>
+static bool launch_get_nf(int nf, uint64_t n_stripes, const GfApplyParams& p, const HashParams& h,
+                          hipStream_t stream) {
+    if constexpr (NF + (TH ? TH : 1) > C + 4) {
+        return false;
+    } else {
+        if (nf != NF) return launch_get_nf<C, G, TH, NF + 1>(nf, n_stripes, p, h, stream);
+        const uint64_t blocks = (n_stripes + G - 1) / G;
+        if (blocks > 0x7fffffffull) return false;
+        launch_get<C, NF, G, TH>(blocks, p, h, stream);
+        return true;
+    }
+}
+
+template <int C, int G>
+static bool launch_get_th(int nf, int th, uint64_t n_stripes, const GfApplyParams& p, const HashParams& h,
+                          hipStream_t stream) {
+    switch (th) {
+        case 0: return launch_get_nf<C, G, 0, C>(nf, n_stripes, p, h, stream);
+        case 1: return launch_get_nf<C, G, 1, C>(nf, n_stripes, p, h, stream);
+        case 2: return launch_get_nf<C, G, 2, C>(nf, n_stripes, p, h, stream);
+        case 3: return launch_get_nf<C, G, 3, C>(nf, n_stripes, p, h, stream);
+        case 4: return launch_get_nf<C, G, 4, C>(nf, n_stripes, p, h, stream);
+    }
+    return false;
+}
+
+static bool launch_get_any(int k, int nf, int th, uint64_t n_stripes, const GfApplyParams& p, const HashParams& h,
+                           hipStream_t stream) {
+    switch (k) {
+        case 2: return launch_get_th<2, get_group(2)>(nf, th, n_stripes, p, h, stream);
+        case 4: return launch_get_th<4, get_group(4)>(nf, th, n_stripes, p, h, stream);
+        case 8: return launch_get_th<8, get_group(8)>(nf, th, n_stripes, p, h, stream);
+        case 16: return launch_get_th<16, get_group(16)>(nf, th, n_stripes, p, h, stream);
+    }
+    return false;
+}
+
+// Geometries with a one-pass kernel: k in {2, 4, 8, 16} (1 MiB blocks give
+// whole 512-byte steps exactly for powers of two), m <= 4, whole steps.
+static bool one_pass_geometry(int k, int m, uint64_t shard_len) {
+    return (k == 2 || k == 4 || k == 8 || k == 16) && m >= 1 && m <= 4 && shard_len >= dma::CH &&
+           shard_len % dma::CH == 0 && shard_len / dma::CH <= 0xffffffffull;
+}
+
+bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len) {
+    return one_pass_geometry(k, m, shard_len) && nf >= k && nf < k + m;
+}
+
+bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len) {
+    return one_pass_geometry(k, m, shard_len) && nf >= k && targets >= 1 && nf + targets <= k + m;
+}
+
+static bool dma_records_aligned(const HashParams& h, int nf) {
+    for (int f = 0; f < nf; ++f)
+        if ((uintptr_t)h.base[f] % 16) return false;
+    return h.stripe_stride % 16 == 0;
+}
+
+hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, int nf, int targets,
+                                   uint64_t shard_len, uint64_t n_stripes, hipStream_t stream) {
+    p.wave_prio = dma_prio();
+    if (!heal_dma_supported(k, m, nf, targets, shard_len) || (int)p.C != k || n_stripes == 0 || p.R > 4 ||
+        p.n_store != (uint32_t)targets || p.copy_mask || !dma_records_aligned(h, nf) ||
+        p.out_stripe_stride != h.stripe_stride)
+        return hipErrorInvalidValue;
+    p.units = (uint32_t)(shard_len / dma::CH);
+    h.n = n_stripes;
+    if (!launch_get_any(k, nf, targets, n_stripes, p, h, stream)) return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int k, int m, int nf, uint64_t shard_len,
+                                     uint64_t n_stripes, hipStream_t stream) {
+    p.wave_prio = dma_prio();
+    if (!decode_dma_supported(k, m, nf, shard_len) || (int)p.C != k || n_stripes == 0 || p.R > 4 ||
+        p.n_store > p.R || !dma_records_aligned(h, nf))
+        return hipErrorInvalidValue;
+    p.units = (uint32_t)(shard_len / dma::CH);
+    h.n = n_stripes;
+    if (!launch_get_any(k, nf, 0, n_stripes, p, h, stream)) return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+}  // namespace rsg

@@ -19,6 +19,36 @@ enum GfMode : uint32_t {
     GF_MODE_STORE_COMPARE = 3,
 };
 
+// Launch-shape knobs for A/B measurements, resolved ONCE per process from
+// the environment (rsg::tuning(), first use: rsg_create) — never read per
+// call.  Production runs leave every variable unset and get the defaults
+// below, which are the measured-best shapes (DESIGN.md cites the A/B runs).
+struct Tuning {
+    bool fused = true;            // RSG_FUSED=0: encode, then a separate hash launch
+    bool lost_disk_fast = true;   // RSG_LOST_DISK_FAST=0: general GET/heal order
+    bool zero_copy = true;        // RSG_ZERO_COPY=0: stage pinned blocks through device memory
+    int vec_block = 64;           // RSG_VEC_BLOCK=256: 4-wave GF workgroups
+    int vec_occ = -1;             // RSG_VEC_OCC=<0..8>: waves per SIMD for every GF launch (-1: default rule)
+    bool rolled = false;          // RSG_ROLLED=1: rolled GF kernel for every C
+    bool hash_direct_copy = false;  // RSG_HASH_COPY=1: 8-byte copy stores in the GET gather
+    int hash_depth = 2;           // RSG_HASH_DEPTH=1..3: 8-packet batches in flight per lane
+    int fused_kind = 0;           // RSG_FUSED_KIND=packed|ring|dma (0: by batch size)
+    bool fused_spw1 = false;      // RSG_FUSED_SPW1=1: one stripe per packed workgroup
+    int enc_prio = 0;             // RSG_ENC_PRIO=<0..3>: wave priorities of the fused DMA kernel
+    int dma_ew = 2;               // RSG_DMA_EW=4: two encoder waves per stripe group
+    int dma_nt = 3;               // RSG_DMA_NT=<0..3>: non-temporal loads (bit 0) / stores (bit 1)
+    int dma_spw = 8;              // RSG_DMA_SPW=4: four stripes per fused DMA workgroup
+    int get_prio = 2;             // RSG_DMA_PRIO=<0..3>: wave priorities of the one-pass GET/heal
+    // fault injection (tests only): RSG_TEST_FAIL_SUBBATCH=<i> makes sub-batch
+    // i of every rsg_encode_batch_host_submit fail to enqueue (-1: never)
+    int test_fail_subbatch = -1;
+};
+const Tuning& tuning();
+
+// Wave-priority bits of the DMA kernels (GfApplyParams::wave_prio): bit 0
+// raises the hash waves (s_setprio 2), bit 1 the GF / encoder waves.
+constexpr uint32_t kPrioHash = 1, kPrioGf = 2;
+
 // Passed by value: lands in the kernel-argument segment (SGPR-loaded).
 struct GfApplyParams {
     const uint8_t* base;         // input stripe 0
@@ -40,6 +70,7 @@ struct GfApplyParams {
     // shards are gathered by the same pass that rebuilds the missing ones)
     uint32_t copy_mask;
     uint64_t copy_off[kMaxC];
+    uint32_t wave_prio;  // DMA kernels: kPrioHash | kPrioGf (set by the launcher)
 };
 
 constexpr int kMaxHashBases = 32;
@@ -83,16 +114,18 @@ hipError_t launch_hh256(const HashParams& p, hipStream_t stream);
 // digest output [n][C+R][32].  Requires shard_len % 512 == 0, C <= 16, R <= 4
 // and 16-B aligned shards.
 bool fused_supported(int C, int R, uint64_t shard_len);
-// One-pass degraded GET for RS(8,4) over nf (8..12) present record files
-// (k_decode_records_dma): false if the shape is not supported.
+// One-pass degraded GET (k_decode_records_dma) for RS(k, m), k in {2, 4, 8,
+// 16}, m <= 4, over nf (k..k+m-1) present record files: false if the shape
+// is not supported.
 bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len);
-hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int nf, uint64_t shard_len, uint64_t n_stripes,
-                                     hipStream_t stream);
-// One-pass heal for RS(8,4) (k_decode_records_dma with target hashing): nf
-// present source files, `targets` absent target files written with digests.
+hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int k, int m, int nf, uint64_t shard_len,
+                                     uint64_t n_stripes, hipStream_t stream);
+// One-pass heal (k_decode_records_dma with target hashing), same
+// geometries: nf present source files, `targets` absent target files
+// written with digests (nf + targets <= k + m).
 bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len);
-hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int nf, int targets, uint64_t shard_len,
-                                   uint64_t n_stripes, hipStream_t stream);
+hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, int nf, int targets,
+                                   uint64_t shard_len, uint64_t n_stripes, hipStream_t stream);
 hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                     hipStream_t stream);
 

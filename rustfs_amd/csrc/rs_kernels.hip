@@ -24,175 +24,12 @@
 #include <stdint.h>
 #include <stdlib.h>
 
-#include "rs_kernels.h"
+#include "rs_device.h"
 #include "gf_bitslice.h"
 
 namespace rsg {
 
-// ---------------------------------------------------------------------------
-// GF(2^8) matrix apply, vector path: 16-byte units, every shard 16-B aligned.
-// Block = 256 threads = 4 waves; thread t of block (stripe, chunk) handles unit
-// chunk*256 + t, so each wave's loads/stores are contiguous 1 KiB per shard
-// (global_load_dwordx4 / global_store_dwordx4).
-
-__device__ __forceinline__ uint32_t gf_mul_word(const uint32_t* t, uint32_t s0, uint32_t s1, uint32_t s2) {
-    return __builtin_amdgcn_perm(t[1], t[0], s0) ^ __builtin_amdgcn_perm(t[3], t[2], s1) ^
-           __builtin_amdgcn_perm(t[4], t[4], s2);
-}
-
-// acc ^= a ^ b ^ c for the three lookups of one word x coefficient, with the
-// gfx950 three-input XOR (v_bitop3_b32, truth table 0x96), which issues at the
-// full v_xor rate (2.3 SIMD cycles per wave64 op, tools/kbench/op_rates.hip).
-// Taking inputs in pairs folds the six lookups into the accumulator with three
-// ops instead of six v_xor: even input: acc = x3(acc, a, b), pend = c; odd
-// input: acc = x3(acc, pend, a), acc = x3(acc, b, c).
-__device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
 #include "rs84_xornet.h"  // generated (tools/gen_xornet.py); uses x3
-
-// odd: input index parity (a compile-time constant in the unrolled loops)
-__device__ __forceinline__ void gf_fold(bool odd, uint32_t& acc, uint32_t& pend, uint32_t a, uint32_t b, uint32_t c) {
-    if (odd) {
-        acc = x3(acc, pend, a);
-        acc = x3(acc, b, c);
-    } else {
-        acc = x3(acc, a, b);
-        pend = c;
-    }
-}
-
-// One 16-byte unit per thread and no loop (126 VGPRs for RS(8,4): 4 waves per
-// SIMD).  A per-thread unit loop pushed it to 130 VGPRs (3 waves per SIMD) and
-// ran ~8 % slower; 2 or 4 units with all loads issued first ran 12-60 % slower
-// (tools/kbench/encode_variants.hip).
-//
-// acc[r] ^= sum over inputs c in [C0, C0+CN) of tab[r][c] * x[c - C0]  (4 words)
-template <int C0, int CN, int R>
-__device__ __forceinline__ void gf_accumulate(const GfApplyParams& p, const uint4* x, uint32_t (&acc)[R][4]) {
-#pragma unroll
-    for (int i = 0; i < CN; ++i) {
-        const int c = C0 + i;
-        const uint32_t w[4] = {x[i].x, x[i].y, x[i].z, x[i].w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t s0 = w[q] & 0x07070707u;
-            const uint32_t s1 = (w[q] >> 3) & 0x07070707u;
-            const uint32_t s2 = (w[q] >> 6) & 0x03030303u;
-#pragma unroll
-            for (int r = 0; r < R; ++r) acc[r][q] ^= gf_mul_word(p.tab[r][c], s0, s1, s2);
-        }
-    }
-}
-
-// 16-byte accesses with no alignment promise: gfx950 runs HSA code in
-// unaligned-access mode, so these stay single global_load/store_dwordx4 and let
-// shards of any length (S = ceil(1 MiB / 6) = 174763, ceil(1 MiB / 12) = 87382)
-// take the vector path; only the S % 16 tail goes to the byte kernel.
-__device__ __forceinline__ uint4 ld16(const uint8_t* p) {
-    uint4 v;
-    __builtin_memcpy(&v, p, 16);
-    return v;
-}
-__device__ __forceinline__ void st16(uint8_t* p, const uint4& v) { __builtin_memcpy(p, &v, 16); }
-// Non-temporal 16-byte store at any alignment (unaligned-access mode): for
-// output that this pass never reads back (GET's gathered data).
-typedef uint32_t v4u_any __attribute__((ext_vector_type(4), aligned(1)));
-__device__ __forceinline__ void st16_nt_half(uint8_t* p, const uint2& v) {  // 8 bytes, non-temporal
-    typedef uint32_t v2u_any __attribute__((ext_vector_type(2), aligned(1)));
-    const v2u_any w = {v.x, v.y};
-    __builtin_nontemporal_store(w, (v2u_any*)p);
-}
-__device__ __forceinline__ void st16_nt(uint8_t* p, const uint4& v) {
-    const v4u_any w = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(w, (v4u_any*)p);
-}
-
-// Output row r of a launch: its effective mode and address.
-__device__ __forceinline__ uint8_t* gf_dst(const GfApplyParams& p, uint8_t* obase, uint64_t off, int r, uint32_t stripe,
-                                          uint32_t& mode) {
-    mode = p.mode;
-    if (mode == GF_MODE_STORE_COMPARE) {
-        mode = (uint32_t)r < p.n_store ? GF_MODE_STORE : GF_MODE_COMPARE;
-        if (mode == GF_MODE_COMPARE) return p.out_base + (uint64_t)stripe * p.cmp_stripe_stride + p.out_off[r] + off;
-    }
-    return obase + p.out_off[r] + off;
-}
-
-// The bytes an XOR / COMPARE row reads back, loaded together with the inputs
-// so their latency overlaps the arithmetic (STORE rows load nothing).
-template <int R>
-__device__ __forceinline__ void gf_preload(const GfApplyParams& p, uint8_t* obase, uint64_t off, uint32_t stripe,
-                                           uint4 (&old)[R]) {
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        uint32_t mode;
-        const uint8_t* dst = gf_dst(p, obase, off, r, stripe, mode);
-        if (mode != GF_MODE_STORE) old[r] = ld16(dst);
-    }
-}
-
-template <int R>
-__device__ __forceinline__ void gf_store(const GfApplyParams& p, uint8_t* obase, uint64_t off,
-                                         const uint32_t (&acc)[R][4], uint32_t stripe, const uint4 (&old)[R]) {
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        uint32_t mode;
-        uint8_t* dst = gf_dst(p, obase, off, r, stripe, mode);
-        const uint4 v = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
-        const uint4 o = old[r];
-        if (mode == GF_MODE_STORE) {
-            st16(dst, v);
-        } else if (mode == GF_MODE_XOR) {
-            st16(dst, make_uint4(o.x ^ v.x, o.y ^ v.y, o.z ^ v.z, o.w ^ v.w));
-        } else {  // GF_MODE_COMPARE: clear the stripe's ok flag on mismatch
-            if ((o.x ^ v.x) | (o.y ^ v.y) | (o.z ^ v.z) | (o.w ^ v.w)) p.ok_flags[stripe] = 0;
-        }
-    }
-}
-
-// B threads per workgroup.  One-wave workgroups (B = 64) are the default:
-// consecutive workgroups still sweep one stripe's columns in order, but waves
-// are replaced one at a time instead of four together; RS(8,4) n = 4096 runs
-// 1.06 ms against 1.09-1.15 ms at B = 256 (tools/kbench/block_probe.hip,
-// profiles/r02/experiments/blk1_block_probe.txt).  RSG_VEC_BLOCK=256 selects
-// the 256-thread form for A/B runs.
-// The !PRE kernels' store: each row loads what it reads back (XOR /
-// COMPARE) only at its store.  The launcher uses them for plain STORE
-// launches, where this form compiles to the fastest measured encode (RS(8,4)
-// n = 4096: 1.065 ms; a store-only body with fewer registers ran 1.10-1.13 ms
-// at every occupancy, profiles/r02/ab_occ/).
-template <int R>
-__device__ __forceinline__ void gf_store_late(const GfApplyParams& p, uint8_t* obase, uint64_t off,
-                                              const uint32_t (&acc)[R][4], uint32_t stripe) {
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        uint32_t mode = p.mode;
-        uint8_t* dst = obase + p.out_off[r] + off;
-        if (mode == GF_MODE_STORE_COMPARE) {
-            mode = (uint32_t)r < p.n_store ? GF_MODE_STORE : GF_MODE_COMPARE;
-            if (mode == GF_MODE_COMPARE) dst = p.out_base + (uint64_t)stripe * p.cmp_stripe_stride + p.out_off[r] + off;
-        }
-        const uint4 v = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
-        if (mode == GF_MODE_STORE) {
-            st16(dst, v);
-        } else if (mode == GF_MODE_XOR) {
-            const uint4 o = ld16(dst);
-            st16(dst, make_uint4(o.x ^ v.x, o.y ^ v.y, o.z ^ v.z, o.w ^ v.w));
-        } else {  // GF_MODE_COMPARE: clear the stripe's ok flag on mismatch
-            const uint4 o = ld16(dst);
-            if ((o.x ^ v.x) | (o.y ^ v.y) | (o.z ^ v.z) | (o.w ^ v.w)) p.ok_flags[stripe] = 0;
-        }
-    }
-}
-
-template <int R>
-__device__ __forceinline__ void gf_store(const GfApplyParams& p, uint8_t* obase, uint64_t off,
-                                         const uint32_t (&acc)[R][4], uint32_t stripe) {
-    uint4 old[R];
-    gf_preload<R>(p, obase, off, stripe, old);
-    gf_store<R>(p, obase, off, acc, stripe, old);
-}
 
 // PRE: the launch has XOR / COMPARE rows, whose read-back operands are loaded
 // with the inputs, or copy-through inputs (a separate instantiation: the
@@ -332,135 +169,6 @@ __global__ __launch_bounds__(256) void k_gf_apply_byte(const GfApplyParams p) {
         else if (*dst != v) p.ok_flags[stripe] = 0;
     }
 }
-
-// ---------------------------------------------------------------------------
-// HighwayHash-256 (public spec; the `highway` crate 1.3.0 behind
-// crates/utils/src/hash.rs:123-127).
-
-// 8-byte little-endian load at any alignment: one global_load_dwordx2 in
-// gfx950's unaligned-access mode (as ld16 below).
-__device__ __forceinline__ uint64_t ld64_any(const uint8_t* p) {
-    uint64_t v;
-    __builtin_memcpy(&v, p, 8);
-    return v;
-}
-
-
-// ---------------------------------------------------------------------------
-// HighwayHash-256, lane-parallel: one message per 4-lane quad, lane q holds
-// u64 lane q of v0/v1/mul0/mul1 (8 VGPRs).  The mul/add half of Update is
-// lane-local; ZipperMergeAndAdd mixes lanes (0,1) and (2,3): it needs only the
-// partner's high dword (one DPP quad_perm move) and is three v_perm_b32 with
-// per-lane-parity selectors (derived in DESIGN.md §HighwayHash):
-//   low  dword = (own.b3, other.b4, own.b2, own.b5)                 both parities
-//   high dword = (other.b6, own.b1, other.b7, own.b0)  even lane  (add0)
-//              = (own.b1, other.b6, own.b0, other.b7)  odd lane   (add1)
-
-struct HHQuad {
-    uint64_t v0, v1, mul0, mul1;
-    uint32_t sel_hi;  // per-lane high-dword selector
-};
-
-__device__ __forceinline__ uint32_t quad_swap_pairs(uint32_t x) {  // lane q <- lane q^1
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-}
-__device__ __forceinline__ uint32_t quad_swap_halves(uint32_t x) {  // lane q <- lane q^2
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-}
-
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
-// Built as a 2-dword vector so the two v_perm results land in one register
-// pair and the following 64-bit add is a single v_lshl_add_u64 (building it
-// with shifts/ors cost an extra v_mov and add per zipper).
-__device__ __forceinline__ uint64_t hh_zip(uint64_t x, uint32_t sel_hi) {
-    const u32x2 xv = __builtin_bit_cast(u32x2, x);
-    const uint32_t other_hi = quad_swap_pairs(xv.y);
-    const uint32_t t = __builtin_amdgcn_perm(xv.y, xv.x, 0x05020C03u);  // own.b3, 0, own.b2, own.b5
-    u32x2 z;
-    z.x = __builtin_amdgcn_perm(other_hi, t, 0x03020400u);  // t.b0, other.b4, t.b2, t.b3
-    z.y = __builtin_amdgcn_perm(other_hi, xv.x, sel_hi);
-    return __builtin_bit_cast(uint64_t, z);
-}
-
-__device__ __forceinline__ void hhq_init(HHQuad& s, const uint64_t* key, uint32_t q) {
-    const uint64_t i0[4] = {0xdbe6d5d5fe4cce2full, 0xa4093822299f31d0ull, 0x13198a2e03707344ull,
-                            0x243f6a8885a308d3ull};
-    const uint64_t i1[4] = {0x3bd39e10cb0ef593ull, 0xc0acf169b5f18a8cull, 0xbe5466cf34e90c6cull,
-                            0x452821e638d01377ull};
-    uint64_t kq = key[0], m0 = i0[0], m1 = i1[0];
-    if (q == 1) { kq = key[1]; m0 = i0[1]; m1 = i1[1]; }
-    if (q == 2) { kq = key[2]; m0 = i0[2]; m1 = i1[2]; }
-    if (q == 3) { kq = key[3]; m0 = i0[3]; m1 = i1[3]; }
-    s.mul0 = m0;
-    s.mul1 = m1;
-    s.v0 = m0 ^ kq;
-    s.v1 = m1 ^ ((kq >> 32) | (kq << 32));
-    s.sel_hi = (q & 1) ? 0x07000601u : 0x00070106u;
-}
-
-__device__ __forceinline__ void hhq_update(HHQuad& s, uint64_t a) {
-    s.v1 += s.mul0 + a;
-    s.mul0 ^= (uint64_t)(uint32_t)s.v1 * (s.v0 >> 32);
-    s.v0 += s.mul1;
-    s.mul1 ^= (uint64_t)(uint32_t)s.v0 * (s.v1 >> 32);
-    s.v0 += hh_zip(s.v1, s.sel_hi);
-    s.v1 += hh_zip(s.v0, s.sel_hi);
-}
-
-// Remainder packet word q built from the message tail (size_mod32 = len % 32 > 0).
-__device__ __forceinline__ void hhq_remainder(HHQuad& s, const uint8_t* tail, uint32_t size_mod32, uint32_t q) {
-    s.v0 += ((uint64_t)size_mod32 << 32) + size_mod32;
-    uint32_t h0 = (uint32_t)s.v1, h1 = (uint32_t)(s.v1 >> 32);
-    h0 = (h0 << size_mod32) | (h0 >> (32u - size_mod32));
-    h1 = (h1 << size_mod32) | (h1 >> (32u - size_mod32));
-    s.v1 = (uint64_t)h0 | ((uint64_t)h1 << 32);
-    const uint32_t copy = size_mod32 & ~3u, mod4 = size_mod32 & 3u;
-    uint64_t w = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < 8; ++b) {
-        const uint32_t pos = 8 * q + b;
-        uint32_t v = 0;
-        if (pos < copy) v = tail[pos];
-        else if (size_mod32 & 16u) { if (pos >= 28) v = tail[size_mod32 - 32 + pos]; }
-        else if (mod4) {
-            if (pos == 16) v = tail[copy];
-            else if (pos == 17) v = tail[copy + (mod4 >> 1)];
-            else if (pos == 18) v = tail[copy + mod4 - 1];
-        }
-        w |= (uint64_t)v << (8 * b);
-    }
-    hhq_update(s, w);
-}
-
-// 10 x PermuteAndUpdate, ModularReduction; lane q writes digest bytes [8q, 8q+8).
-// Finalize; returns lane q's digest word (bytes [8q, 8q+8) little-endian).
-__device__ __forceinline__ uint64_t hhq_digest(HHQuad& s, uint32_t q) {
-#pragma unroll 1
-    for (int it = 0; it < 10; ++it) {
-        const uint32_t lo = quad_swap_halves((uint32_t)s.v0), hi = quad_swap_halves((uint32_t)(s.v0 >> 32));
-        hhq_update(s, (uint64_t)hi | ((uint64_t)lo << 32));  // rot32 of v0[q^2]
-    }
-    const uint64_t a_v1 = s.v1 + s.mul1, a_v0 = s.v0 + s.mul0;
-    const uint32_t p_lo = quad_swap_pairs((uint32_t)a_v1), p_hi = quad_swap_pairs((uint32_t)(a_v1 >> 32));
-    const uint64_t partner_v1 = (uint64_t)p_lo | ((uint64_t)p_hi << 32);
-    uint64_t h;
-    if (q & 1) {  // h[odd] from a3 = own v1+mul1, a2 = partner's, a1 = own v0+mul0
-        const uint64_t a3 = a_v1 & 0x3FFFFFFFFFFFFFFFull, a2 = partner_v1;
-        h = a_v0 ^ ((a3 << 1) | (a2 >> 63)) ^ ((a3 << 2) | (a2 >> 62));
-    } else {      // h[even] = a0 ^ (a2 << 1) ^ (a2 << 2), a2 = own v1+mul1
-        h = a_v0 ^ (a_v1 << 1) ^ (a_v1 << 2);
-    }
-    return h;
-}
-
-__device__ __forceinline__ void hhq_finish(HHQuad& s, uint8_t* out, uint32_t q) {
-    const uint64_t h = hhq_digest(s, q);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) out[8 * q + b] = (uint8_t)(h >> (8 * b));  // any alignment
-}
-
-__device__ __forceinline__ void st64_any(uint8_t* p, uint64_t v) { __builtin_memcpy(p, &v, 8); }
 
 // Plain / per-shard batch hash: quad j hashes message j (16 messages per wave).
 // Every lane issues its own 8-byte loads.  DEPTH = 1: one batch of 8 packets
@@ -618,20 +326,6 @@ __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
 // of the batch keep their waves in the barrier sequence with memory ops masked.
 constexpr uint32_t kFusedChunk = 512;                 // bytes per shard per step
 constexpr uint32_t kFusedPitch = kFusedChunk + 32;    // LDS row pitch: conflict-free ds_read_b64
-
-__device__ __forceinline__ void lds_barrier() {
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-}
-
-// A constant in a VGPR: VOP2 v_and with two VGPR operands issues at full rate
-// on gfx950, with a literal (constant bus) at half rate (tools/kbench/op_rates.hip).
-__device__ __forceinline__ uint32_t vgpr_const(uint32_t v) {
-    uint32_t r;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "i"(v));
-    return r;
-}
 
 constexpr int fused_spw_for(int T) {  // stripes per workgroup: fill hasher waves, cap LDS
     return (T % 16 == 0) ? 1 : (T % 8 == 0) ? 2 : (T % 4 == 0 || T <= 6) ? 4 : 2;
@@ -796,45 +490,8 @@ void k_encode_hash_fused(const GfApplyParams p,
 // One barrier per step.  The DMA writes LDS behind the compiler's back, so
 // its completion is awaited with counted vmcnt waits and the data rows are
 // read with asm ds_read_b64 (the compiler adds no vmcnt(0) for them).  Dead
-// stripes (past n) re-read stripe 0 and store stripe 0's own bytes.
+// stripes (past n) re-read stripe 0 and store nothing.
 namespace dma {
-constexpr uint32_t CH = 512;          // bytes per shard per step
-constexpr uint32_t IP = 2 * CH + 32;  // LDS pitch of one DMA instruction (rows of stripes i and i+4)
-constexpr uint32_t PP = CH + 32;      // parity row pitch
-constexpr int SPW = 8, HS = 4, D = 3, NP = 2, EW = 4;
-
-// s_waitcnt vmcnt(n) only (gfx9 encoding; n <= 63)
-constexpr uint32_t vmcnt_imm(int n) {
-    return 0x0F70u | ((uint32_t)(n > 63 ? 63 : n) & 15u) | (((uint32_t)(n > 63 ? 63 : n) >> 4) & 3u) << 14;
-}
-
-// 16 packets of one stream (8 B per lane, 32 B apart) from LDS, one asm.
-__device__ __forceinline__ void read16(uint32_t a, uint64_t (&w)[16]) {
-    asm volatile(
-        "ds_read_b64 %0, %16 offset:0\n\t"
-        "ds_read_b64 %1, %16 offset:32\n\t"
-        "ds_read_b64 %2, %16 offset:64\n\t"
-        "ds_read_b64 %3, %16 offset:96\n\t"
-        "ds_read_b64 %4, %16 offset:128\n\t"
-        "ds_read_b64 %5, %16 offset:160\n\t"
-        "ds_read_b64 %6, %16 offset:192\n\t"
-        "ds_read_b64 %7, %16 offset:224\n\t"
-        "ds_read_b64 %8, %16 offset:256\n\t"
-        "ds_read_b64 %9, %16 offset:288\n\t"
-        "ds_read_b64 %10, %16 offset:320\n\t"
-        "ds_read_b64 %11, %16 offset:352\n\t"
-        "ds_read_b64 %12, %16 offset:384\n\t"
-        "ds_read_b64 %13, %16 offset:416\n\t"
-        "ds_read_b64 %14, %16 offset:448\n\t"
-        "ds_read_b64 %15, %16 offset:480\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(w[4]), "=&v"(w[5]), "=&v"(w[6]), "=&v"(w[7]),
-          "=&v"(w[8]), "=&v"(w[9]), "=&v"(w[10]), "=&v"(w[11]), "=&v"(w[12]), "=&v"(w[13]), "=&v"(w[14]),
-          "=&v"(w[15])
-        : "v"(a)
-        : "memory");
-}
-
 __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
     uint32_t r;
     asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
@@ -910,8 +567,12 @@ __device__ __forceinline__ void encoder(const GfApplyParams& p, uint64_t n, uint
     const uint32_t mys[4] = {2 * g, 2 * g + 1, 2 * g + HS, 2 * g + HS + 1};
     uint8_t* const base = p.out_base;
     uint64_t pdst[4];
+    bool live[4];  // wave-uniform: a dead stripe (past n) computes stripe 0's rows and stores nothing
 #pragma unroll
-    for (int j = 0; j < 4; ++j) pdst[j] = (s0 + mys[j] < n ? s0 + mys[j] : 0) * p.stripe_stride + lane * 8u;
+    for (int j = 0; j < 4; ++j) {
+        live[j] = s0 + mys[j] < n;
+        pdst[j] = (live[j] ? s0 + mys[j] : 0) * p.stripe_stride + lane * 8u;
+    }
     lds_barrier();  // B(0): slot 0 landed
 #pragma unroll 1
     for (uint32_t s = 0; s < steps; ++s) {
@@ -940,9 +601,7 @@ __device__ __forceinline__ void encoder(const GfApplyParams& p, uint64_t n, uint
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const uint2 v = make_uint2(acc[r][2 * j], acc[r][2 * j + 1]);
-                // a dead stripe's lanes computed stripe 0's parity from stripe
-                // 0's data and store exactly the bytes stripe 0's lanes store
-                *(uint2*)(base + pdst[j] + p.out_off[R0 + r] + (uint64_t)s * CH) = v;
+                if (live[j]) *(uint2*)(base + pdst[j] + p.out_off[R0 + r] + (uint64_t)s * CH) = v;
                 *(uint2*)(prow + (s % NP) * L::PSLOT + ((R0 + r) * SPW + mys[j]) * PP + lane * 8u) = v;
             }
         }
@@ -967,8 +626,12 @@ __device__ __forceinline__ void encoder_net(const GfApplyParams& p, uint64_t n, 
     const uint32_t mys[4] = {2 * g, 2 * g + 1, 2 * g + HS, 2 * g + HS + 1};
     uint8_t* const base = p.out_base;
     uint64_t pdst[4];
+    bool live[4];  // wave-uniform: a dead stripe (past n) computes stripe 0's rows and stores nothing
 #pragma unroll
-    for (int j = 0; j < 4; ++j) pdst[j] = (s0 + mys[j] < n ? s0 + mys[j] : 0) * p.stripe_stride + lane * 8u;
+    for (int j = 0; j < 4; ++j) {
+        live[j] = s0 + mys[j] < n;
+        pdst[j] = (live[j] ? s0 + mys[j] : 0) * p.stripe_stride + lane * 8u;
+    }
     lds_barrier();  // B(0): slot 0 landed
 #pragma unroll 1
     for (uint32_t s = 0; s < steps; ++s) {
@@ -995,8 +658,10 @@ __device__ __forceinline__ void encoder_net(const GfApplyParams& p, uint64_t n, 
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const uint2 v = make_uint2(w[2 * j], w[2 * j + 1]);
-                if constexpr (NT & 2) st16_nt_half(base + pdst[j] + p.out_off[r] + (uint64_t)s * CH, v);
-                else *(uint2*)(base + pdst[j] + p.out_off[r] + (uint64_t)s * CH) = v;
+                if (live[j]) {
+                    if constexpr (NT & 2) st16_nt_half(base + pdst[j] + p.out_off[r] + (uint64_t)s * CH, v);
+                    else *(uint2*)(base + pdst[j] + p.out_off[r] + (uint64_t)s * CH) = v;
+                }
                 *(uint2*)(prow + (s % NP) * L::PSLOT + (r * SPW + mys[j]) * PP + lane * 8u) = v;
             }
         }
@@ -1022,7 +687,7 @@ __global__ __launch_bounds__((64 * dma::Shape<K, M, NE, SP>::WAVES)) void k_enco
     const uint32_t ring_base = (uint32_t)(uintptr_t)ring;
 
     if (wave < (uint32_t)NE) {
-        if (p.byte_begin & 2) __builtin_amdgcn_s_setprio(2);  // RSG_ENC_PRIO A/B knob
+        if (p.wave_prio & kPrioGf) __builtin_amdgcn_s_setprio(2);
         const uint32_t g = wave % 2;
         if constexpr (NE == SP / 4) encoder_net<K, M, NT, SP>(p, n, steps, s0, g, ring, prow);
         else if (wave < 2) encoder<K, M, 0>(p, n, steps, s0, g, ring, prow);
@@ -1030,7 +695,7 @@ __global__ __launch_bounds__((64 * dma::Shape<K, M, NE, SP>::WAVES)) void k_enco
         return;
     }
     // ---------------------------------- hashers ----------------------------------
-    if (p.byte_begin & 1) __builtin_amdgcn_s_setprio(2);
+    if (p.wave_prio & kPrioHash) __builtin_amdgcn_s_setprio(2);
     const uint32_t hw = wave - NE, j = lane >> 2;
     const bool is_data = hw < (uint32_t)L::DATA;
     constexpr int NDI = 8;  // DMA instructions a data-hasher wave owns
@@ -1101,231 +766,6 @@ __global__ __launch_bounds__((64 * dma::Shape<K, M, NE, SP>::WAVES)) void k_enco
         }
     }
     if (live) hhq_finish(st, h.out + ((s0 + stripe_l) * (K + M) + shard) * 32u, q);
-}
-
-// ---------------------------------------------------------------------------
-// One-pass degraded GET for RS(8,4) (rsg_decode_records_dev, a data disk
-// lost): every present record of 8 stripes is verified, the missing data
-// shards rebuilt from the first 8 present (survivors), the present data
-// shards copied through and the surplus parity compared with its re-derived
-// value — reading each present record once.  The k_encode_hash_dma layout:
-// NF present files, 4 x NF LDS-DMA instructions per 512-byte step (one shard
-// of stripes i and i+4 each) into a 3-slot ring; ceil(NF/2) DMA/hash waves
-// (8 instructions each, 16 verify streams straight out of the ring) and 8
-// table-GF waves, one per stripe (survivor rows from the ring: rebuilt rows
-// stored to the output, surplus rows compared against their ring rows,
-// survivor data copied to the output).  One barrier per step.  The host
-// redoes the stripes whose verify flags differ from the assumed pattern.
-//   p: tab[r][c] over the 8 survivors (present files 0..7 of the launch),
-//      rows [0, n_store) rebuilt into out_base + s*out_stripe_stride +
-//      out_off[r], rows [n_store, R) compared with present file 8 + (r -
-//      n_store); copy_mask/copy_off: survivors copied to the output;
-//      ok_flags[s] cleared on a compare mismatch; units = S / 512.
-//   h: base[f] = body of record 0 of present file f, stripe_stride = record
-//      pitch, flag_base[f][s] cleared on a digest mismatch, key, n.
-// TH > 0 is the one-pass heal (rsg_heal_records_dev): the TH stored rows are
-// target record bodies (out_stripe_stride = record pitch, no copy-through);
-// the GF waves also write them into a double-buffered LDS row area, and
-// ceil(8 TH / 16) target-hasher waves hash them one step behind and write
-// each target record's digest header (BitrotWriter::write).
-// Issue priority of the wave roles in the DMA kernels (passed in an unused
-// kernel-argument field): bit 0 raises the hash waves, bit 1 the GF /
-// encoder waves.  Default 2: the GF waves of the one-pass GET/heal run ahead
-// of the latency-bound hash chains instead of queueing behind them (RS(8,4),
-// n = 4096: GET 2 lost 2.44 -> 2.18 ms, heal 1.92 -> 1.69 ms;
-// profiles/r02/ab_prio/).  RSG_DMA_PRIO=<0..3> overrides for A/B runs.
-static uint64_t dma_prio() {
-    static const uint64_t v = [] {
-        const char* e = getenv("RSG_DMA_PRIO");
-        return e ? (uint64_t)(atoi(e) & 3) : 2ull;
-    }();
-    return v;
-}
-
-template <int NF, int G, int TH = 0>
-struct GetShape {
-    static constexpr int SPW = G, HS = G / 2;             // stripes per workgroup, per DMA half
-    static constexpr int NI = HS * NF;                    // DMA instructions per step
-    static constexpr uint32_t DSLOT = NI * dma::IP;
-    static constexpr int HW = (NI + 7) / 8;               // DMA/hash waves
-    static constexpr int LAST = NI - 8 * (HW - 1);        // instructions of the last one
-    static constexpr uint32_t TSLOT = SPW * (TH ? TH : 1) * dma::PP;  // one step of target rows
-    static constexpr int TW = (SPW * TH + 15) / 16;       // target-hasher waves
-    static constexpr int WAVES = HW + SPW + TW;
-};
-
-template <int NF, int G, int TH>
-__global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_records_dma(const GfApplyParams p,
-                                                                                          const HashParams h) {
-    using dma::CH;
-    using dma::D;
-    using dma::IP;
-    using dma::read16;
-    using dma::vmcnt_imm;
-    using dma::PP;
-    using L = GetShape<NF, G, TH>;
-    constexpr int SPW = L::SPW, HS = L::HS;
-    constexpr int C = 8, RM = 4;
-    __shared__ __attribute__((aligned(16))) uint8_t ring[D * L::DSLOT];
-    __shared__ __attribute__((aligned(16))) uint8_t tabs[C * RM * 32];
-    __shared__ __attribute__((aligned(16))) uint8_t trow[TH ? 2 * L::TSLOT : 16];
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u, q = lane & 3u;
-    const uint64_t n = h.n;
-    const uint32_t steps = p.units;
-    const uint64_t s0 = (uint64_t)blockIdx.x * SPW;
-    const uint32_t ring_base = (uint32_t)(uintptr_t)ring;
-    for (uint32_t i = threadIdx.x; i < (uint32_t)(C * RM); i += blockDim.x) {
-        const int c = i / RM, r = i % RM;
-        *(uint4*)(tabs + i * 32) = make_uint4(p.tab[r][c][0], p.tab[r][c][1], p.tab[r][c][2], p.tab[r][c][3]);
-        *(uint32_t*)(tabs + i * 32 + 16) = p.tab[r][c][4];
-    }
-    // (the tables are published by B(0), which every wave passes before use)
-
-    if (TH && wave >= (uint32_t)(L::HW + SPW)) {
-        // ------------- target hasher: quad j hashes target row stream -------------
-        if (p.byte_begin & 1) __builtin_amdgcn_s_setprio(2);
-        const uint32_t pi = 16 * (wave - L::HW - SPW) + (lane >> 2);  // r * SPW + stripe
-        const bool on = pi < (uint32_t)(SPW * TH);
-        const uint32_t r = on ? pi / SPW : 0, e = pi % SPW;
-        const bool live = on && s0 + e < n;
-        const uint32_t roff = (on ? pi : 0) * PP + 8 * q;
-        HHQuad st;
-        hhq_init(st, h.key, q);
-        lds_barrier();  // B(0)
-#pragma unroll 1
-        for (uint32_t s = 0; s <= steps; ++s) {
-            if (s > 0) {  // target rows of step s-1, published by B(s)
-                uint64_t w[16];
-                read16((uint32_t)(uintptr_t)trow + ((s - 1) & 1) * L::TSLOT + roff, w);
-#pragma unroll
-                for (int t = 0; t < 16; ++t) hhq_update(st, w[t]);
-            }
-            if (s < steps) lds_barrier();  // B(s+1)
-        }
-        if (live) hhq_finish(st, p.out_base + (s0 + e) * p.out_stripe_stride + p.out_off[r] - 32, q);
-        return;
-    }
-    if (wave >= (uint32_t)L::HW) {
-        // ------------------------- GF wave: one stripe -------------------------
-        if (p.byte_begin & 2) __builtin_amdgcn_s_setprio(2);  // A/B knob (RSG_DMA_PRIO)
-        const uint32_t e = wave - L::HW;
-        const uint64_t stripe = s0 + e;
-        const bool live = stripe < n;
-        uint8_t* ob = p.out_base + (live ? stripe : 0) * p.out_stripe_stride + lane * 8u;
-        const uint32_t R = p.R, nst = p.n_store, cmask = p.copy_mask;
-        const uint32_t m7 = vgpr_const(0x07070707u), m3 = vgpr_const(0x03030303u);
-        // row of present file f for this stripe: instruction f*HS + e%HS, half e/HS
-        const uint32_t roff = (e % HS) * IP + (e / HS) * CH + lane * 8u;
-        bool bad = false;  // this lane saw a surplus-parity mismatch
-        lds_barrier();  // B(0)
-#pragma unroll 1
-        for (uint32_t s = 0; s < steps; ++s) {
-            const uint8_t* slot = ring + (s % D) * L::DSLOT + roff;
-            uint2 x[C];
-#pragma unroll
-            for (int c = 0; c < C; ++c) x[c] = *(const uint2*)(slot + c * HS * IP);
-            uint32_t tz;  // opaque zero: table reads stay at their use
-            asm volatile("s_mov_b32 %0, 0" : "=s"(tz));
-            const uint8_t* tb = tabs + tz;
-            uint32_t acc[RM][2], pend[RM][2];
-#pragma unroll
-            for (int r = 0; r < RM; ++r) acc[r][0] = acc[r][1] = pend[r][0] = pend[r][1] = 0u;
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                const uint32_t s0a = x[c].x & m7, s0b = x[c].y & m7;
-                const uint32_t s1a = (x[c].x >> 3) & m7, s1b = (x[c].y >> 3) & m7;
-                const uint32_t s2a = (x[c].x >> 6) & m3, s2b = (x[c].y >> 6) & m3;
-#pragma unroll
-                for (int r = 0; r < RM; ++r) {
-                    if ((uint32_t)r >= R) break;  // wave-uniform
-                    const uint8_t* tp = tb + (c * RM + r) * 32;
-                    const uint4 t4 = *(const uint4*)tp;
-                    const uint32_t t2 = *(const uint32_t*)(tp + 16);
-                    gf_fold(c & 1, acc[r][0], pend[r][0], __builtin_amdgcn_perm(t4.y, t4.x, s0a),
-                            __builtin_amdgcn_perm(t4.w, t4.z, s1a), __builtin_amdgcn_perm(t2, t2, s2a));
-                    gf_fold(c & 1, acc[r][1], pend[r][1], __builtin_amdgcn_perm(t4.y, t4.x, s0b),
-                            __builtin_amdgcn_perm(t4.w, t4.z, s1b), __builtin_amdgcn_perm(t2, t2, s2b));
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < RM; ++r) {
-                if ((uint32_t)r >= R) break;
-                const uint2 v = make_uint2(acc[r][0], acc[r][1]);
-                if ((uint32_t)r < nst) {
-                    if (live) st16_nt_half(ob + p.out_off[r] + (uint64_t)s * CH, v);
-                    if constexpr (TH > 0)
-                        *(uint2*)(trow + (s & 1) * L::TSLOT + (r * SPW + e) * PP + lane * 8u) = v;
-                } else {
-                    const uint2 o = *(const uint2*)(slot + (C + (r - nst)) * HS * IP);
-                    bad |= ((o.x ^ v.x) | (o.y ^ v.y)) != 0u;
-                }
-            }
-            if (live) {
-#pragma unroll
-                for (int c = 0; c < C; ++c)
-                    if ((cmask >> c) & 1u) st16_nt_half(ob + p.copy_off[c] + (uint64_t)s * CH, x[c]);
-            }
-            lds_barrier();  // B(s+1): done with slot s % D
-        }
-        // the stripe's surplus verdict, written whole (no memset before the launch)
-        const bool any_bad = __builtin_amdgcn_ballot_w64(bad) != 0;
-        if (live && nst < R && lane == 0) p.ok_flags[stripe] = any_bad ? 0 : 1;
-        return;
-    }
-    // ------------------------- DMA + verify-hash wave -------------------------
-    if (p.byte_begin & 1) __builtin_amdgcn_s_setprio(2);  // A/B knob (RSG_DMA_PRIO)
-    const uint32_t hw = wave, j = lane >> 2;
-    const int ndi = (hw == (uint32_t)(L::HW - 1)) ? L::LAST : 8;  // instructions this wave owns
-    const uint32_t idx = 8 * hw + (j & 7u), half = j >> 3;
-    const bool quad_on = (int)(j & 7u) < ndi;
-    const uint32_t file = quad_on ? idx / HS : 0, stripe_l = (idx % HS) + HS * half;
-    const uint32_t roff = (quad_on ? idx : 0) * IP + half * CH + 8 * q;
-    const bool live = quad_on && s0 + stripe_l < n;
-    HHQuad st;
-    hhq_init(st, h.key, q);
-    uint64_t dsrc[HS];
-#pragma unroll
-    for (int i = 0; i < HS; ++i) {
-        const uint64_t sg = s0 + i + (lane >> 5) * HS;
-        dsrc[i] = (sg < n ? sg : 0) * h.stripe_stride + (lane & 31u) * 16u;
-    }
-    auto dma_step = [&](uint32_t step) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            if (k >= ndi) break;  // wave-uniform
-            const uint32_t ins = 8 * hw + k;
-            const uint8_t* src = h.base[ins / HS] + dsrc[k % HS] + (uint64_t)step * CH;
-            __builtin_amdgcn_global_load_lds(
-                (const void*)src, (__attribute__((address_space(3))) void*)(ring + (step % D) * L::DSLOT + ins * IP), 16,
-                0, 0);
-        }
-    };
-    auto wait_next = [&]() {  // DMA of the next step landed (D - 2 steps younger in flight)
-        if (ndi == 8) __builtin_amdgcn_s_waitcnt(vmcnt_imm((D - 2) * 8));
-        else __builtin_amdgcn_s_waitcnt(vmcnt_imm((D - 2) * L::LAST));
-    };
-#pragma unroll
-    for (int d = 0; d < D - 1; ++d) dma_step(d < (int)steps ? d : steps - 1);
-    wait_next();  // DMA(0) landed
-    lds_barrier();  // B(0)
-#pragma unroll 1
-    for (uint32_t s = 0; s < steps; ++s) {
-        dma_step(s + D - 1 < steps ? s + D - 1 : steps - 1);  // into the slot step s-1 used
-        uint64_t w[16];
-        read16(ring_base + (s % D) * L::DSLOT + roff, w);
-#pragma unroll
-        for (int t = 0; t < 16; ++t) hhq_update(st, w[t]);
-        wait_next();
-        lds_barrier();  // B(s+1)
-    }
-    __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // the clamped tail DMA has landed before the wave ends
-    // verify before use (split_and_verify, bitrot.rs:227-247): lane 0 of each
-    // live quad writes its record's flag whole (no memset before the launch)
-    const uint64_t d = hhq_digest(st, q);
-    bool mis = false;
-    if (live) mis = d != ld64_any(h.base[file] + (s0 + stripe_l) * h.stripe_stride - 32 + 8 * q);
-    const uint64_t bal = __builtin_amdgcn_ballot_w64(mis);
-    if (live && q == 0) h.flag_base[file][s0 + stripe_l] = ((bal >> lane) & 0xFull) ? 0 : 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -1495,6 +935,41 @@ void k_encode_hash_ring(const GfApplyParams p, const HashParams h, const uint32_
 // ---------------------------------------------------------------------------
 // Launchers.
 
+const Tuning& tuning() {
+    static const Tuning t = [] {
+        Tuning v;
+        auto num = [](const char* name, int def, int lo, int hi) {
+            const char* e = getenv(name);
+            if (!e || !*e) return def;
+            const int x = atoi(e);
+            return (x < lo || x > hi) ? def : x;
+        };
+        auto flag = [](const char* name, bool def) {
+            const char* e = getenv(name);
+            return (e && *e) ? e[0] != '0' : def;
+        };
+        v.fused = flag("RSG_FUSED", true);
+        v.lost_disk_fast = flag("RSG_LOST_DISK_FAST", true);
+        v.zero_copy = flag("RSG_ZERO_COPY", true);
+        v.vec_block = num("RSG_VEC_BLOCK", 64, 64, 256) == 256 ? 256 : 64;
+        v.vec_occ = num("RSG_VEC_OCC", -1, 0, 8);
+        v.rolled = flag("RSG_ROLLED", false);
+        v.hash_direct_copy = flag("RSG_HASH_COPY", false);
+        v.hash_depth = num("RSG_HASH_DEPTH", 2, 1, 3);
+        if (const char* e = getenv("RSG_FUSED_KIND"))
+            v.fused_kind = e[0] == 'p' ? 1 : e[0] == 'r' ? 2 : e[0] == 'd' ? 3 : 0;
+        v.fused_spw1 = flag("RSG_FUSED_SPW1", false);
+        v.enc_prio = num("RSG_ENC_PRIO", 0, 0, 3);
+        v.dma_ew = num("RSG_DMA_EW", 2, 2, 4) == 4 ? 4 : 2;
+        v.dma_nt = num("RSG_DMA_NT", 3, 0, 3);
+        v.dma_spw = num("RSG_DMA_SPW", 8, 4, 8) == 4 ? 4 : 8;
+        v.get_prio = num("RSG_DMA_PRIO", 2, 0, 3);
+        v.test_fail_subbatch = num("RSG_TEST_FAIL_SUBBATCH", -1, 0, 1 << 30);
+        return v;
+    }();
+    return t;
+}
+
 using GfKernel = void (*)(const GfApplyParams);
 
 template <int C, int B, bool PRE>
@@ -1512,11 +987,7 @@ static GfKernel pick_vec_r(int R) {
 // (k_gf_apply_loop); RSG_ROLLED=1 forces the rolled kernel for A/B runs.
 template <int B, bool PRE>
 static GfKernel pick_vec_b(int C, int R) {
-    static const bool force_rolled = [] {
-        const char* s = std::getenv("RSG_ROLLED");
-        return s && s[0] == '1';
-    }();
-    if (C <= 8 && R <= 4 && !force_rolled) {
+    if (C <= 8 && R <= 4 && !tuning().rolled) {
         switch (C) {
             case 1: return pick_vec_r<1, B, PRE>(R);
             case 2: return pick_vec_r<2, B, PRE>(R);
@@ -1543,32 +1014,17 @@ static GfKernel pick_vec_b(int C, int R) {
     return nullptr;
 }
 
-static int vec_block() {
-    static const int b = [] {
-        const char* e = std::getenv("RSG_VEC_BLOCK");
-        return (e && std::atoi(e) == 256) ? 256 : 64;
-    }();
-    return b;
-}
+static int vec_block() { return tuning().vec_block; }
 
-// Waves per SIMD the vector kernels may keep resident (RSG_VEC_OCC, A/B
-// runs; default 0 = whatever their registers allow, 3 for the 163-VGPR
-// RS(8,4) encode).  Enforced with an otherwise unused dynamic LDS allocation
-// per one-wave workgroup: 160 KiB / (4 SIMDs x occ) each.
 // Resident waves per SIMD for a vector GF launch, imposed through padding LDS
-// (0 = as many as the registers allow).  RSG_VEC_OCC=<n> forces n for every
-// launch (A/B runs, tools/ab_occ.sh).  Default: 2 for the read-heavy
-// rebuilds of one or two shards from 8 inputs, where fewer waves in flight
-// stream better (RS(8,4) n = 4096: 1 lost 0.846 -> 0.814 ms, 2 lost 0.905 ->
-// 0.888 ms; profiles/r02/ab_occ2/), else no cap.
+// (0 = as many as the registers allow; enforced with an otherwise unused
+// dynamic LDS allocation per one-wave workgroup: 160 KiB / (4 SIMDs x occ)
+// each).  Default: 2 for the read-heavy rebuilds of one or two shards from 8
+// inputs, where fewer waves in flight stream better (RS(8,4) n = 4096: 1 lost
+// 0.846 -> 0.814 ms, 2 lost 0.905 -> 0.888 ms; profiles/r02/ab_occ2/), else
+// no cap.  RSG_VEC_OCC forces one value for A/B runs (tools/ab_occ.sh).
 static int vec_occupancy(int C, int R, bool pre) {
-    static const int forced = [] {
-        const char* e = std::getenv("RSG_VEC_OCC");
-        if (!e) return -1;
-        const int v = std::atoi(e);
-        return (v < 0 || v > 8) ? 0 : v;
-    }();
-    if (forced >= 0) return forced;
+    if (tuning().vec_occ >= 0) return tuning().vec_occ;
     return (!pre && C == 8 && R <= 2) ? 2 : 0;
 }
 
@@ -1622,19 +1078,11 @@ hipError_t launch_hh256(const HashParams& p, hipStream_t stream) {
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
     bool copy = false;  // copy mode when any file of the launch has a copy target
     for (uint32_t b = 0; b < p.nbases; ++b) copy = copy || p.copy_base[b];
-    // copy mode: staged 16-byte stores (COPY = 2) by default; RSG_HASH_COPY=1
-    // selects the direct 8-byte stores for A/B runs
-    static const bool direct_copy = [] {
-        const char* e = getenv("RSG_HASH_COPY");
-        return e && e[0] == '1';
-    }();
-    // Batches of 8 packets in flight per lane: 2 by default; RSG_HASH_DEPTH
-    // = 1, 2 or 3 forces one for A/B runs.
-    static const int depth = [] {
-        const char* e = getenv("RSG_HASH_DEPTH");
-        const int v = e ? atoi(e) : 2;
-        return v >= 1 && v <= 3 ? v : 2;
-    }();
+    // copy mode: staged 16-byte stores (COPY = 2) by default (Tuning:
+    // direct 8-byte stores for A/B runs); 8-packet batches in flight per
+    // lane: 2 by default
+    const bool direct_copy = tuning().hash_direct_copy;
+    const int depth = tuning().hash_depth;
     using HashKernel = void (*)(const HashParams);
     HashKernel k;
     if (!copy) k = depth == 1 ? k_hh256_quad<0, 1> : depth == 2 ? k_hh256_quad<0, 2> : k_hh256_quad<0, 3>;
@@ -1741,35 +1189,18 @@ static bool dma_supported(const GfApplyParams& p, uint64_t shard_len, uint64_t n
 
 static hipError_t launch_encode_hash_dma(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                          hipStream_t stream) {
-    // RSG_ENC_PRIO = 1 (hashers), 2 (encoders), 3: wave priorities for A/B runs
-    static const uint64_t prio = [] {
-        const char* e = getenv("RSG_ENC_PRIO");
-        return e ? (uint64_t)(atoi(e) & 3) : 0ull;
-    }();
-    // RSG_DMA_EW = 4: two encoder waves per stripe group (per-row XOR folds),
-    // else one per group running the generated XOR network (A/B runs)
-    static const int ew = [] {
-        const char* e = getenv("RSG_DMA_EW");
-        return e && atoi(e) == 4 ? 4 : 2;
-    }();
-    p.byte_begin = prio;
+    // Tuning (A/B runs only): enc_prio = wave priorities (default none);
+    // dma_ew = 4: two encoder waves per stripe group (per-row XOR folds)
+    // instead of one running the generated XOR network; dma_nt: non-temporal
+    // data loads (bit 0) and parity stores (bit 1), default both: 1.30 ->
+    // 1.28 ms at n = 4096 (profiles/r02/ab_nt/); dma_spw = 4: four stripes
+    // per workgroup, two workgroups per CU — measured slower (n = 4096: 1.39
+    // vs 1.25 ms; profiles/r02/ab_spw/)
+    const int ew = tuning().dma_ew, nt = tuning().dma_nt, spw = tuning().dma_spw;
+    p.wave_prio = (uint32_t)tuning().enc_prio;
     p.units = (uint32_t)(shard_len / dma::CH);
     h.n = n_stripes;
     const uint64_t blocks = (n_stripes + dma::SPW - 1) / dma::SPW;
-    // Non-temporal data loads and parity stores (default 3): 1.30 -> 1.28 ms
-    // at n = 4096 (profiles/r02/ab_nt/); RSG_DMA_NT = bit 0 loads, bit 1
-    // stores, for A/B runs
-    static const int nt = [] {
-        const char* e = getenv("RSG_DMA_NT");
-        return e ? atoi(e) & 3 : 3;
-    }();
-    // RSG_DMA_SPW = 4 (A/B only): four stripes per workgroup, two workgroups
-    // per CU — measured slower (n = 4096: 1.39 vs 1.25 ms; 4 MiB stripes,
-    // n = 1024: 2.00 ms vs 1.70 ms for the ring kernel; profiles/r02/ab_spw/)
-    static const int spw = [] {
-        const char* e = getenv("RSG_DMA_SPW");
-        return e && atoi(e) == 4 ? 4 : 8;
-    }();
     const dim3 grid((uint32_t)blocks), blk2(64 * dma::Shape<8, 4, 2>::WAVES);
     if (spw == 4 && ew != 4 && (n_stripes + 3) / 4 <= 0x7fffffffull) {
         const dim3 g4((uint32_t)((n_stripes + 3) / 4)), b4(64 * dma::Shape<8, 4, 1, 4>::WAVES);
@@ -1786,112 +1217,17 @@ static hipError_t launch_encode_hash_dma(GfApplyParams p, HashParams h, uint64_t
     return hipGetLastError();
 }
 
-// stripes per workgroup of the one-pass GET kernel: 8 (one workgroup of 13
-// waves per CU) or 4 (two of 7); RSG_GET_SPW for A/B runs
-static int get_spw() {
-    static const int v = [] {
-        const char* e = getenv("RSG_GET_SPW");
-        return e && atoi(e) == 4 ? 4 : 8;
-    }();
-    return v;
-}
-
-template <int NF, int G, int TH = 0>
-static void launch_get(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
-    hipLaunchKernelGGL((k_decode_records_dma<NF, G, TH>), dim3((uint32_t)blocks),
-                       dim3(64 * GetShape<NF, G, TH>::WAVES), 0, stream, p, h);
-}
-
-bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len) {
-    return decode_dma_supported(k, m, nf, shard_len) && targets >= 1 && targets <= 4 && nf + targets <= 12;
-}
-
-hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int nf, int targets, uint64_t shard_len,
-                                   uint64_t n_stripes, hipStream_t stream) {
-    p.byte_begin = dma_prio();
-    if (!heal_dma_supported(8, 4, nf, targets, shard_len) || n_stripes == 0 || p.R > 4 ||
-        p.n_store != (uint32_t)targets || p.copy_mask)
-        return hipErrorInvalidValue;
-    for (int f = 0; f < nf; ++f)
-        if ((uintptr_t)h.base[f] % 16) return hipErrorInvalidValue;
-    if (h.stripe_stride % 16 || p.out_stripe_stride != h.stripe_stride) return hipErrorInvalidValue;
-    p.units = (uint32_t)(shard_len / dma::CH);
-    h.n = n_stripes;
-    const uint64_t blocks = (n_stripes + 7) / 8;
-    if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    // the present + target files are at most the k + m shards
-    switch (nf * 8 + targets) {
-        case 8 * 8 + 1: launch_get<8, 8, 1>(blocks, p, h, stream); break;
-        case 8 * 8 + 2: launch_get<8, 8, 2>(blocks, p, h, stream); break;
-        case 8 * 8 + 3: launch_get<8, 8, 3>(blocks, p, h, stream); break;
-        case 8 * 8 + 4: launch_get<8, 8, 4>(blocks, p, h, stream); break;
-        case 9 * 8 + 1: launch_get<9, 8, 1>(blocks, p, h, stream); break;
-        case 9 * 8 + 2: launch_get<9, 8, 2>(blocks, p, h, stream); break;
-        case 9 * 8 + 3: launch_get<9, 8, 3>(blocks, p, h, stream); break;
-        case 10 * 8 + 1: launch_get<10, 8, 1>(blocks, p, h, stream); break;
-        case 10 * 8 + 2: launch_get<10, 8, 2>(blocks, p, h, stream); break;
-        case 11 * 8 + 1: launch_get<11, 8, 1>(blocks, p, h, stream); break;
-        default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
-bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len) {
-    return k == 8 && m == 4 && nf >= 8 && nf <= 12 && shard_len >= dma::CH && shard_len % dma::CH == 0 &&
-           shard_len / dma::CH <= 0xffffffffull;
-}
-
-hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int nf, uint64_t shard_len, uint64_t n_stripes,
-                                     hipStream_t stream) {
-    p.byte_begin = dma_prio();
-    if (!decode_dma_supported(8, 4, nf, shard_len) || n_stripes == 0 || p.R > 4 || p.n_store > p.R)
-        return hipErrorInvalidValue;
-    for (int f = 0; f < nf; ++f)
-        if ((uintptr_t)h.base[f] % 16) return hipErrorInvalidValue;
-    if (h.stripe_stride % 16) return hipErrorInvalidValue;
-    p.units = (uint32_t)(shard_len / dma::CH);
-    h.n = n_stripes;
-    const uint64_t blocks = (n_stripes + dma::SPW - 1) / dma::SPW;
-    if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    if (get_spw() == 4) {
-        const uint64_t b4 = (n_stripes + 3) / 4;
-        if (b4 > 0x7fffffffull) return hipErrorInvalidValue;
-        switch (nf) {
-            case 8: launch_get<8, 4>(b4, p, h, stream); break;
-            case 9: launch_get<9, 4>(b4, p, h, stream); break;
-            case 10: launch_get<10, 4>(b4, p, h, stream); break;
-            case 11: launch_get<11, 4>(b4, p, h, stream); break;
-            default: launch_get<12, 4>(b4, p, h, stream); break;
-        }
-        return hipGetLastError();
-    }
-    switch (nf) {
-        case 8: launch_get<8, 8>(blocks, p, h, stream); break;
-        case 9: launch_get<9, 8>(blocks, p, h, stream); break;
-        case 10: launch_get<10, 8>(blocks, p, h, stream); break;
-        case 11: launch_get<11, 8>(blocks, p, h, stream); break;
-        default: launch_get<12, 8>(blocks, p, h, stream); break;
-    }
-    return hipGetLastError();
-}
-
 hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                     hipStream_t stream) {
     // Packed workgroups measured as fast or faster than one stripe per
     // workgroup at every batch size tried (n = 256..65536; tools/sweep_small_batch.sh);
-    // RSG_FUSED_SPW1=1 selects the unpacked variant for A/B runs.
-    static const bool unpacked = [] {
-        const char* e = getenv("RSG_FUSED_SPW1");
-        return e && e[0] == '1';
-    }();
+    // Tuning::fused_spw1 selects the unpacked variant for A/B runs.
+    const bool unpacked = tuning().fused_spw1;
     // Few stripes (below ~8 per CU): the ring kernel (one stripe per
     // workgroup, E KiB chunks, next chunk in flight) beats the packed one
     // 1.1-3.2x (tools/kbench/ring_variants.hip);
-    // RSG_FUSED_KIND=packed|ring forces one for A/B runs.
-    static const int kind = [] {
-        const char* e = getenv("RSG_FUSED_KIND");
-        return !e ? 0 : (e[0] == 'p' ? 1 : e[0] == 'r' ? 2 : e[0] == 'd' ? 3 : 0);
-    }();
+    // Tuning::fused_kind (packed|ring|dma) forces one for A/B runs.
+    const int kind = tuning().fused_kind;
     if (kind != 1 && kind != 3 && (kind == 2 || n_stripes < 2048)) {
         uint32_t E = n_stripes <= 768 ? 2u : 1u;
         if (E == 2 && !ring_supported((int)p.C, (int)p.R, shard_len, E)) E = 1;

@@ -312,14 +312,9 @@ void fill_params(const RowSet& rs, int r0, int c0, const uint8_t* base, uint8_t*
             }
 }
 
-// RSG_FUSED=0 disables the fused encode+hash kernel (A/B measurements).
-bool fused_enabled() {
-    static const bool on = [] {
-        const char* s = std::getenv("RSG_FUSED");
-        return !(s && s[0] == '0');
-    }();
-    return on;
-}
+// Tuning::fused = false (RSG_FUSED=0) disables the fused encode+hash kernel
+// (A/B measurements).
+bool fused_enabled() { return rsg::tuning().fused; }
 
 int apply_rows(const RowSet& rs, const uint8_t* base, uint8_t* out_base, uint64_t stride, uint64_t out_stride,
                uint64_t len, uint64_t n, uint32_t mode, uint8_t* ok_flags, hipStream_t stream);
@@ -505,10 +500,19 @@ struct rsg_ctx {
     size_t stage_cap = 0;
     unsigned next_slot = 0;
     uint64_t next_ticket = 1;
+    // A job's completion events, destroyed with the last reference: a ticket
+    // waited on by several threads keeps its events alive until every waiter
+    // has returned.
     struct Job {
         std::vector<hipEvent_t> done;
+        Job() = default;
+        Job(const Job&) = delete;
+        Job& operator=(const Job&) = delete;
+        ~Job() {
+            for (hipEvent_t e : done) (void)hipEventDestroy(e);
+        }
     };
-    std::map<uint64_t, Job> jobs;
+    std::map<uint64_t, std::shared_ptr<Job>> jobs;
 
     // page-locked mirror of the flag scratch: the verdict D2H of the record
     // engines is a few tens of KB, where a pageable copy's staging costs more
@@ -532,6 +536,7 @@ struct rsg_ctx {
     // around the record engines' kernel launches on the call's stream, summed
     // after the call's last synchronisation (ctx->mu held).
     bool timing = false;
+    int record_engine = RSG_RECORD_ENGINE_AUTO;  // rsg_set_record_engine (ctx->mu held)
     std::vector<hipEvent_t> tev;
     size_t tev_used = 0;
     float last_kernel_ms = -1.f;
@@ -641,23 +646,11 @@ uint8_t* pinned_view(const uint8_t* p, size_t len, int device) {
     return (uint8_t*)a.devicePointer;
 }
 
-// RSG_LOST_DISK_FAST=0 disables the optimistic lost-disk GET pass (A/B runs).
-bool lost_disk_fast_enabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("RSG_LOST_DISK_FAST");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
-// RSG_ZERO_COPY=0 disables the in-place kernels on pinned blocks (A/B runs).
-bool zero_copy_enabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("RSG_ZERO_COPY");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
+// Tuning (A/B runs): lost_disk_fast = false disables the optimistic
+// lost-disk GET/heal order, zero_copy = false the in-place kernels on pinned
+// blocks.
+bool lost_disk_fast_enabled() { return rsg::tuning().lost_disk_fast; }
+bool zero_copy_enabled() { return rsg::tuning().zero_copy; }
 
 // Device-batch calls run on the caller's stream; NULL is the HIP null (default)
 // stream, which is also torch's default stream, so ordering with the caller holds.
@@ -707,6 +700,7 @@ int rsg_create(int device, rsg_ctx** out) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return RSG_ERR_NO_DEVICE;
     if (hipSetDevice(device) != hipSuccess) return RSG_ERR_NO_DEVICE;
+    (void)rsg::tuning();  // A/B knobs resolved once, before any launch
     auto* c = new rsg_ctx();
     c->device = device;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -741,8 +735,7 @@ void rsg_destroy(rsg_ctx* ctx) {
         }
         if (ctx->d_stage[i]) (void)hipFree(ctx->d_stage[i]);
     }
-    for (auto& j : ctx->jobs)
-        for (hipEvent_t e : j.second.done) (void)hipEventDestroy(e);
+    ctx->jobs.clear();  // events destroyed with the last reference
     for (hipEvent_t e : ctx->tev) (void)hipEventDestroy(e);
     delete ctx;
 }
@@ -782,7 +775,7 @@ int rsg_encode_batch_host_submit(rsg_ctx* ctx, int k, int m, size_t shard_len, s
     const bool want_hash = h_digests && algo != RSG_HASH_NONE;
     if (want_hash && !hash_key(algo)) return RSG_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> g(ctx->pipe_mu);
-    rsg_ctx::Job job;
+    auto job = std::make_shared<rsg_ctx::Job>();
     // nothing to move: parity of m = 0 is empty; digests are still computed
     // (an empty shard hashes to the digest of the empty message)
     const bool work = n > 0 && ((m > 0 && shard_len > 0) || want_hash);
@@ -796,7 +789,9 @@ int rsg_encode_batch_host_submit(rsg_ctx* ctx, int k, int m, size_t shard_len, s
         if ((st = ctx->ensure_pipeline((size_t)(chunk * dstride + dig_bytes)))) return st;
         const size_t dpitch_data = (shard_pitch == dpitch) ? (size_t)(k * dpitch) : 0;
         bool used[rsg_ctx::kPipeSlots] = {};
-        for (uint64_t s0 = 0; s0 < n; s0 += chunk) {
+        const int fail_at = rsg::tuning().test_fail_subbatch;
+        int sub = 0;
+        for (uint64_t s0 = 0; s0 < n && !st; s0 += chunk, ++sub) {
             const int b = (int)(ctx->next_slot++ % rsg_ctx::kPipeSlots);
             used[b] = true;
             hipStream_t s = ctx->pipe_stream[b];
@@ -812,26 +807,36 @@ int rsg_encode_batch_host_submit(rsg_ctx* ctx, int k, int m, size_t shard_len, s
                     st = hip_status(hipMemcpy2DAsync(d + i * dpitch, dstride, hbase + i * shard_pitch,
                                                      stripe_stride, shard_len, cnt, hipMemcpyHostToDevice, s));
             }
-            if (st) return st;
             uint8_t* ddig = want_hash ? d + chunk * dstride : nullptr;
-            if ((st = rsg_encode_batch_dev(ctx, k, m, shard_len, cnt, d, dpitch, dstride, ddig, algo, s))) return st;
+            if (!st && sub == fail_at) st = RSG_ERR_DEVICE;  // fault injection (tests only)
+            if (!st) st = rsg_encode_batch_dev(ctx, k, m, shard_len, cnt, d, dpitch, dstride, ddig, algo, s);
             for (int p = 0; p < m && shard_len && !st; ++p)
                 st = hip_status(hipMemcpy2DAsync(hbase + (k + p) * shard_pitch, stripe_stride, d + (k + p) * dpitch,
                                                  dstride, shard_len, cnt, hipMemcpyDeviceToHost, s));
             if (!st && want_hash)
                 st = hip_status(hipMemcpyAsync(h_digests + s0 * (k + m) * 32, ddig, cnt * (k + m) * 32,
                                                hipMemcpyDeviceToHost, s));
-            if (st) return st;
-        }
-        for (int b = 0; b < rsg_ctx::kPipeSlots; ++b) {
-            if (!used[b]) continue;
-            hipEvent_t e;
-            if ((st = hip_status(hipEventCreateWithFlags(&e, hipEventDisableTiming)))) return st;
-            job.done.push_back(e);
-            if ((st = hip_status(hipEventRecord(e, ctx->pipe_stream[b])))) break;
         }
         if (st) {
-            for (hipEvent_t e : job.done) (void)hipEventDestroy(e);
+            // An enqueue failed after earlier sub-batches were queued: their
+            // copies still read h_stripes and write parity / digests into the
+            // caller's buffers.  Drain every slot this job used before
+            // returning the error, so no copy outlives the call (the caller
+            // gets no ticket and may free the buffers at once).
+            for (int b = 0; b < rsg_ctx::kPipeSlots; ++b)
+                if (used[b]) (void)hipStreamSynchronize(ctx->pipe_stream[b]);
+            return st;
+        }
+        for (int b = 0; b < rsg_ctx::kPipeSlots && !st; ++b) {
+            if (!used[b]) continue;
+            hipEvent_t e;
+            if ((st = hip_status(hipEventCreateWithFlags(&e, hipEventDisableTiming)))) break;
+            job->done.push_back(e);
+            st = hip_status(hipEventRecord(e, ctx->pipe_stream[b]));
+        }
+        if (st) {  // no ticket: drain the queued sub-batches here (as above)
+            for (int b = 0; b < rsg_ctx::kPipeSlots; ++b)
+                if (used[b]) (void)hipStreamSynchronize(ctx->pipe_stream[b]);
             return st;
         }
     }
@@ -843,31 +848,37 @@ int rsg_encode_batch_host_submit(rsg_ctx* ctx, int k, int m, size_t shard_len, s
 namespace {
 // Query (wait = false) or finish (wait = true) a ticket; a finished ticket is
 // released.  *done = 1 once every sub-batch of the job has completed.
+// Several threads may wait on or poll one ticket: each holds a reference to
+// the job, so its events outlive every waiter; all of them see it finish,
+// and the ticket is unknown (RSG_ERR_INVALID_ARG) only to calls made after.
 int finish_ticket(rsg_ctx* ctx, uint64_t ticket, bool wait, int* done) {
     int st = enter(ctx);
     if (st) return st;
     if (done) *done = 0;
-    std::vector<hipEvent_t> evs;
+    std::shared_ptr<rsg_ctx::Job> job;
     {
         std::lock_guard<std::mutex> g(ctx->pipe_mu);
         auto it = ctx->jobs.find(ticket);
         if (it == ctx->jobs.end()) return RSG_ERR_INVALID_ARG;
-        evs = it->second.done;
+        job = it->second;
     }
     int res = RSG_OK;
-    for (hipEvent_t e : evs) {
+    for (hipEvent_t e : job->done) {
         const hipError_t q = wait ? hipEventSynchronize(e) : hipEventQuery(e);
         if (q == hipErrorNotReady) {  // still in flight (poll only)
-            (void)hipGetLastError();  // not an error: keep it out of the next launch check
+            // hipEventQuery's "not ready" is recorded as the thread's last
+            // error: clear exactly that, so the next launch check does not
+            // fail on it, and leave any other pending error in place
+            if (hipPeekAtLastError() == hipErrorNotReady) (void)hipGetLastError();
             return RSG_OK;
         }
         if (q != hipSuccess && !res) res = hip_status(q);
     }
-    std::lock_guard<std::mutex> g(ctx->pipe_mu);
-    auto it = ctx->jobs.find(ticket);
-    if (it == ctx->jobs.end()) return RSG_ERR_INVALID_ARG;  // finished by a concurrent caller
-    for (hipEvent_t e : it->second.done) (void)hipEventDestroy(e);
-    ctx->jobs.erase(it);
+    {
+        std::lock_guard<std::mutex> g(ctx->pipe_mu);
+        auto it = ctx->jobs.find(ticket);
+        if (it != ctx->jobs.end() && it->second == job) ctx->jobs.erase(it);
+    }
     if (done) *done = 1;
     return res;
 }
@@ -1203,17 +1214,16 @@ int verify_gather(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64_t n, co
     return flags_to_host(ctx, d_flags + (size_t)k * n, (size_t)m * n, flags.data() + (size_t)k * n, s);
 }
 
-// RSG_GET_DMA=0 keeps the two-pass lost-disk GET (A/B runs).
 // One-pass GET/heal (k_decode_records_dma) for a batch of n stripes.  A
 // workgroup walks its 8 stripes front to back (~0.6 ms for 1 MiB RS(8,4)
 // stripes), so below ~1024 stripes, where the grid does not fill the CUs,
 // the two-pass path (GF pass spread over every column, then one verify
-// launch) returns sooner: n = 8 takes 0.67 ms one-pass.  RSG_GET_DMA=0 never,
-// =1 always (tests, A/B runs); read per call.
-bool get_dma_enabled(uint64_t n) {
-    const char* e = std::getenv("RSG_GET_DMA");
-    if (e && e[0] == '0') return false;
-    if (e && e[0] == '1') return true;
+// launch) returns sooner: n = 8 takes 0.67 ms one-pass.  The context's
+// record-engine setting (rsg_set_record_engine: tests and A/B runs) forces
+// either path.
+bool get_dma_enabled(const rsg_ctx* ctx, uint64_t n) {
+    if (ctx->record_engine == RSG_RECORD_ENGINE_ONE_PASS) return true;
+    if (ctx->record_engine == RSG_RECORD_ENGINE_TWO_PASS) return false;
     return n >= 1024;
 }
 
@@ -1277,7 +1287,8 @@ int launch_get_one_pass(Codec& cd, const std::vector<uint8_t>& present, const st
         h.flag_base[f] = d_flags + (size_t)files[f] * n;
     }
     (void)t;
-    return hip_status(rsg::launch_decode_records_dma(p, h, (int)files.size(), shard_len, n, s));
+    return hip_status(rsg::launch_decode_records_dma(p, h, k, (int)present.size() - k, (int)files.size(), shard_len,
+                                                     n, s));
 }
 
 // Launch the one-pass heal (k_decode_records_dma with target hashing) for
@@ -1331,7 +1342,8 @@ int launch_heal_one_pass(Codec& cd, const std::vector<uint8_t>& present, const s
         h.flag_base[f] = d_flags + (size_t)files[f] * n;
     }
     return hip_status(
-        rsg::launch_heal_records_dma(p, h, (int)files.size(), (int)targets.size(), shard_len, n, s));
+        rsg::launch_heal_records_dma(p, h, k, (int)present.size() - k, (int)files.size(), (int)targets.size(),
+                                     shard_len, n, s));
 }
 
 // GET engine body (ctx->mu held): verify records, copy/rebuild the k data
@@ -1445,7 +1457,7 @@ int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64
         std::vector<int> all_idx;
         for (int i = 0; i < t; ++i)
             if (d_files[i]) all_idx.push_back(i);
-        bool one_pass = get_dma_enabled(n) && rsg::decode_dma_supported(k, m, nfiles, shard_len) &&
+        bool one_pass = get_dma_enabled(ctx, n) && rsg::decode_dma_supported(k, m, nfiles, shard_len) &&
                         rec % 16 == 0;
         for (int i : all_idx) one_pass = one_pass && (uintptr_t)(d_files[i] + 32) % 16 == 0;
         if (one_pass) {
@@ -1551,6 +1563,15 @@ int rsg_set_kernel_timing(rsg_ctx* ctx, int on) {
     return RSG_OK;
 }
 
+int rsg_set_record_engine(rsg_ctx* ctx, int engine) {
+    int st = enter(ctx);
+    if (st) return st;
+    if (engine < RSG_RECORD_ENGINE_AUTO || engine > RSG_RECORD_ENGINE_TWO_PASS) return RSG_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    ctx->record_engine = engine;
+    return RSG_OK;
+}
+
 int rsg_last_kernel_ms(rsg_ctx* ctx, float* ms) {
     int st = enter(ctx);
     if (st) return st;
@@ -1576,6 +1597,23 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
     }
     const int t = k + m;
     const uint64_t rec = 32 + shard_len, ks = (uint64_t)k * shard_len;
+    // Targets are written in the same pass that reads the sources: a target
+    // range overlapping any source (or another target) would be silent
+    // corruption (e.g. rewriting a rotten shard file in place), so it is
+    // rejected up front.
+    {
+        const uint64_t span = n * rec;
+        auto overlap = [span](const uint8_t* a, const uint8_t* b) {
+            return (uintptr_t)a < (uintptr_t)b + span && (uintptr_t)b < (uintptr_t)a + span;
+        };
+        for (int i = 0; i < t; ++i) {
+            if (!d_targets[i]) continue;
+            for (int j = 0; j < t; ++j)
+                if ((d_files[j] && overlap(d_targets[i], d_files[j])) ||
+                    (j != i && d_targets[j] && overlap(d_targets[i], d_targets[j])))
+                    return RSG_ERR_INVALID_ARG;
+        }
+    }
     hipStream_t s = pick_stream(ctx, stream);
     std::lock_guard<std::mutex> g(ctx->mu);
     if ((st = ctx->ensure_scratch((size_t)(t + 1) * n))) return st;
@@ -1654,7 +1692,7 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
             if (d_files[i]) all_idx.push_back(i);
             if (d_targets[i]) tg_idx.push_back(i);
         }
-        bool one_pass = get_dma_enabled(n) &&
+        bool one_pass = get_dma_enabled(ctx, n) &&
                         rsg::heal_dma_supported(k, m, (int)all_idx.size(), (int)tg_idx.size(), shard_len) &&
                         rec % 16 == 0;
         for (int i : all_idx) one_pass = one_pass && (uintptr_t)(d_files[i] + 32) % 16 == 0;

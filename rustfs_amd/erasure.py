@@ -446,9 +446,10 @@ class HostBatchTicket:
         if self._done:
             return True
         done = ctypes.c_int(0)
-        check(_lib.load().rsg_poll(self._ctx.handle, self.ticket, ctypes.byref(done)), "Reed-Solomon encode failed")
-        if done.value:
+        st = _lib.load().rsg_poll(self._ctx.handle, self.ticket, ctypes.byref(done))
+        if done.value:  # finished (successfully or not): nothing writes into the arrays any more
             self._done, self._keep = True, None
+        check(st, "Reed-Solomon encode failed")
         return self._done
 
     def wait(self) -> None:

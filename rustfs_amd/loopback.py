@@ -54,6 +54,11 @@ class LocalErasureSet:
         self._get_stage = GetStage()  # page-locked GET staging + device buffers, reused across objects
         self.last_put: dict = {}  # put_stream's counts and producer/consumer clocks
 
+    def close(self) -> None:
+        """Release the reusable GET stage's read pool (a later streamed GET
+        starts a new one)."""
+        self._get_stage.close()
+
     @property
     def k(self) -> int:
         return self.erasure.data_shards
@@ -120,21 +125,28 @@ class LocalErasureSet:
                 os.close(fd)
 
     def put_object_stream(self, name: str, reader, size: int, batch_blocks: int = DEFAULT_BATCH_BLOCKS,
-                          inflight_batches: int = DEFAULT_INFLIGHT_BATCHES, read_threads: int = 4) -> dict:
+                          inflight_batches: int = DEFAULT_INFLIGHT_BATCHES, read_threads: int = 4,
+                          write_quorum: Optional[int] = None) -> dict:
         """PUT of a `size`-byte body read from `reader` (``readinto``) without
         holding it in memory: encode_batched's pipeline (encode.rs:795-919) —
         B-block batches through page-locked staging, GPU encode + HH256S of
         batch i overlapping the read of batch i+1 and the shard-file writes of
-        batch i-1.  Produces the same files as put_object."""
+        batch i-1.  Produces the same files as put_object.  A shard file
+        whose write fails is dropped and the PUT completes while the write
+        quorum holds (MultiWriter::write_shards, encode.rs:374-430); the
+        dropped shards are not committed and heal rebuilds them."""
         e, t = self.erasure, self.k + self.m
-        fds = []
+        fds: List[Optional[int]] = []
         staged = self._stage_lock.acquire(blocking=False)  # else another PUT holds the stage
         try:
             for i in range(t):
-                os.makedirs(os.path.dirname(self._path(i, name)), exist_ok=True)
-                fds.append(os.open(self._path(i, name), os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644))
+                try:  # a disk that cannot take the part has no writer (DiskNotFound)
+                    os.makedirs(os.path.dirname(self._path(i, name)), exist_ok=True)
+                    fds.append(os.open(self._path(i, name), os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644))
+                except OSError:
+                    fds.append(None)
             info = put_stream(e, reader, size, fds, self.algo, batch_blocks, inflight_batches,
-                              self._put_stage if staged else None, read_threads)
+                              self._put_stage if staged else None, read_threads, write_quorum)
             stage = info.pop("stage")
             if staged:
                 self._put_stage = stage
@@ -143,14 +155,29 @@ class LocalErasureSet:
             if staged:
                 self._stage_lock.release()
             for fd in fds:
-                os.close(fd)
-        return self._write_meta(name, size)
+                if fd is not None:
+                    try:
+                        os.close(fd)
+                    except OSError:
+                        pass
+        # the dropped writers' disks are left out of the commit (their
+        # partial part files removed), as the reference drops them before
+        # renaming the object into place
+        failed = set(info["failed_shards"])
+        for i in failed:
+            try:
+                os.unlink(self._path(i, name))
+            except OSError:
+                pass
+        return self._write_meta(name, size, skip=failed)
 
-    def _write_meta(self, name: str, size: int) -> dict:
+    def _write_meta(self, name: str, size: int, skip=()) -> dict:
         e = self.erasure
         meta = {"size": int(size), "data_blocks": self.k, "parity_blocks": self.m, "block_size": e.block_size,
                 "shard_size": e.shard_size(), "algorithm": self.algo.name}
         for i in range(self.k + self.m):
+            if i in skip:
+                continue
             with open(os.path.join(self.dirs[i], name, "meta.json"), "w") as f:
                 json.dump(meta, f)
         return meta
@@ -188,7 +215,10 @@ class LocalErasureSet:
         """Stream bytes [offset, offset + length) (default: to the end) of
         `name`: decode_inner's range read (decode.rs:1702-1968) with full
         blocks verified and rebuilt on the GPU B blocks at a time, the next
-        batch read from the shard files while this one decodes."""
+        batch read from the shard files while this one decodes.  The set's
+        reusable GET stage stays locked while the stream is open: close() an
+        abandoned stream (or consume it) so other GETs can reuse the stage;
+        get_object_range does."""
         size = self._meta(name)["size"]
         fds = self._open_shards(name, size)
         try:

@@ -72,6 +72,17 @@ def _file_source(reader):
     return None
 
 
+def default_write_quorum(k: int, m: int) -> int:
+    """The erasure set's write quorum: the data drive count, plus one when
+    data == parity (set_disk/mod.rs:2792-2795, set_disk/metadata.rs:336-340)."""
+    return k + (1 if k == m else 0)
+
+
+class WriteQuorumError(IOError):
+    """MultiWriter::write_shards' "Failed to write data: ..." once fewer
+    shard writers than the write quorum are still alive (encode.rs:408-429)."""
+
+
 def _write_all(fd: int, iov: List[memoryview]) -> None:
     want = sum(len(v) for v in iov)
     done = os.writev(fd, iov)
@@ -95,21 +106,42 @@ class PutStage:
         return c >= count and b >= blocks and tt == t and s == S
 
 
-def put_stream(erasure: Erasure, reader, size: int, fds: List[int],
+def put_stream(erasure: Erasure, reader, size: int, fds: List[Optional[int]],
                algo: HashAlgorithm = HashAlgorithm.HighwayHash256S,
                batch_blocks: int = DEFAULT_BATCH_BLOCKS,
                inflight_batches: int = DEFAULT_INFLIGHT_BATCHES,
-               stage: Optional[PutStage] = None, read_threads: int = 4) -> dict:
+               stage: Optional[PutStage] = None, read_threads: int = 4,
+               write_quorum: Optional[int] = None) -> dict:
     """Encode `size` bytes read from `reader` (``readinto``) and append one
     BitrotWriter record per block to each shard file descriptor in `fds`
-    (k data then m parity).  Returns the block/batch counts and the stage
-    used (pass it back in to reuse its page-locked buffers).  A regular-file
+    (k data then m parity; None: that disk has no writer).  Returns the
+    block/batch counts, the shards whose writers failed and the stage used
+    (pass it back in to reuse its page-locked buffers).  A regular-file
     `reader` is read `read_threads` blocks at a time with pread (and left
-    positioned after the body, like a sequential read)."""
+    positioned after the body, like a sequential read).
+
+    Write quorum (MultiWriter::write_shards, encode.rs:374-430): a shard
+    file whose write fails (or short-writes) is dropped — nothing more is
+    written to it — and the PUT goes on while at least `write_quorum`
+    writers (default: default_write_quorum) are alive; below that it raises
+    WriteQuorumError.  The caller must not commit the dropped shards."""
     k, m = erasure.data_shards, erasure.parity_shards
     t = k + m
     if len(fds) != t:
         raise ValueError("one file descriptor per shard")
+    wq = default_write_quorum(k, m) if write_quorum is None else write_quorum
+    # per-writer error: None = alive (the reference's errs[i] with writer Some)
+    werr: List[Optional[BaseException]] = [None if fd is not None else FileNotFoundError("disk not found")
+                                           for fd in fds]
+
+    def check_quorum() -> None:
+        alive = sum(e is None for e in werr)
+        if alive < wq:
+            failed = {i: repr(e) for i, e in enumerate(werr) if e is not None}
+            raise WriteQuorumError(f"Failed to write data: write quorum {wq} not met: {alive} of {t} shard "
+                                   f"writers alive, failed {failed}")
+
+    check_quorum()
     bs = erasure.block_size
     S = erasure.shard_size()
     nfull, tail = divmod(size, bs)
@@ -135,10 +167,14 @@ def put_stream(erasure: Erasure, reader, size: int, fds: List[int],
             for b in range(cnt):
                 iov.append(memoryview(dg[b, i]))
                 iov.append(memoryview(st[b, i]))
-            _write_all(fds[i], iov)
+            try:
+                _write_all(fds[i], iov)
+            except OSError as exc:  # drop this writer (write_shard, encode.rs:342-362)
+                werr[i] = exc
 
-        for f in [pool.submit(one, i) for i in range(t)]:
+        for f in [pool.submit(one, i) for i in range(t) if werr[i] is None]:
             f.result()
+        check_quorum()
 
     def consumer():
         while True:
@@ -201,8 +237,15 @@ def put_stream(erasure: Erasure, reader, size: int, fds: List[int],
             raise EOFError("object body shorter than its declared size")
         shards = erasure.encode_data(buf)
         for i in range(t):
-            _write_all(fds[i], [memoryview(algo.hash_encode(shards[i]) + shards[i])])
+            if werr[i] is not None:
+                continue
+            try:
+                _write_all(fds[i], [memoryview(algo.hash_encode(shards[i]) + shards[i])])
+            except OSError as exc:
+                werr[i] = exc
+        check_quorum()
     return {"size": size, "full_blocks": nfull, "tail": tail, "batches": batches, "batch_blocks": blocks,
+            "failed_shards": [i for i in range(t) if werr[i] is not None], "write_quorum": wq,
             "stage": stage, **clock}
 
 

@@ -9,12 +9,17 @@ pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("engine_path")]
 
 
 @pytest.fixture(params=["one_pass", "two_pass"], autouse=False)
-def engine_path(request, monkeypatch):
-    """Every test runs through both lost-disk engines: the one-pass RS(8,4)
-    kernel (forced at any batch size) and the two-pass path (librsgpu reads
-    RSG_GET_DMA per call; by default the one-pass kernel takes >= 1024 stripes)."""
-    monkeypatch.setenv("RSG_GET_DMA", "1" if request.param == "one_pass" else "0")
-    return request.param
+def engine_path(request, gpu):
+    """Every test runs through both lost-disk engines: the one-pass kernel
+    (forced at any batch size where the geometry has one) and the two-pass
+    path, selected on the device-0 context with rsg_set_record_engine (by
+    default the one-pass kernel takes >= 1024 stripes)."""
+    from rustfs_amd import _lib
+    L = _lib.load()
+    want = _lib.RSG_RECORD_ENGINE_ONE_PASS if request.param == "one_pass" else _lib.RSG_RECORD_ENGINE_TWO_PASS
+    _lib.check(L.rsg_set_record_engine(gpu.handle, want))
+    yield request.param
+    _lib.check(L.rsg_set_record_engine(gpu.handle, _lib.RSG_RECORD_ENGINE_AUTO))
 
 
 def _records(torch, k, m, S, n, seed):
@@ -86,6 +91,8 @@ def test_decode_records_detects_inconsistent_parity(gpu, oracle):
     (8, 4, 4096, 7, (3, 9)), (8, 4, 4096, 5, (2, 8, 11)), (4, 2, 65536, 4, (1,)), (6, 3, 4096, 3, (0, 5, 7)),
     (2, 2, 1024, 3, (0,)), (1, 3, 512, 2, (0, 2)), (5, 4, 2048, 9, (4,)),
     (8, 4, 512, 17, (0,)), (8, 4, 512, 3, (1, 2, 3, 4)), (8, 4, 1024, 8, (7, 8, 9)), (8, 4, 4608, 11, (6,)),
+    (16, 4, 4096, 9, (0,)), (16, 4, 4096, 5, (3, 17)), (16, 4, 512, 13, (0, 5, 9, 15)), (16, 2, 1024, 4, (15,)),
+    (16, 4, 65536, 6, (2, 11)), (2, 4, 2048, 6, (0, 1)), (4, 4, 1024, 5, (1, 2, 6)), (2, 2, 524288, 3, (1,)),
 ])
 def test_decode_records_lost_disk_one_pass(gpu, oracle, k, m, S, n, lost):
     """A lost disk (whole data shard files missing) takes the one-pass GET
@@ -137,17 +144,19 @@ def test_decode_records_lost_disk_inconsistent_surplus(gpu, oracle):
     assert torch.equal(out[:4], want[:4])
 
 
-def test_decode_records_lost_disk_many_workgroups(gpu, oracle):
-    """RS(8,4) one-pass GET kernel over many 8-stripe workgroups and a ragged
-    last one: rotten records and an inconsistent surplus parity scattered
-    over the batch are each caught for their own stripe only."""
+@pytest.mark.parametrize("k,m,lost", [(8, 4, (0, 5)), (16, 4, (0, 5)), (16, 4, (9,)), (4, 4, (1, 2))])
+def test_decode_records_lost_disk_many_workgroups(gpu, oracle, k, m, lost):
+    """One-pass GET kernel over many workgroups (8 stripes each, 4 for
+    RS(16,4)) and a ragged last one: rotten records and an inconsistent
+    surplus parity scattered over the batch are each caught for their own
+    stripe only."""
     import torch
     from rustfs_amd import _lib
-    k, m, S, n = 8, 4, 4096, 2051
-    e, st, files = _records(torch, k, m, S, n, seed=17)
+    S, n = 4096, 2051
+    e, st, files = _records(torch, k, m, S, n, seed=17 + k)
     rec = 32 + S
     want = st[:, :k].reshape(n, k * S)
-    f = [None if i in (0, 5) else files[i].clone() for i in range(k + m)]
+    f = [None if i in lost else files[i].clone() for i in range(k + m)]
     f[3][2050 * rec + 32 + 9] ^= 0x02       # data record body, last stripe
     f[k + 1][8 * rec + 1] ^= 0x80           # survivor parity digest, stripe 8
     body = f[k + 3][1234 * rec + 32: 1235 * rec].cpu().numpy().copy()

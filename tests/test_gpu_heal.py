@@ -10,12 +10,17 @@ pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("engine_path")]
 
 
 @pytest.fixture(params=["one_pass", "two_pass"], autouse=False)
-def engine_path(request, monkeypatch):
-    """Every test runs through both lost-disk engines: the one-pass RS(8,4)
-    kernel (forced at any batch size) and the two-pass path (librsgpu reads
-    RSG_GET_DMA per call; by default the one-pass kernel takes >= 1024 stripes)."""
-    monkeypatch.setenv("RSG_GET_DMA", "1" if request.param == "one_pass" else "0")
-    return request.param
+def engine_path(request, gpu):
+    """Every test runs through both lost-disk engines: the one-pass kernel
+    (forced at any batch size where the geometry has one) and the two-pass
+    path, selected on the device-0 context with rsg_set_record_engine (by
+    default the one-pass kernel takes >= 1024 stripes)."""
+    from rustfs_amd import _lib
+    L = _lib.load()
+    want = _lib.RSG_RECORD_ENGINE_ONE_PASS if request.param == "one_pass" else _lib.RSG_RECORD_ENGINE_TWO_PASS
+    _lib.check(L.rsg_set_record_engine(gpu.handle, want))
+    yield request.param
+    _lib.check(L.rsg_set_record_engine(gpu.handle, _lib.RSG_RECORD_ENGINE_AUTO))
 
 
 def _records(torch, oracle, k, m, S, n, seed):
@@ -176,17 +181,20 @@ def test_heal_one_pass_short_walks(gpu, oracle, k, m, S, n):
             assert np.array_equal(tgt[i].cpu().numpy().reshape(n, rec), recs[i]), (lost, i)
 
 
-@pytest.mark.parametrize("lost", [(1, 8), (0,), (0, 1, 2, 3), (9, 10, 11), (2, 5, 10)])
-def test_heal_one_pass_many_workgroups(gpu, oracle, lost):
-    """RS(8,4) heal through the one-pass kernel (verify every source record,
-    write every target record with its digest, compare the surplus parity)
-    over many 8-stripe workgroups and a ragged last one: the healed files are
+@pytest.mark.parametrize("k,m,lost", [(8, 4, (1, 8)), (8, 4, (0,)), (8, 4, (0, 1, 2, 3)), (8, 4, (9, 10, 11)),
+                                      (8, 4, (2, 5, 10)), (16, 4, (3, 16)), (16, 4, (0, 7, 15, 19)),
+                                      (16, 4, (18,)), (2, 2, (2,)), (2, 2, (0,)), (4, 2, (3,)), (4, 4, (0, 5, 6))])
+def test_heal_one_pass_many_workgroups(gpu, oracle, k, m, lost):
+    """Heal through the one-pass kernel (verify every source record, write
+    every target record with its digest, compare the surplus parity) over
+    many workgroups (8 stripes each, 4 for RS(16,4)) and a ragged last one,
+    for every geometry with a one-pass kernel: the healed files are
     byte-identical to the originals; a rotten source record is redone from
     other survivors; a re-hashed inconsistent surplus parity fails its stripe
     alone, whose target digests are zeroed."""
     import torch
     from rustfs_amd import Erasure, _lib
-    k, m, S, n = 8, 4, 4096, 2051
+    S, n = 4096, 2051
     rec = 32 + S
     e = Erasure(k, m, k * S)
     g = torch.Generator(device="cuda").manual_seed(len(lost) * 7 + lost[0])

@@ -131,3 +131,91 @@ def test_concurrent_submitters(gpu, oracle):
     for t in th:
         t.join()
     assert not errors, errors[:2]
+
+
+def test_ticket_waited_from_many_threads(gpu, oracle):
+    """Several threads waiting on and polling one ticket all see it finish
+    (the job's events live until the last waiter returns); afterwards the
+    ticket is released."""
+    import ctypes
+    import threading
+    import torch
+    from rustfs_amd import Erasure, _lib
+    k, m, S, n = 8, 4, 131072, 96
+    e = Erasure(k, m, k * S)
+    L, ctx = _lib.load(), _lib.context(0).handle
+    st = _pinned(torch, (n, k + m, S))
+    st[:, :k] = np.random.default_rng(9).integers(0, 256, (n, k, S), dtype=np.uint8)
+    dig = _pinned(torch, (n, k + m, 32))
+    for rep in range(3):
+        t = ctypes.c_uint64(0)
+        _lib.check(L.rsg_encode_batch_host_submit(ctx, k, m, S, n, st.ctypes.data, S, (k + m) * S,
+                                                  dig.ctypes.data, _lib.RSG_HASH_HIGHWAY256S, ctypes.byref(t)))
+        res = []
+
+        def waiter(poll):
+            if poll:
+                done = ctypes.c_int(0)
+                while True:
+                    rc = L.rsg_poll(ctx, t.value, ctypes.byref(done))
+                    if rc != 0 or done.value:
+                        res.append((rc, done.value))
+                        return
+            else:
+                res.append((L.rsg_wait(ctx, t.value), 1))
+
+        th = [threading.Thread(target=waiter, args=(i % 2 == 1,)) for i in range(6)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(timeout=60)
+        # every caller either saw the job finish or, arriving after another
+        # released it, got INVALID_ARG; at least one saw it finish
+        assert all(rc in (_lib.RSG_OK, _lib.RSG_ERR_INVALID_ARG) for rc, _ in res), res
+        assert any(rc == _lib.RSG_OK and d == 1 for rc, d in res), res
+        assert L.rsg_wait(ctx, t.value) == _lib.RSG_ERR_INVALID_ARG
+    _check(oracle, k, m, st, dig, [0, n - 1])
+
+
+def test_submit_failure_drains_queued_subbatches(tmp_path):
+    """rsg_encode_batch_host_submit failing on a later sub-batch (fault
+    injected with RSG_TEST_FAIL_SUBBATCH, in a child process) returns the
+    error only after the sub-batches it had queued have landed: their parity
+    and digests are in the caller's buffers when the call returns, nothing is
+    left in flight, and no ticket is issued."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "child.py"
+    script.write_text(f'''
+import ctypes, sys
+sys.path.insert(0, {root!r})
+import numpy as np, torch
+from oracle import oracle as O
+from rustfs_amd import _lib
+L = _lib.load(); ctx = _lib.context(0).handle
+k, m, S = 8, 4, 131072
+n = 3 * ((96 << 20) // ((k + m) * S))  # three ~96 MiB sub-batches
+st = torch.zeros((n, k + m, S), dtype=torch.uint8).pin_memory().numpy()
+st[:, :k] = np.random.default_rng(4).integers(0, 256, (n, k, S), dtype=np.uint8)
+st[:, k:] = 0xEE
+dig = torch.zeros((n, k + m, 32), dtype=torch.uint8).pin_memory().numpy()
+t = ctypes.c_uint64(77)
+rc = L.rsg_encode_batch_host_submit(ctx, k, m, S, n, st.ctypes.data, S, (k + m) * S, dig.ctypes.data,
+                                    _lib.RSG_HASH_HIGHWAY256S, ctypes.byref(t))
+assert rc == _lib.RSG_ERR_DEVICE and t.value == 0, (rc, t.value)
+# sub-batch 0 completed before the call returned: no synchronisation here
+ref = st[0].copy(); ref[k:] = 0; O.encode(k, m, ref)
+assert np.array_equal(ref, st[0]) and dig[0, 0].tobytes() == O.hh256s(ref[0])
+assert (st[n - 1, k:] == 0xEE).all()  # the failed and later sub-batches wrote nothing
+# the context still works afterwards
+t2 = ctypes.c_uint64(0)
+assert L.rsg_encode_batch_host_submit(ctx, k, m, S, 4, st.ctypes.data, S, (k + m) * S, None, 0,
+                                      ctypes.byref(t2)) == _lib.RSG_OK  # one sub-batch: index 1 never comes
+assert L.rsg_wait(ctx, t2.value) == _lib.RSG_OK
+print("child ok")
+''')
+    env = dict(os.environ, RSG_TEST_FAIL_SUBBATCH="1")
+    p = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=150)
+    assert p.returncode == 0 and "child ok" in p.stdout, p.stderr[-3000:]

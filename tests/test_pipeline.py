@@ -171,3 +171,89 @@ def test_stream_close_early(gpu, tmp_path):
     assert next(g) == data[BS // 2: BS]
     g.close()  # joins the read-ahead thread, closes the shard files
     assert es.get_object("b/o") == data
+
+
+class _BreakWriters(io.BytesIO):
+    """A body reader that, once `after` bytes have been read, breaks the
+    shard writers in `targets`: their descriptors are replaced (dup2) by a
+    read-only one, so every later write to them fails (EBADF) — a shard disk
+    that goes away mid-stream."""
+
+    def __init__(self, data, after, es, name, targets):
+        super().__init__(data)
+        self.after, self.es, self.name, self.targets, self.read_so_far = after, es, name, targets, 0
+        self.ro = os.open(os.devnull, os.O_RDONLY)
+
+    def readinto(self, b):
+        n = super().readinto(b)
+        self.read_so_far += n
+        if self.read_so_far >= self.after and self.targets:
+            for i in self.targets:
+                fd = self._fd_of(i)
+                if fd is not None:
+                    os.dup2(self.ro, fd)
+            self.targets = ()
+        return n
+
+    def _fd_of(self, i):
+        want = os.path.realpath(os.path.join(self.es.dirs[i], self.name, "part.1"))
+        for fd in os.listdir("/proc/self/fd"):
+            try:
+                if os.path.realpath(f"/proc/self/fd/{fd}") == want:
+                    return int(fd)
+            except OSError:
+                pass
+        return None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,m,broken,ok", [(4, 2, (1,), True), (4, 2, (0, 5), True), (4, 2, (0, 2, 5), False),
+                                           (2, 2, (3,), True), (2, 2, (0, 3), False)])
+def test_put_stream_write_quorum(gpu, tmp_path, k, m, broken, ok):
+    """MultiWriter::write_shards (encode.rs:374-430): writers that fail
+    mid-stream are dropped and the PUT completes while >= write quorum (k, or
+    k+1 when k == m) remain; the dropped shards are not committed, GET reads
+    the object back and heal rebuilds their files byte for byte.  Below
+    quorum the PUT fails with "Failed to write data"."""
+    from rustfs_amd.pipeline import WriteQuorumError
+    size = 9 * BS + 777
+    es, dirs = _set(tmp_path, k, m)
+    data = np.random.default_rng(k * 10 + len(broken)).integers(0, 256, size, dtype=np.uint8).tobytes()
+    r = _BreakWriters(data, 3 * BS, es, "b/o", broken)
+    if not ok:
+        with pytest.raises(WriteQuorumError, match="Failed to write data"):
+            es.put_object_stream("b/o", r, size, batch_blocks=2, inflight_batches=1)
+        return
+    es.put_object_stream("b/o", r, size, batch_blocks=2, inflight_batches=1)
+    assert es.last_put["failed_shards"] == sorted(broken)
+    for i in broken:
+        assert not os.path.exists(os.path.join(dirs[i], "b/o", "part.1"))
+        assert not os.path.exists(os.path.join(dirs[i], "b/o", "meta.json"))
+    assert es.get_object("b/o") == data
+    es.put_object("b/ref", data)
+    es.heal_object("b/o", list(broken))
+    assert _files(dirs, "b/o") == _files(dirs, "b/ref")
+
+
+@pytest.mark.gpu
+def test_put_stream_disk_missing_from_start(gpu, tmp_path):
+    """A disk with no writer at all (None: DiskNotFound) counts against the
+    quorum from the first block."""
+    from rustfs_amd.pipeline import WriteQuorumError, put_stream
+    from rustfs_amd.erasure import Erasure
+    k, m = 4, 2
+    e = Erasure(k, m, BS)
+    size = 5 * BS
+    data = np.random.default_rng(1).integers(0, 256, size, dtype=np.uint8).tobytes()
+    paths = [tmp_path / f"s{i}" for i in range(k + m)]
+    fds = [os.open(p, os.O_WRONLY | os.O_CREAT) for p in paths]
+    try:
+        info = put_stream(e, io.BytesIO(data), size, [None if i == 4 else fd for i, fd in enumerate(fds)],
+                          batch_blocks=2)
+        assert info["failed_shards"] == [4] and info["write_quorum"] == 4
+        assert os.path.getsize(paths[4]) == 0 and os.path.getsize(paths[0]) == 5 * (32 + BS // k)
+        with pytest.raises(WriteQuorumError):
+            put_stream(e, io.BytesIO(data), size, [None, None, None] + fds[3:], batch_blocks=2)
+    finally:
+        for fd in fds:
+            os.close(fd)

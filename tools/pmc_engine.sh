@@ -10,9 +10,11 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 G1="SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE"
 G2="SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_COUNT"
+G3="FETCH_SIZE"
+G4="WRITE_SIZE"
 for what in get2 heal; do
   i=0
-  for CTRS in "$G1" "$G2"; do
+  for CTRS in "$G1" "$G2" "$G3" "$G4"; do
     i=$((i+1))
     timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $CTRS -d $OUT/$what/p$i -o run --output-format csv -- python3 $R/tools/engine_prof.py $what 3 > $OUT/${what}_p$i.txt 2>&1 || exit $?
   done
