@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <string>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -769,6 +770,164 @@ __global__ __launch_bounds__((64 * dma::Shape<K, M, NE, SP>::WAVES)) void k_enco
 }
 
 // ---------------------------------------------------------------------------
+// Fused RS(8,4) encode + HighwayHash-256 for batches of FEW LARGE stripes
+// (config 4's 4-8 MiB stripes at 4 GiB per launch: 512-1024 stripes), where
+// k_encode_hash_dma's 8-stripe workgroups leave CUs idle and the ring
+// kernel's table-GF encoder wave is the pace.  One
+// workgroup owns SPW (2 or 4) stripes and walks them in 1 KiB steps:
+//   data-hasher waves (SPW/2): each brings 16 of the step's SPW x 8 data
+//     rows into a 3-slot LDS ring by LDS-DMA (one 1 KiB row = one
+//     global_load_lds of 16 B per lane) two steps ahead, then hashes those 16
+//     streams straight out of the ring (32 packets per stream per step);
+//   encoder waves (SPW/2): stripe pair e, 16 B of each stripe per lane
+//     (8 dwords), bit-transposed into planes, all four parity rows from the
+//     generated XOR network (rs84_xornet.h), transposed back, stored to HBM
+//     and into a double-buffered parity-row area;
+//   one parity-hasher wave: the SPW x 4 parity streams one step behind.
+// One barrier per step.  Per stripe-KiB this issues ~408 encoder and ~456
+// hash instructions against ~768 + 456 for the ring kernel's table GF.
+namespace wide {
+constexpr uint32_t CH = 1024;       // bytes per shard per step
+constexpr uint32_t RP = CH + 32;    // LDS row pitch: the 8 quads of a half-wave hit distinct banks
+constexpr int D = 3, NP = 2;
+template <int SPW>
+struct Shape {
+    static constexpr int ENC = SPW / 2, DH = SPW / 2, PH = 1;
+    static constexpr int WAVES = ENC + DH + PH;
+    static constexpr uint32_t DSLOT = SPW * 8 * RP;  // one step of data rows
+    static constexpr uint32_t PSLOT = SPW * 4 * RP;  // one step of parity rows
+    static constexpr uint32_t LDS = D * DSLOT + NP * PSLOT;
+};
+// 32 packets of one stream (8 B per lane, 32 B apart) from LDS
+__device__ __forceinline__ void read32(uint32_t a, uint64_t (&w)[32]) {
+    uint64_t (&lo)[16] = *reinterpret_cast<uint64_t(*)[16]>(&w[0]);
+    uint64_t (&hi)[16] = *reinterpret_cast<uint64_t(*)[16]>(&w[16]);
+    dma::read16(a, lo);
+    dma::read16(a + 512, hi);
+}
+}  // namespace wide
+
+template <int SPW>
+__global__ __launch_bounds__(64 * wide::Shape<SPW>::WAVES) void k_encode_hash_wide(const GfApplyParams p,
+                                                                                   const HashParams h) {
+    using namespace wide;
+    using L = Shape<SPW>;
+    static_assert(SPW == 2 || SPW == 4, "stripe pairs per encoder wave");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[L::LDS];
+    uint8_t* const ring = lds;
+    uint8_t* const prow = lds + D * L::DSLOT;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u, q = lane & 3u;
+    const uint64_t n = h.n;
+    const uint32_t steps = p.units;  // S / CH
+    const uint64_t s0 = (uint64_t)blockIdx.x * SPW;
+    uint8_t* const base = p.out_base;
+
+    if (wave < (uint32_t)L::ENC) {
+        // ------------------------------ encoder ------------------------------
+        const uint32_t e = wave;  // stripes 2e, 2e+1 of the workgroup
+        const bool liveA = s0 + 2 * e < n, liveB = s0 + 2 * e + 1 < n;
+        const uint64_t dA = (liveA ? s0 + 2 * e : 0) * p.stripe_stride + lane * 16u;
+        const uint64_t dB = (liveB ? s0 + 2 * e + 1 : 0) * p.stripe_stride + lane * 16u;
+        const uint32_t m4 = vgpr_const(0x0f0f0f0fu), m2 = vgpr_const(0x33333333u), m1 = vgpr_const(0x55555555u);
+        lds_barrier();  // B(0): slot 0 landed
+#pragma unroll 1
+        for (uint32_t s = 0; s < steps; ++s) {
+            const uint8_t* slot = ring + (s % D) * L::DSLOT + lane * 16u;
+            uint32_t P[64];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const uint4 a = *(const uint4*)(slot + ((2 * e) * 8 + c) * RP);
+                const uint4 b = *(const uint4*)(slot + ((2 * e + 1) * 8 + c) * RP);
+                uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+                dma::transpose(w, m4, m2, m1);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) P[8 * c + j] = w[j];
+            }
+            uint32_t O[32];
+            xn::rs84_encode_planes(P, O);
+            uint8_t* pr = prow + (s % NP) * L::PSLOT + lane * 16u;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                uint32_t w[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) w[i] = O[8 * r + i];
+                dma::transpose(w, m4, m2, m1);
+                const uint4 va = make_uint4(w[0], w[1], w[2], w[3]), vb = make_uint4(w[4], w[5], w[6], w[7]);
+                const uint64_t off = p.out_off[r] + (uint64_t)s * CH;
+                if (liveA) st16_nt(base + dA + off, va);
+                if (liveB) st16_nt(base + dB + off, vb);
+                *(uint4*)(pr + ((2 * e) * 4 + r) * RP) = va;
+                *(uint4*)(pr + ((2 * e + 1) * 4 + r) * RP) = vb;
+            }
+            lds_barrier();  // B(s+1): parity rows of step s published
+        }
+        return;
+    }
+    HHQuad st;
+    hhq_init(st, h.key, q);
+    const uint32_t j = lane >> 2;  // stream (quad) of this wave
+    if (wave < (uint32_t)(L::ENC + L::DH)) {
+        // ------------- data hasher + DMA: stripes 2w, 2w+1, all 8 data shards -------------
+        const uint32_t w = wave - L::ENC;
+        const uint32_t stripe_l = 2 * w + j / 8, shard = j % 8;
+        const bool live = s0 + stripe_l < n;
+        uint64_t src[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const uint64_t sg = s0 + 2 * w + i;
+            src[i] = (sg < n ? sg : 0) * p.stripe_stride + lane * 16u;
+        }
+        const uint32_t row_of = (stripe_l * 8 + shard) * RP + 8 * q;
+        auto dma = [&](uint32_t step) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {  // row k: stripe 2w + k/8, shard k%8 (wave-uniform)
+                const uint8_t* g = base + src[k / 8] + p.in_off[k % 8] + (uint64_t)step * CH;
+                __builtin_amdgcn_global_load_lds(
+                    (const void*)g,
+                    (__attribute__((address_space(3))) void*)(ring + (step % D) * L::DSLOT + ((2 * w + k / 8) * 8 + k % 8) * RP),
+                    16, 0, 2);  // non-temporal: read once
+            }
+        };
+#pragma unroll
+        for (int d = 0; d < D - 1; ++d) dma(d < (int)steps ? d : steps - 1);
+        __builtin_amdgcn_s_waitcnt(dma::vmcnt_imm((D - 2) * 16));  // DMA(0) landed
+        lds_barrier();  // B(0)
+        const uint32_t ring_base = (uint32_t)(uintptr_t)ring;
+#pragma unroll 1
+        for (uint32_t s = 0; s < steps; ++s) {
+            dma(s + D - 1 < steps ? s + D - 1 : steps - 1);  // into the slot step s-1 used
+            uint64_t wv[32];
+            read32(ring_base + (s % D) * L::DSLOT + row_of, wv);
+#pragma unroll
+            for (int t = 0; t < 32; ++t) hhq_update(st, wv[t]);
+            __builtin_amdgcn_s_waitcnt(dma::vmcnt_imm((D - 2) * 16));  // DMA(s+1) landed
+            lds_barrier();  // B(s+1)
+        }
+        __builtin_amdgcn_s_waitcnt(dma::vmcnt_imm(0));  // the clamped tail DMA has landed
+        if (live) hhq_finish(st, h.out + ((s0 + stripe_l) * 12 + shard) * 32u, q);
+        return;
+    }
+    // ------------------- parity hasher: SPW x 4 streams, one step behind -------------------
+    const bool on = j < (uint32_t)(SPW * 4);
+    const uint32_t pj = on ? j : 0, stripe_l = pj / 4, r = pj % 4;
+    const bool live = on && s0 + stripe_l < n;
+    const uint32_t row_of = (stripe_l * 4 + r) * RP + 8 * q;
+    const uint32_t prow_base = (uint32_t)(uintptr_t)prow;
+    lds_barrier();  // B(0)
+#pragma unroll 1
+    for (uint32_t s = 0; s <= steps; ++s) {
+        if (s > 0) {  // parity rows of step s-1, published by B(s)
+            uint64_t wv[32];
+            read32(prow_base + ((s - 1) % NP) * L::PSLOT + row_of, wv);
+#pragma unroll
+            for (int t = 0; t < 32; ++t) hhq_update(st, wv[t]);
+        }
+        if (s < steps) lds_barrier();  // B(s+1)
+    }
+    if (live) hhq_finish(st, h.out + ((s0 + stripe_l) * 12 + 8 + r) * 32u, q);
+}
+
+// ---------------------------------------------------------------------------
 // Fused RS encode + HighwayHash-256, ring variant for batches of few large
 // stripes (config 4's 4-16 MiB stripes at 4 GiB per launch: 256-1024 stripes).
 // There the packed kernel above has too few bytes in flight (one 512-B chunk
@@ -956,8 +1115,10 @@ const Tuning& tuning() {
         v.rolled = flag("RSG_ROLLED", false);
         v.hash_direct_copy = flag("RSG_HASH_COPY", false);
         v.hash_depth = num("RSG_HASH_DEPTH", 2, 1, 3);
-        if (const char* e = getenv("RSG_FUSED_KIND"))
-            v.fused_kind = e[0] == 'p' ? 1 : e[0] == 'r' ? 2 : e[0] == 'd' ? 3 : 0;
+        if (const char* e = getenv("RSG_FUSED_KIND")) {
+            const std::string k(e);
+            v.fused_kind = k == "packed" ? 1 : k == "ring" ? 2 : k == "dma" ? 3 : k == "wide2" ? 4 : k == "wide4" ? 5 : 0;
+        }
         v.fused_spw1 = flag("RSG_FUSED_SPW1", false);
         v.enc_prio = num("RSG_ENC_PRIO", 0, 0, 3);
         v.dma_ew = num("RSG_DMA_EW", 2, 2, 4) == 4 ? 4 : 2;
@@ -1217,6 +1378,28 @@ static hipError_t launch_encode_hash_dma(GfApplyParams p, HashParams h, uint64_t
     return hipGetLastError();
 }
 
+// Few large RS(8,4) stripes: k_encode_hash_wide with SPW stripes per
+// workgroup (same preconditions as the DMA kernel, plus whole 1 KiB steps).
+static bool wide_supported(const GfApplyParams& p, uint64_t shard_len, uint64_t n_stripes) {
+    return dma_supported(p, shard_len, n_stripes) && shard_len % wide::CH == 0 && p.out_off[0] % 16 == 0 &&
+           p.out_off[1] % 16 == 0 && p.out_off[2] % 16 == 0 && p.out_off[3] % 16 == 0;
+}
+
+static hipError_t launch_encode_hash_wide(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
+                                          int spw, hipStream_t stream) {
+    p.units = (uint32_t)(shard_len / wide::CH);
+    h.n = n_stripes;
+    const uint64_t blocks = (n_stripes + spw - 1) / spw;
+    if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+    if (spw == 4)
+        hipLaunchKernelGGL((k_encode_hash_wide<4>), dim3((uint32_t)blocks), dim3(64 * wide::Shape<4>::WAVES), 0,
+                           stream, p, h);
+    else
+        hipLaunchKernelGGL((k_encode_hash_wide<2>), dim3((uint32_t)blocks), dim3(64 * wide::Shape<2>::WAVES), 0,
+                           stream, p, h);
+    return hipGetLastError();
+}
+
 hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                     hipStream_t stream) {
     // Packed workgroups measured as fast or faster than one stripe per
@@ -1228,6 +1411,8 @@ hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shar
     // 1.1-3.2x (tools/kbench/ring_variants.hip);
     // Tuning::fused_kind (packed|ring|dma) forces one for A/B runs.
     const int kind = tuning().fused_kind;
+    if ((kind == 4 || kind == 5) && wide_supported(p, shard_len, n_stripes))
+        return launch_encode_hash_wide(p, h, shard_len, n_stripes, kind == 5 ? 4 : 2, stream);
     if (kind != 1 && kind != 3 && (kind == 2 || n_stripes < 2048)) {
         uint32_t E = n_stripes <= 768 ? 2u : 1u;
         if (E == 2 && !ring_supported((int)p.C, (int)p.R, shard_len, E)) E = 1;

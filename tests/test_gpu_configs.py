@@ -184,3 +184,44 @@ def test_dma_kernel_ab_variants(gpu, oracle, env):
                            env={**os.environ, **env, "RSG_FUSED_KIND": "dma"}, capture_output=True, text=True,
                            timeout=150)
         assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (env, n, r.stdout[-500:], r.stderr[-2000:])
+
+
+_WIDE_SNIPPET = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, {root!r})
+from rustfs_amd import Erasure
+from oracle import oracle as O
+k, m, S, n = 8, 4, {S}, {n}
+g = torch.Generator(device="cuda").manual_seed(n + S)
+st = torch.zeros((n, k + m, S), dtype=torch.uint8, device="cuda")
+st[:, :k] = torch.randint(0, 256, (n, k, S), dtype=torch.uint8, device="cuda", generator=g)
+st[:, k:] = 0xA5
+dig = torch.zeros((n, k + m, 32), dtype=torch.uint8, device="cuda")
+Erasure(k, m, k * S).encode_batch(st, dig)
+torch.cuda.synchronize()
+for s in sorted({{0, 1, 2, 3, n // 2, n - 3, n - 2, n - 1}} & set(range(n))):
+    got = st[s].cpu().numpy(); ref = got.copy(); ref[k:] = 0
+    O.encode(k, m, ref)
+    assert np.array_equal(got[k:], ref[k:]), s
+    d = dig[s].cpu().numpy()
+    for i in range(k + m):
+        assert d[i].tobytes() == O.hh256s(ref[i]), (s, i)
+print("ok")
+"""
+
+
+@pytest.mark.parametrize("kind", ["wide2", "wide4"])
+def test_wide_kernel_ragged_batches(gpu, oracle, kind):
+    """k_encode_hash_wide (RS(8,4), few large stripes: SPW = 2 or 4 stripes
+    per workgroup, 1 KiB steps, XOR-network encoder on 16 B per lane of a
+    stripe pair): parity and all 12 digests vs the oracle on ragged batches
+    (dead stripes in the last workgroup), a single step and many steps.
+    Forced with RSG_FUSED_KIND (read once per process: own process each)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for n, S in ((1, 1024), (3, 4096), (5, 2048), (6, 65536), (1027, 8192)):
+        r = subprocess.run([sys.executable, "-c", _WIDE_SNIPPET.format(root=root, n=n, S=S)],
+                           env={**os.environ, "RSG_FUSED_KIND": kind}, capture_output=True, text=True, timeout=150)
+        assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (kind, n, S, r.stdout[-500:], r.stderr[-2000:])
