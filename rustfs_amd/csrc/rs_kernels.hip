@@ -779,24 +779,32 @@ __global__ __launch_bounds__((64 * dma::Shape<K, M, NE, SP>::WAVES)) void k_enco
 //     rows into a 3-slot LDS ring by LDS-DMA (one 1 KiB row = one
 //     global_load_lds of 16 B per lane) two steps ahead, then hashes those 16
 //     streams straight out of the ring (32 packets per stream per step);
-//   encoder waves (SPW/2): stripe pair e, 16 B of each stripe per lane
-//     (8 dwords), bit-transposed into planes, all four parity rows from the
-//     generated XOR network (rs84_xornet.h), transposed back, stored to HBM
-//     and into a double-buffered parity-row area;
-//   one parity-hasher wave: the SPW x 4 parity streams one step behind.
-// One barrier per step.  Per stripe-KiB this issues ~408 encoder and ~456
-// hash instructions against ~768 + 456 for the ring kernel's table GF.
+//   encoder waves: stripe pair e, 16 B of each stripe per lane (8 dwords),
+//     bit-transposed into planes, all four parity rows from the generated XOR
+//     network (rs84_xornet.h), transposed back, stored to HBM and into a
+//     double-buffered parity-row area;
+//   one parity-hasher wave: the SPW x 4 parity streams.
+// One barrier per step.  A lone encoder wave issues its ~830 dependent
+// instructions per step at ~5 cycles each, more than a step's memory time
+// (4 MiB stripes, SPW = 4: the encoder SIMD sets the pace), so with SPLIT
+// each stripe pair has TWO encoder waves taking alternate steps, and each
+// step's work straddles one barrier: in the interval a step's data is in the
+// ring the wave reads and bit-transposes it (the planes stay in registers),
+// in the next it runs the network, transposes back and stores; the parity
+// hasher is then two steps behind.  Per stripe-KiB this issues ~408 encoder
+// and ~456 hash instructions against ~768 + 456 for the ring kernel's table GF.
 namespace wide {
 constexpr uint32_t CH = 1024;       // bytes per shard per step
 constexpr uint32_t RP = CH + 32;    // LDS row pitch: the 8 quads of a half-wave hit distinct banks
 constexpr int D = 3, NP = 2;
-template <int SPW>
+template <int SPW, bool SPLIT>
 struct Shape {
-    static constexpr int ENC = SPW / 2, DH = SPW / 2, PH = 1;
+    static constexpr int ENC = SPLIT ? SPW : SPW / 2, DH = SPW / 2, PH = 1;
     static constexpr int WAVES = ENC + DH + PH;
     static constexpr uint32_t DSLOT = SPW * 8 * RP;  // one step of data rows
     static constexpr uint32_t PSLOT = SPW * 4 * RP;  // one step of parity rows
     static constexpr uint32_t LDS = D * DSLOT + NP * PSLOT;
+    static constexpr int LAG = SPLIT ? 2 : 1;        // steps the parity hasher trails the DMA
 };
 // 32 packets of one stream (8 B per lane, 32 B apart) from LDS
 __device__ __forceinline__ void read32(uint32_t a, uint64_t (&w)[32]) {
@@ -805,13 +813,48 @@ __device__ __forceinline__ void read32(uint32_t a, uint64_t (&w)[32]) {
     dma::read16(a, lo);
     dma::read16(a + 512, hi);
 }
+// Planes of stripe pair e (16 B of each per lane) from a ring slot.
+__device__ __forceinline__ void load_planes(const uint8_t* slot, uint32_t e, uint32_t (&P)[64], uint32_t m4,
+                                            uint32_t m2, uint32_t m1) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const uint4 a = *(const uint4*)(slot + ((2 * e) * 8 + c) * RP);
+        const uint4 b = *(const uint4*)(slot + ((2 * e + 1) * 8 + c) * RP);
+        uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        dma::transpose(w, m4, m2, m1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) P[8 * c + j] = w[j];
+    }
+}
+// Network + back-transposes + stores of one step of stripe pair e.
+template <int SPW, bool SPLIT>
+__device__ __forceinline__ void emit_parity(const GfApplyParams& p, const uint32_t (&P)[64], uint32_t e, uint32_t s,
+                                            bool liveA, bool liveB, uint64_t dA, uint64_t dB, uint8_t* prow_slot,
+                                            uint32_t m4, uint32_t m2, uint32_t m1) {
+    uint32_t O[32];
+    xn::rs84_encode_planes(P, O);
+    uint8_t* pr = prow_slot + (threadIdx.x & 63u) * 16u;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        uint32_t w[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[i] = O[8 * r + i];
+        dma::transpose(w, m4, m2, m1);
+        const uint4 va = make_uint4(w[0], w[1], w[2], w[3]), vb = make_uint4(w[4], w[5], w[6], w[7]);
+        const uint64_t off = p.out_off[r] + (uint64_t)s * CH;
+        if (liveA) st16_nt(p.out_base + dA + off, va);
+        if (liveB) st16_nt(p.out_base + dB + off, vb);
+        *(uint4*)(pr + ((2 * e) * 4 + r) * RP) = va;
+        *(uint4*)(pr + ((2 * e + 1) * 4 + r) * RP) = vb;
+    }
+}
 }  // namespace wide
 
-template <int SPW>
-__global__ __launch_bounds__(64 * wide::Shape<SPW>::WAVES) void k_encode_hash_wide(const GfApplyParams p,
-                                                                                   const HashParams h) {
+template <int SPW, bool SPLIT>
+__global__ __launch_bounds__((64 * wide::Shape<SPW, SPLIT>::WAVES)) void k_encode_hash_wide(const GfApplyParams p,
+                                                                                          const HashParams h) {
     using namespace wide;
-    using L = Shape<SPW>;
+    using L = Shape<SPW, SPLIT>;
     static_assert(SPW == 2 || SPW == 4, "stripe pairs per encoder wave");
     __shared__ __attribute__((aligned(16))) uint8_t lds[L::LDS];
     uint8_t* const ring = lds;
@@ -821,45 +864,35 @@ __global__ __launch_bounds__(64 * wide::Shape<SPW>::WAVES) void k_encode_hash_wi
     const uint32_t steps = p.units;  // S / CH
     const uint64_t s0 = (uint64_t)blockIdx.x * SPW;
     uint8_t* const base = p.out_base;
+    // Intervals: interval t runs between barriers B(t) and B(t+1); there are
+    // steps + LAG of them (the last ends without a barrier), so every wave
+    // passes B(0) .. B(steps + LAG - 1).
+    const uint32_t intervals = steps + L::LAG;
 
     if (wave < (uint32_t)L::ENC) {
         // ------------------------------ encoder ------------------------------
-        const uint32_t e = wave;  // stripes 2e, 2e+1 of the workgroup
+        const uint32_t e = SPLIT ? wave / 2 : wave;  // stripes 2e, 2e+1 of the workgroup
+        const uint32_t ph = SPLIT ? wave % 2 : 0;    // SPLIT: this wave's steps are s % 2 == ph
         const bool liveA = s0 + 2 * e < n, liveB = s0 + 2 * e + 1 < n;
         const uint64_t dA = (liveA ? s0 + 2 * e : 0) * p.stripe_stride + lane * 16u;
         const uint64_t dB = (liveB ? s0 + 2 * e + 1 : 0) * p.stripe_stride + lane * 16u;
         const uint32_t m4 = vgpr_const(0x0f0f0f0fu), m2 = vgpr_const(0x33333333u), m1 = vgpr_const(0x55555555u);
+        uint32_t P[64];
         lds_barrier();  // B(0): slot 0 landed
 #pragma unroll 1
-        for (uint32_t s = 0; s < steps; ++s) {
-            const uint8_t* slot = ring + (s % D) * L::DSLOT + lane * 16u;
-            uint32_t P[64];
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                const uint4 a = *(const uint4*)(slot + ((2 * e) * 8 + c) * RP);
-                const uint4 b = *(const uint4*)(slot + ((2 * e + 1) * 8 + c) * RP);
-                uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-                dma::transpose(w, m4, m2, m1);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) P[8 * c + j] = w[j];
+        for (uint32_t t = 0; t < intervals; ++t) {
+            if constexpr (SPLIT) {
+                if (t < steps && t % 2 == ph) {  // first half of step t: its data is in the ring now
+                    load_planes(ring + (t % D) * L::DSLOT + lane * 16u, e, P, m4, m2, m1);
+                } else if (t >= 1 && t - 1 < steps && (t - 1) % 2 == ph) {  // second half of step t-1
+                    emit_parity<SPW, SPLIT>(p, P, e, t - 1, liveA, liveB, dA, dB, prow + ((t - 1) % NP) * L::PSLOT,
+                                            m4, m2, m1);
+                }
+            } else if (t < steps) {
+                load_planes(ring + (t % D) * L::DSLOT + lane * 16u, e, P, m4, m2, m1);
+                emit_parity<SPW, SPLIT>(p, P, e, t, liveA, liveB, dA, dB, prow + (t % NP) * L::PSLOT, m4, m2, m1);
             }
-            uint32_t O[32];
-            xn::rs84_encode_planes(P, O);
-            uint8_t* pr = prow + (s % NP) * L::PSLOT + lane * 16u;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                uint32_t w[8];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) w[i] = O[8 * r + i];
-                dma::transpose(w, m4, m2, m1);
-                const uint4 va = make_uint4(w[0], w[1], w[2], w[3]), vb = make_uint4(w[4], w[5], w[6], w[7]);
-                const uint64_t off = p.out_off[r] + (uint64_t)s * CH;
-                if (liveA) st16_nt(base + dA + off, va);
-                if (liveB) st16_nt(base + dB + off, vb);
-                *(uint4*)(pr + ((2 * e) * 4 + r) * RP) = va;
-                *(uint4*)(pr + ((2 * e + 1) * 4 + r) * RP) = vb;
-            }
-            lds_barrier();  // B(s+1): parity rows of step s published
+            if (t + 1 < intervals) lds_barrier();  // B(t+1)
         }
         return;
     }
@@ -884,7 +917,8 @@ __global__ __launch_bounds__(64 * wide::Shape<SPW>::WAVES) void k_encode_hash_wi
                 const uint8_t* g = base + src[k / 8] + p.in_off[k % 8] + (uint64_t)step * CH;
                 __builtin_amdgcn_global_load_lds(
                     (const void*)g,
-                    (__attribute__((address_space(3))) void*)(ring + (step % D) * L::DSLOT + ((2 * w + k / 8) * 8 + k % 8) * RP),
+                    (__attribute__((address_space(3))) void*)(ring + (step % D) * L::DSLOT +
+                                                              ((2 * w + k / 8) * 8 + k % 8) * RP),
                     16, 0, 2);  // non-temporal: read once
             }
         };
@@ -894,20 +928,22 @@ __global__ __launch_bounds__(64 * wide::Shape<SPW>::WAVES) void k_encode_hash_wi
         lds_barrier();  // B(0)
         const uint32_t ring_base = (uint32_t)(uintptr_t)ring;
 #pragma unroll 1
-        for (uint32_t s = 0; s < steps; ++s) {
-            dma(s + D - 1 < steps ? s + D - 1 : steps - 1);  // into the slot step s-1 used
-            uint64_t wv[32];
-            read32(ring_base + (s % D) * L::DSLOT + row_of, wv);
+        for (uint32_t t = 0; t < intervals; ++t) {
+            if (t < steps) {
+                dma(t + D - 1 < steps ? t + D - 1 : steps - 1);  // into the slot step t-1 used
+                uint64_t wv[32];
+                read32(ring_base + (t % D) * L::DSLOT + row_of, wv);
 #pragma unroll
-            for (int t = 0; t < 32; ++t) hhq_update(st, wv[t]);
-            __builtin_amdgcn_s_waitcnt(dma::vmcnt_imm((D - 2) * 16));  // DMA(s+1) landed
-            lds_barrier();  // B(s+1)
+                for (int k = 0; k < 32; ++k) hhq_update(st, wv[k]);
+                __builtin_amdgcn_s_waitcnt(dma::vmcnt_imm((D - 2) * 16));  // DMA(t+1) landed
+            }
+            if (t + 1 < intervals) lds_barrier();  // B(t+1)
         }
         __builtin_amdgcn_s_waitcnt(dma::vmcnt_imm(0));  // the clamped tail DMA has landed
         if (live) hhq_finish(st, h.out + ((s0 + stripe_l) * 12 + shard) * 32u, q);
         return;
     }
-    // ------------------- parity hasher: SPW x 4 streams, one step behind -------------------
+    // -------------- parity hasher: SPW x 4 streams, LAG steps behind the DMA --------------
     const bool on = j < (uint32_t)(SPW * 4);
     const uint32_t pj = on ? j : 0, stripe_l = pj / 4, r = pj % 4;
     const bool live = on && s0 + stripe_l < n;
@@ -915,14 +951,14 @@ __global__ __launch_bounds__(64 * wide::Shape<SPW>::WAVES) void k_encode_hash_wi
     const uint32_t prow_base = (uint32_t)(uintptr_t)prow;
     lds_barrier();  // B(0)
 #pragma unroll 1
-    for (uint32_t s = 0; s <= steps; ++s) {
-        if (s > 0) {  // parity rows of step s-1, published by B(s)
+    for (uint32_t t = 0; t < intervals; ++t) {
+        if (t >= (uint32_t)L::LAG) {  // parity rows of step t-LAG, published by B(t)
             uint64_t wv[32];
-            read32(prow_base + ((s - 1) % NP) * L::PSLOT + row_of, wv);
+            read32(prow_base + ((t - L::LAG) % NP) * L::PSLOT + row_of, wv);
 #pragma unroll
-            for (int t = 0; t < 32; ++t) hhq_update(st, wv[t]);
+            for (int k = 0; k < 32; ++k) hhq_update(st, wv[k]);
         }
-        if (s < steps) lds_barrier();  // B(s+1)
+        if (t + 1 < intervals) lds_barrier();  // B(t+1)
     }
     if (live) hhq_finish(st, h.out + ((s0 + stripe_l) * 12 + 8 + r) * 32u, q);
 }
@@ -1117,7 +1153,8 @@ const Tuning& tuning() {
         v.hash_depth = num("RSG_HASH_DEPTH", 2, 1, 3);
         if (const char* e = getenv("RSG_FUSED_KIND")) {
             const std::string k(e);
-            v.fused_kind = k == "packed" ? 1 : k == "ring" ? 2 : k == "dma" ? 3 : k == "wide2" ? 4 : k == "wide4" ? 5 : 0;
+            v.fused_kind = k == "packed" ? 1 : k == "ring" ? 2 : k == "dma" ? 3 : k == "wide2" ? 4 : k == "wide4" ? 5 :
+                          k == "split2" ? 6 : k == "split4" ? 7 : 0;
         }
         v.fused_spw1 = flag("RSG_FUSED_SPW1", false);
         v.enc_prio = num("RSG_ENC_PRIO", 0, 0, 3);
@@ -1386,17 +1423,22 @@ static bool wide_supported(const GfApplyParams& p, uint64_t shard_len, uint64_t 
 }
 
 static hipError_t launch_encode_hash_wide(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
-                                          int spw, hipStream_t stream) {
+                                          int spw, bool split, hipStream_t stream) {
     p.units = (uint32_t)(shard_len / wide::CH);
     h.n = n_stripes;
     const uint64_t blocks = (n_stripes + spw - 1) / spw;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    if (spw == 4)
-        hipLaunchKernelGGL((k_encode_hash_wide<4>), dim3((uint32_t)blocks), dim3(64 * wide::Shape<4>::WAVES), 0,
-                           stream, p, h);
+    const dim3 grid((uint32_t)blocks);
+    if (spw == 4 && split)
+        hipLaunchKernelGGL((k_encode_hash_wide<4, true>), grid, dim3(64 * wide::Shape<4, true>::WAVES), 0, stream, p, h);
+    else if (spw == 4)
+        hipLaunchKernelGGL((k_encode_hash_wide<4, false>), grid, dim3(64 * wide::Shape<4, false>::WAVES), 0, stream, p,
+                           h);
+    else if (split)
+        hipLaunchKernelGGL((k_encode_hash_wide<2, true>), grid, dim3(64 * wide::Shape<2, true>::WAVES), 0, stream, p, h);
     else
-        hipLaunchKernelGGL((k_encode_hash_wide<2>), dim3((uint32_t)blocks), dim3(64 * wide::Shape<2>::WAVES), 0,
-                           stream, p, h);
+        hipLaunchKernelGGL((k_encode_hash_wide<2, false>), grid, dim3(64 * wide::Shape<2, false>::WAVES), 0, stream, p,
+                           h);
     return hipGetLastError();
 }
 
@@ -1411,8 +1453,16 @@ hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shar
     // 1.1-3.2x (tools/kbench/ring_variants.hip);
     // Tuning::fused_kind (packed|ring|dma) forces one for A/B runs.
     const int kind = tuning().fused_kind;
-    if ((kind == 4 || kind == 5) && wide_supported(p, shard_len, n_stripes))
-        return launch_encode_hash_wide(p, h, shard_len, n_stripes, kind == 5 ? 4 : 2, stream);
+    if (kind >= 4 && kind <= 7 && wide_supported(p, shard_len, n_stripes))
+        return launch_encode_hash_wide(p, h, shard_len, n_stripes, (kind == 5 || kind == 7) ? 4 : 2, kind >= 6,
+                                       stream);
+    // RS(8,4), 512-2047 stripes (config 4's 4 and 8 MiB stripes at 4 GiB per
+    // launch): the wide kernel with split encoders, 4 stripes per workgroup
+    // from 1024 stripes (256+ workgroups), else 2; 4 MiB stripes, n = 1024:
+    // 1.27 ms against 1.77 ms for the ring kernel, 8 MiB, n = 512: 1.51 ms
+    // against 2.04 ms (profiles/r03/kind/).
+    if (kind == 0 && n_stripes >= 512 && n_stripes < 2048 && wide_supported(p, shard_len, n_stripes))
+        return launch_encode_hash_wide(p, h, shard_len, n_stripes, n_stripes >= 1024 ? 4 : 2, true, stream);
     if (kind != 1 && kind != 3 && (kind == 2 || n_stripes < 2048)) {
         uint32_t E = n_stripes <= 768 ? 2u : 1u;
         if (E == 2 && !ring_supported((int)p.C, (int)p.R, shard_len, E)) E = 1;

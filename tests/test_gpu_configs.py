@@ -4,9 +4,10 @@ Config 2: RS(8,4) encode of 1 MiB stripes at batch 4096 (6 GiB resident).
 Config 3: RS(8,4) reconstruct of that batch with 1-4 missing shards.
 Config 4: RS(8,4) encode + fused HighwayHash256S over the 64 KiB-16 MiB stripe
 sweep at SURVEY §8(d)'s sizing (n = 4 GiB / stripe), which walks every fused
-kernel the launcher picks for RS(8,4): the LDS-DMA kernel (n >= 2048), ring
-E = 1 (768 < n < 2048) and ring E = 2 with up to 1024 chunks per shard
-(S = 2 MiB).
+kernel the launcher picks for RS(8,4): the LDS-DMA kernel (n >= 2048), the
+wide kernel with split encoders (4 MiB stripes: 4 per workgroup, n = 1024;
+8 MiB: 2 per workgroup, n = 512) and ring E = 2 with 1024 chunks per shard
+(16 MiB, S = 2 MiB).
 
 The whole batch stays on the device; a sample of stripes (always the first and
 the last) is copied back and checked byte for byte — parity and all k+m
@@ -210,7 +211,7 @@ print("ok")
 """
 
 
-@pytest.mark.parametrize("kind", ["wide2", "wide4"])
+@pytest.mark.parametrize("kind", ["wide2", "wide4", "split2", "split4"])
 def test_wide_kernel_ragged_batches(gpu, oracle, kind):
     """k_encode_hash_wide (RS(8,4), few large stripes: SPW = 2 or 4 stripes
     per workgroup, 1 KiB steps, XOR-network encoder on 16 B per lane of a

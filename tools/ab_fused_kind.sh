@@ -3,15 +3,15 @@
 # launcher's choice, ring, wide2, wide4, dma) for the few-large-stripe points
 # (2, 4, 8, 16 MiB stripes, n = 4 GiB / stripe), one process per kind (the
 # kind is read once per process).  Output: gpurun_out/<TAG>/<kind>_<MiB>m.json
-# Usage: bash tools/ab_fused_kind.sh TAG [kinds...]
+# Usage: [SIZES="1 2 4 8 16"] bash tools/ab_fused_kind.sh TAG [kinds...]  (1 MiB: n = 4096)
 set -o pipefail
 TAG=${1:-ab_kind}; shift
 KINDS=${@:-auto ring wide2 wide4 dma}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-for mib in 2 4 8 16; do
+for mib in ${SIZES:-2 4 8 16}; do
   bytes=$((mib * 1024 * 1024))
-  n=$((4096 / mib))
+  n=$((4096 / mib)); [ "$n" -lt 4096 ] || n=4096
   for kind in $KINDS; do
     if [ "$kind" = auto ]; then env=""; else env="RSG_FUSED_KIND=$kind"; fi
     env $env timeout -k 10 120 python bench.py --stripe-bytes $bytes --batch $n --digests --steps 10 --warmup 3 \
