@@ -63,6 +63,8 @@ def parse(argv=None):
                     help="rehearsal only: let ranks share GPUs when fewer are visible than ranks")
     ap.add_argument("--no-config-extras", action="store_true",
                     help="skip the config 4 (fused digests) and config 5 (RS(16,4)) encode extras")
+    ap.add_argument("--record-engine", choices=["auto", "one-pass", "two-pass"], default="auto",
+                    help="GET/heal engine path for the engine extras (rsg_set_record_engine)")
     return ap.parse_args(argv)
 
 
@@ -234,13 +236,20 @@ def random_stripes(dev, k, m, S, n, seed):
     return st
 
 
-def time_encode(e, stripes, digests, stream, reps, warm=3):
+def time_encode(e, stripes, digests, stream, reps, warm=3, warm_seconds=0.3):
     """Average device time (ms) of one rsg_encode_batch_dev over `reps`
-    launches: HIP events on the launch stream around each."""
+    launches: HIP events on the launch stream around each, after `warm`
+    untimed launches continued until the device has been busy with this
+    kernel for `warm_seconds` (clock ramp after the previous extras)."""
     import torch
     for _ in range(warm):
         e.encode_batch(stripes, digests, stream=stream)
     torch.cuda.synchronize()
+    t_w = time.perf_counter()
+    while time.perf_counter() - t_w < warm_seconds:
+        for _ in range(4):
+            e.encode_batch(stripes, digests, stream=stream)
+        torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     for s, t in ev:
         s.record(stream)
@@ -295,7 +304,7 @@ def config_extras(a, e_main, stripes, k, m, dev, stream, rank):
     return out
 
 
-def engine_extras(e, stripes, k, m, S, n, stream):
+def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto"):
     """SURVEY §8(f) engines on the same device-resident batch, as BitrotWriter
     record files ([HH256S][S bytes] per block): GET all present, GET with two
     data disks lost, heal of one data + one parity disk, whole-file
@@ -354,6 +363,11 @@ def engine_extras(e, stripes, k, m, S, n, stream):
             res[name].update({"kernel_ms": round(km, 4), "frac": round(alg / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
         else:
             res[name]["frac"] = res[name]["frac_call"]
+
+    _lib.check(L.rsg_set_record_engine(ctx, {"auto": _lib.RSG_RECORD_ENGINE_AUTO,
+                                              "one-pass": _lib.RSG_RECORD_ENGINE_ONE_PASS,
+                                              "two-pass": _lib.RSG_RECORD_ENGINE_TWO_PASS}[record_engine]))
+    res["record_engine"] = record_engine
 
     def ok_get(r):
         o, status = r
@@ -494,7 +508,7 @@ def main(argv=None):
         torch.cuda.synchronize()
         extras["verify_all_ok_after_reconstruct"] = bool(ok.all().item())
         if not a.no_engines and world == 1 and not a.digests:
-            extras["engines"] = engine_extras(e, stripes, k, m, S, n, stream)
+            extras["engines"] = engine_extras(e, stripes, k, m, S, n, stream, a.record_engine)
         if not a.no_config_extras and world == 1:
             extras.update(config_extras(a, e, stripes, k, m, dev, stream, rank))
 

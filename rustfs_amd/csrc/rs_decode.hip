@@ -266,6 +266,9 @@ static bool launch_get_nf(int nf, uint64_t n_stripes, const GfApplyParams& p, co
 template <int C, int G>
 static bool launch_get_th(int nf, int th, uint64_t n_stripes, const GfApplyParams& p, const HashParams& h,
                           hipStream_t stream) {
+    if constexpr (C > 8) {  // no one-pass heal above 8 survivors (heal_dma_supported)
+        return th == 0 && launch_get_nf<C, G, 0, C>(nf, n_stripes, p, h, stream);
+    }
     switch (th) {
         case 0: return launch_get_nf<C, G, 0, C>(nf, n_stripes, p, h, stream);
         case 1: return launch_get_nf<C, G, 1, C>(nf, n_stripes, p, h, stream);
@@ -298,8 +301,12 @@ bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len) {
     return one_pass_geometry(k, m, shard_len) && nf >= k && nf < k + m;
 }
 
+// One-pass heal for k <= 8: at RS(16,4) its four GF waves per workgroup (16
+// survivors x 4 rows each) set the pace and the two-pass path is faster
+// (n = 4096, one data + one parity disk: 2.14 ms one-pass, 1.98 ms two-pass;
+// profiles/r03/eng_ab/).
 bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len) {
-    return one_pass_geometry(k, m, shard_len) && nf >= k && targets >= 1 && nf + targets <= k + m;
+    return one_pass_geometry(k, m, shard_len) && k <= 8 && nf >= k && targets >= 1 && nf + targets <= k + m;
 }
 
 static bool dma_records_aligned(const HashParams& h, int nf) {

@@ -120,9 +120,9 @@ bool fused_supported(int C, int R, uint64_t shard_len);
 bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len);
 hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int k, int m, int nf, uint64_t shard_len,
                                      uint64_t n_stripes, hipStream_t stream);
-// One-pass heal (k_decode_records_dma with target hashing), same
-// geometries: nf present source files, `targets` absent target files
-// written with digests (nf + targets <= k + m).
+// One-pass heal (k_decode_records_dma with target hashing), the same
+// geometries with k <= 8: nf present source files, `targets` absent target
+// files written with digests (nf + targets <= k + m).
 bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len);
 hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, int nf, int targets,
                                    uint64_t shard_len, uint64_t n_stripes, hipStream_t stream);
