@@ -63,7 +63,7 @@ def parse(argv=None):
                     help="rehearsal only: let ranks share GPUs when fewer are visible than ranks")
     ap.add_argument("--no-config-extras", action="store_true",
                     help="skip the config 4 (fused digests) and config 5 (RS(16,4)) encode extras")
-    ap.add_argument("--record-engine", choices=["auto", "one-pass", "two-pass", "syndrome"], default="auto",
+    ap.add_argument("--record-engine", choices=["auto", "one-pass", "two-pass"], default="auto",
                     help="GET/heal engine path for the engine extras (rsg_set_record_engine)")
     return ap.parse_args(argv)
 
@@ -366,8 +366,7 @@ def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto"):
 
     _lib.check(L.rsg_set_record_engine(ctx, {"auto": _lib.RSG_RECORD_ENGINE_AUTO,
                                               "one-pass": _lib.RSG_RECORD_ENGINE_ONE_PASS,
-                                              "two-pass": _lib.RSG_RECORD_ENGINE_TWO_PASS,
-                                              "syndrome": _lib.RSG_RECORD_ENGINE_SYNDROME}[record_engine]))
+                                              "two-pass": _lib.RSG_RECORD_ENGINE_TWO_PASS}[record_engine]))
     res["record_engine"] = record_engine
 
     def ok_get(r):

@@ -99,16 +99,14 @@ int rsg_set_kernel_timing(rsg_ctx *ctx, int on);
 int rsg_last_kernel_ms(rsg_ctx *ctx, float *ms);
 
 /* Record-engine path of rsg_decode_records_dev / rsg_heal_records_dev (no
- * reference counterpart; tests and A/B runs).  AUTO (default): a one-pass
+ * reference counterpart; tests and A/B runs).  AUTO (default): the one-pass
  * kernel from 1024 stripes where the geometry has one, else the two-pass
- * path; ONE_PASS (the table-GF one-pass kernel), SYNDROME (RS(8,4): the
- * syndrome-form one-pass kernel) and TWO_PASS force a path where the
- * geometry allows it.  Every path produces identical bytes and statuses. */
+ * path; ONE_PASS / TWO_PASS force a path where the geometry allows it.  Both
+ * paths produce identical bytes and statuses. */
 typedef enum rsg_record_engine {
     RSG_RECORD_ENGINE_AUTO = 0,
     RSG_RECORD_ENGINE_ONE_PASS = 1,
-    RSG_RECORD_ENGINE_TWO_PASS = 2,
-    RSG_RECORD_ENGINE_SYNDROME = 3
+    RSG_RECORD_ENGINE_TWO_PASS = 2
 } rsg_record_engine;
 int rsg_set_record_engine(rsg_ctx *ctx, int engine);
 

@@ -51,7 +51,6 @@ RSG_RECONSTRUCT_REENCODE_PARITY = 2
 RSG_RECORD_ENGINE_AUTO = 0
 RSG_RECORD_ENGINE_ONE_PASS = 1
 RSG_RECORD_ENGINE_TWO_PASS = 2
-RSG_RECORD_ENGINE_SYNDROME = 3
 
 # Every symbol include/rsgpu.h declares (checked by tests/test_abi.py).
 EXPORTED = (

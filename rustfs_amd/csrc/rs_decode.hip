@@ -10,8 +10,6 @@
 
 namespace rsg {
 
-#include "rs84_xornet.h"  // generated (tools/gen_xornet.py); uses x3
-
 // ---------------------------------------------------------------------------
 // One-pass degraded GET (rsg_decode_records_dev, a data disk lost) for
 // RS(k, m) with k in {2, 4, 8, 16} and m <= 4: every present record of G
@@ -339,317 +337,6 @@ hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int k, int m
     p.units = (uint32_t)(shard_len / dma::CH);
     h.n = n_stripes;
     if (!launch_get_any(k, nf, 0, n_stripes, p, h, stream)) return hipErrorInvalidValue;
-    return hipGetLastError();
-}
-
-
-// ---------------------------------------------------------------------------
-// One-pass GET / heal for RS(8,4) in syndrome form (rsg_decode_records_dev /
-// rsg_heal_records_dev with a lost disk; SynParams in rs_kernels.h).  The
-// table kernel above spends ~435 VALU per stripe-step on its run-time GF
-// rows (8 survivors x 4 rows) and heal runs 86 % VALU-busy
-// (profiles/r03/pmc_engines/).  Here, per stripe:
-//   E   = encode network (rs84_xornet.h) over the present data (absent = 0)
-//   V_j = E_j ^ parity_j for every present parity j (its syndrome)
-//   lost data d = sum_i A^-1[d][i] V_{Ps_i}  (Ps = the first e present
-//         parities: with the present data, exactly the reference's first-k
-//         survivors, so the same linear system and the same bytes)
-//   parity target j = E_j ^ (P_j[lost] A^-1) V_Ps;  surplus parity j is
-//         consistent iff V_j == (P_j[lost] A^-1) V_Ps
-// so the run-time GF covers only e <= 4 syndrome inputs.  Layout of
-// k_encode_hash_wide: 4 stripes per workgroup, 1 KiB steps, present records
-// LDS-DMA'd into a 3-slot ring by the hash waves (which verify every record
-// straight from the ring), and two GF waves per stripe pair on alternate
-// steps (16 B of each stripe per lane: read + bit-transpose in the interval
-// the step is in the ring, network + syndromes + stores in the next).  Heal
-// target rows go through a double-buffered LDS area to target hashers in
-// the same waves (quads past the verify streams), two steps behind.
-namespace syn {
-constexpr uint32_t CH = 1024, RP = CH + 32;
-constexpr int D = 3, NP = 2, G = 4, LAG = 2;
-template <int NF, int TH>
-struct Shape {
-    static constexpr int NV = 4 * NF, NT = 4 * TH, NS = NV + NT;
-    static constexpr int HW = (NS + 15) / 16;               // hash waves
-    static constexpr int GW = 4;                            // GF waves: 2 stripe pairs x 2 phases
-    static constexpr int WAVES = GW + HW;
-    static constexpr int VW = (NV + 15) / 16;               // hash waves that own DMA rows
-    static constexpr int LASTV = NV - 16 * (VW - 1);        // rows of the last of them
-    static constexpr uint32_t DSLOT = NV * RP;              // ring row g = file * 4 + stripe
-    static constexpr uint32_t TSLOT = (TH ? NT : 1) * RP;   // target row t * 4 + stripe
-    static constexpr uint32_t LDS = D * DSLOT + (TH ? NP * TSLOT : 0);
-};
-// w = V[j] for a wave-uniform j
-__device__ __forceinline__ void pick(const uint32_t (&V)[4][8], uint32_t j, uint32_t (&w)[8]) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) w[i] = j == 0 ? V[0][i] : j == 1 ? V[1][i] : j == 2 ? V[2][i] : V[3][i];
-}
-}  // namespace syn
-
-template <int NF, int TH, bool COPY>
-__global__ __launch_bounds__((64 * syn::Shape<NF, TH>::WAVES)) void k_records_syn(const SynParams p,
-                                                                                  const HashParams h) {
-    using namespace syn;
-    using L = Shape<NF, TH>;
-    static_assert(NF >= 8 && NF + TH <= 12 && TH <= 4 && (TH == 0 || !COPY), "RS(8,4)");
-    __shared__ __attribute__((aligned(16))) uint8_t lds[L::LDS];
-    __shared__ __attribute__((aligned(16))) uint8_t tabs[4 * 4 * 32];
-    __shared__ uint32_t vbad[G];
-    uint8_t* const ring = lds;
-    uint8_t* const trow = lds + D * L::DSLOT;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u, q = lane & 3u;
-    const uint64_t n = h.n;
-    const uint32_t steps = p.units;
-    const uint64_t s0 = (uint64_t)blockIdx.x * G;
-    const uint32_t intervals = steps + LAG;  // interval t: between B(t) and B(t+1)
-    for (uint32_t i = threadIdx.x; i < 16; i += blockDim.x) {
-        const int r = i / 4, c = i % 4;
-        *(uint4*)(tabs + i * 32) = make_uint4(p.tab[r][c][0], p.tab[r][c][1], p.tab[r][c][2], p.tab[r][c][3]);
-        *(uint32_t*)(tabs + i * 32 + 16) = p.tab[r][c][4];
-    }
-    if (threadIdx.x < G) vbad[threadIdx.x] = 0;
-    // (tables and verdict slots are published by B(0))
-
-    if (wave < (uint32_t)L::GW) {
-        // --------------------- GF wave: stripe pair e, steps t % 2 == ph ---------------------
-        if (p.wave_prio & kPrioGf) __builtin_amdgcn_s_setprio(2);
-        const uint32_t e = wave / 2, ph = wave % 2;
-        const bool liveA = s0 + 2 * e < n, liveB = s0 + 2 * e + 1 < n;
-        const uint64_t oA = (liveA ? s0 + 2 * e : 0) * p.out_stripe_stride + lane * 16u;
-        const uint64_t oB = (liveB ? s0 + 2 * e + 1 : 0) * p.out_stripe_stride + lane * 16u;
-        const uint32_t m4 = vgpr_const(0x0f0f0f0fu), m2 = vgpr_const(0x33333333u), m1 = vgpr_const(0x55555555u);
-        const uint32_t m7 = vgpr_const(0x07070707u), m3 = vgpr_const(0x03030303u);
-        const uint32_t R = p.R, nst = p.n_store, ne = p.e;
-        uint32_t P[64], PR[4][8];
-        bool badA = false, badB = false;
-        lds_barrier();  // B(0)
-#pragma unroll 1
-        for (uint32_t t = 0; t < intervals; ++t) {
-            if (t < steps && t % 2 == ph) {
-                // first half of step t: its records are in the ring during this interval only
-                const uint8_t* slot = ring + (t % D) * L::DSLOT + lane * 16u;
-#pragma unroll
-                for (int c = 0; c < 8; ++c) {
-                    const uint32_t f = p.data_row[c];  // wave-uniform
-                    if (f == kSynAbsent) {
-#pragma unroll
-                        for (int j = 0; j < 8; ++j) P[8 * c + j] = 0u;
-                        continue;
-                    }
-                    const uint4 a = *(const uint4*)(slot + (f * 4 + 2 * e) * RP);
-                    const uint4 b = *(const uint4*)(slot + (f * 4 + 2 * e + 1) * RP);
-                    if constexpr (COPY) {  // GET: present data copied through to the output
-                        if ((p.copy_mask >> c) & 1u) {
-                            if (liveA) st16_nt(p.out_base + oA + p.copy_off[c] + (uint64_t)t * CH, a);
-                            if (liveB) st16_nt(p.out_base + oB + p.copy_off[c] + (uint64_t)t * CH, b);
-                        }
-                    }
-                    uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-                    dma::transpose(w, m4, m2, m1);
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) P[8 * c + j] = w[j];
-                }
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint32_t f = p.par_row[j];
-                    if (f == kSynAbsent) continue;
-                    const uint4 a = *(const uint4*)(slot + (f * 4 + 2 * e) * RP);
-                    const uint4 b = *(const uint4*)(slot + (f * 4 + 2 * e + 1) * RP);
-                    PR[j][0] = a.x; PR[j][1] = a.y; PR[j][2] = a.z; PR[j][3] = a.w;
-                    PR[j][4] = b.x; PR[j][5] = b.y; PR[j][6] = b.z; PR[j][7] = b.w;
-                }
-            } else if (t >= 1 && t - 1 < steps && (t - 1) % 2 == ph) {
-                // second half of step st = t - 1
-                const uint32_t st = t - 1;
-                uint32_t O[32];
-                xn::rs84_encode_planes(P, O);
-                uint32_t V[4][8];  // E_j back in bytes; for a present parity its syndrome V_j
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) V[j][i] = 0u;
-                    if (!((p.need_e >> j) & 1u)) continue;  // wave-uniform
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) V[j][i] = O[8 * j + i];
-                    dma::transpose(V[j], m4, m2, m1);
-                    if (p.par_row[j] != kSynAbsent) {
-#pragma unroll
-                        for (int i = 0; i < 8; ++i) V[j][i] ^= PR[j][i];
-                    }
-                }
-                uint32_t acc[4][8];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) acc[r][i] = 0u;
-                    if ((uint32_t)r < nst && p.base[r] != kSynAbsent) syn::pick(V, p.base[r], acc[r]);
-                }
-                uint32_t tz;  // opaque zero: table reads stay at their use
-                asm volatile("s_mov_b32 %0, 0" : "=s"(tz));
-                const uint8_t* tb = tabs + tz;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if ((uint32_t)i >= ne) break;  // wave-uniform
-                    uint32_t x[8];
-                    syn::pick(V, p.syn_par[i], x);
-#pragma unroll
-                    for (int d = 0; d < 8; ++d) {
-                        const uint32_t sa = x[d] & m7, sb = (x[d] >> 3) & m7, sc = (x[d] >> 6) & m3;
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            if ((uint32_t)r >= R) break;
-                            const uint8_t* tp = tb + (r * 4 + i) * 32;
-                            const uint4 t4 = *(const uint4*)tp;
-                            const uint32_t t2 = *(const uint32_t*)(tp + 16);
-                            acc[r][d] = x3(acc[r][d], __builtin_amdgcn_perm(t4.y, t4.x, sa),
-                                           __builtin_amdgcn_perm(t4.w, t4.z, sb)) ^
-                                        __builtin_amdgcn_perm(t2, t2, sc);
-                        }
-                    }
-                }
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    if ((uint32_t)r >= R) break;
-                    if ((uint32_t)r < nst) {
-                        const uint4 va = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
-                        const uint4 vb = make_uint4(acc[r][4], acc[r][5], acc[r][6], acc[r][7]);
-                        if (liveA) st16_nt(p.out_base + oA + p.out_off[r] + (uint64_t)st * CH, va);
-                        if (liveB) st16_nt(p.out_base + oB + p.out_off[r] + (uint64_t)st * CH, vb);
-                        if constexpr (TH > 0) {
-                            uint8_t* tr = trow + (st % NP) * L::TSLOT + lane * 16u;
-                            *(uint4*)(tr + (r * 4 + 2 * e) * RP) = va;
-                            *(uint4*)(tr + (r * 4 + 2 * e + 1) * RP) = vb;
-                        }
-                    } else {
-                        uint32_t v[8];
-                        syn::pick(V, p.base[r], v);
-                        badA |= ((acc[r][0] ^ v[0]) | (acc[r][1] ^ v[1]) | (acc[r][2] ^ v[2]) | (acc[r][3] ^ v[3])) != 0u;
-                        badB |= ((acc[r][4] ^ v[4]) | (acc[r][5] ^ v[5]) | (acc[r][6] ^ v[6]) | (acc[r][7] ^ v[7])) != 0u;
-                    }
-                }
-            }
-            if (t + 1 < intervals) lds_barrier();  // B(t+1)
-        }
-        // the pair's surplus verdict over both phase waves' steps
-        const bool anyA = __builtin_amdgcn_ballot_w64(badA) != 0, anyB = __builtin_amdgcn_ballot_w64(badB) != 0;
-        if (lane == 0 && (anyA || anyB)) atomicOr(&vbad[2 * e], (anyA ? 1u : 0u) | (anyB ? 2u : 0u));
-        lds_barrier();  // final: both phases' verdicts in vbad
-        if (ph == 0 && nst < R && lane == 0) {
-            const uint32_t b = vbad[2 * e];
-            if (liveA) p.ok_flags[s0 + 2 * e] = (b & 1u) ? 0 : 1;
-            if (liveB) p.ok_flags[s0 + 2 * e + 1] = (b & 2u) ? 0 : 1;
-        }
-        return;
-    }
-    // ----------------- hash wave: record DMA + verify streams, then target streams -----------------
-    if (p.wave_prio & kPrioHash) __builtin_amdgcn_s_setprio(2);
-    const uint32_t w = wave - L::GW, g = 16 * w + (lane >> 2);
-    const bool is_v = g < (uint32_t)L::NV, is_t = !is_v && g < (uint32_t)L::NS;
-    const uint32_t gv = is_v ? g : 0, gt = is_t ? g - L::NV : 0;
-    const uint32_t sl = is_v ? gv % 4 : gt % 4;  // local stripe of this quad's stream
-    const bool live = (is_v || is_t) && s0 + sl < n;
-    const int cnt = (int)w < L::VW - 1 ? 16 : (int)w == L::VW - 1 ? L::LASTV : 0;  // DMA rows of this wave
-    HHQuad st;
-    hhq_init(st, h.key, q);
-    uint64_t dsrc[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint64_t sg = s0 + i;
-        dsrc[i] = (sg < n ? sg : 0) * h.stripe_stride + lane * 16u;
-    }
-    auto dma = [&](uint32_t step) {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            if (k >= cnt) break;  // wave-uniform
-            const uint32_t row = 16 * w + k;  // file row / 4, stripe k % 4
-            const uint8_t* src = h.base[row / 4] + dsrc[k % 4] + (uint64_t)step * CH;
-            __builtin_amdgcn_global_load_lds(
-                (const void*)src, (__attribute__((address_space(3))) void*)(ring + (step % D) * L::DSLOT + row * RP),
-                16, 0, 2);  // non-temporal: read once
-        }
-    };
-    auto wait_next = [&]() {  // DMA of the next step landed (D - 2 steps younger in flight)
-        if (cnt == 16) __builtin_amdgcn_s_waitcnt(dma::vmcnt_imm((D - 2) * 16));
-        else if (cnt == L::LASTV) __builtin_amdgcn_s_waitcnt(dma::vmcnt_imm((D - 2) * L::LASTV));
-    };
-    if (cnt > 0) {
-#pragma unroll
-        for (int d = 0; d < D - 1; ++d) dma(d < (int)steps ? d : steps - 1);
-        wait_next();  // DMA(0) landed
-    }
-    lds_barrier();  // B(0)
-    const uint32_t ring_base = (uint32_t)(uintptr_t)ring, trow_base = (uint32_t)(uintptr_t)trow;
-#pragma unroll 1
-    for (uint32_t t = 0; t < intervals; ++t) {
-        if (t < steps && cnt > 0) dma(t + D - 1 < steps ? t + D - 1 : steps - 1);  // into the slot step t-1 used
-        if (is_v && t < steps) {
-            uint64_t wv[32];
-            dma::read32(ring_base + (t % D) * L::DSLOT + gv * RP + 8 * q, wv);
-#pragma unroll
-            for (int k = 0; k < 32; ++k) hhq_update(st, wv[k]);
-        } else if (TH > 0 && is_t && t >= (uint32_t)LAG) {  // target rows of step t - LAG, published by B(t)
-            uint64_t wv[32];
-            dma::read32(trow_base + ((t - LAG) % NP) * L::TSLOT + gt * RP + 8 * q, wv);
-#pragma unroll
-            for (int k = 0; k < 32; ++k) hhq_update(st, wv[k]);
-        }
-        if (t < steps && cnt > 0) wait_next();
-        if (t + 1 < intervals) lds_barrier();  // B(t+1)
-    }
-    lds_barrier();  // final (the GF waves' verdict barrier)
-    __builtin_amdgcn_s_waitcnt(dma::vmcnt_imm(0));  // the clamped tail DMA has landed
-    const uint64_t dg = hhq_digest(st, q);
-    // verify before use (split_and_verify, bitrot.rs:227-247): each record's flag written whole
-    bool mis = false;
-    if (is_v && live) mis = dg != ld64_any(h.base[gv / 4] + (s0 + sl) * h.stripe_stride - 32 + 8 * q);
-    const uint64_t bal = __builtin_amdgcn_ballot_w64(mis);
-    if (is_v && live && q == 0) h.flag_base[gv / 4][s0 + sl] = ((bal >> lane) & 0xFull) ? 0 : 1;
-    if (TH > 0 && is_t && live) {  // target record header (BitrotWriter::write)
-        uint8_t* hd = p.out_base + (s0 + sl) * p.out_stripe_stride + p.out_off[gt / 4] - 32;
-#pragma unroll
-        for (int b = 0; b < 8; ++b) hd[8 * q + b] = (uint8_t)(dg >> (8 * b));
-    }
-}
-
-bool syn_supported(int k, int m, int nf, int targets, uint64_t shard_len) {
-    return k == 8 && m == 4 && nf >= 8 && targets >= 0 && targets <= 4 && nf + targets <= 12 &&
-           (targets > 0 || nf < 12) && shard_len >= syn::CH && shard_len % syn::CH == 0 &&
-           shard_len / syn::CH <= 0xffffffffull;
-}
-
-template <int NF, int TH, bool COPY>
-static void launch_syn(uint64_t blocks, const SynParams& p, const HashParams& h, hipStream_t stream) {
-    hipLaunchKernelGGL((k_records_syn<NF, TH, COPY>), dim3((uint32_t)blocks), dim3(64 * syn::Shape<NF, TH>::WAVES),
-                       0, stream, p, h);
-}
-
-hipError_t launch_records_syn(SynParams p, HashParams h, int nf, int targets, bool copy, uint64_t n_stripes,
-                              hipStream_t stream) {
-    const uint64_t shard_len = (uint64_t)p.units * syn::CH;
-    if (!syn_supported(8, 4, nf, targets, shard_len) || n_stripes == 0 || p.R > 4 || p.n_store > p.R || p.e > 4 ||
-        (copy && targets) || !dma_records_aligned(h, nf))
-        return hipErrorInvalidValue;
-    p.wave_prio = dma_prio();
-    h.n = n_stripes;
-    const uint64_t blocks = (n_stripes + syn::G - 1) / syn::G;
-    if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    switch (targets * 16 + nf) {
-        case 0 * 16 + 8: copy ? launch_syn<8, 0, true>(blocks, p, h, stream) : launch_syn<8, 0, false>(blocks, p, h, stream); break;
-        case 0 * 16 + 9: copy ? launch_syn<9, 0, true>(blocks, p, h, stream) : launch_syn<9, 0, false>(blocks, p, h, stream); break;
-        case 0 * 16 + 10: copy ? launch_syn<10, 0, true>(blocks, p, h, stream) : launch_syn<10, 0, false>(blocks, p, h, stream); break;
-        case 0 * 16 + 11: copy ? launch_syn<11, 0, true>(blocks, p, h, stream) : launch_syn<11, 0, false>(blocks, p, h, stream); break;
-        case 1 * 16 + 8: launch_syn<8, 1, false>(blocks, p, h, stream); break;
-        case 1 * 16 + 9: launch_syn<9, 1, false>(blocks, p, h, stream); break;
-        case 1 * 16 + 10: launch_syn<10, 1, false>(blocks, p, h, stream); break;
-        case 1 * 16 + 11: launch_syn<11, 1, false>(blocks, p, h, stream); break;
-        case 2 * 16 + 8: launch_syn<8, 2, false>(blocks, p, h, stream); break;
-        case 2 * 16 + 9: launch_syn<9, 2, false>(blocks, p, h, stream); break;
-        case 2 * 16 + 10: launch_syn<10, 2, false>(blocks, p, h, stream); break;
-        case 3 * 16 + 8: launch_syn<8, 3, false>(blocks, p, h, stream); break;
-        case 3 * 16 + 9: launch_syn<9, 3, false>(blocks, p, h, stream); break;
-        case 4 * 16 + 8: launch_syn<8, 4, false>(blocks, p, h, stream); break;
-        default: return hipErrorInvalidValue;
-    }
     return hipGetLastError();
 }
 

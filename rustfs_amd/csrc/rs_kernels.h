@@ -39,7 +39,6 @@ struct Tuning {
     int dma_nt = 3;               // RSG_DMA_NT=<0..3>: non-temporal loads (bit 0) / stores (bit 1)
     int dma_spw = 8;              // RSG_DMA_SPW=4: four stripes per fused DMA workgroup
     int get_prio = 2;             // RSG_DMA_PRIO=<0..3>: wave priorities of the one-pass GET/heal
-    bool syn = false;             // RSG_SYN=1: RS(8,4) one-pass GET/heal in syndrome form by default
     // fault injection (tests only): RSG_TEST_FAIL_SUBBATCH=<i> makes sub-batch
     // i of every rsg_encode_batch_host_submit fail to enqueue (-1: never)
     int test_fail_subbatch = -1;
@@ -129,36 +128,6 @@ hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, 
                                    uint64_t shard_len, uint64_t n_stripes, hipStream_t stream);
 hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                     hipStream_t stream);
-
-// One-pass GET / heal for RS(8,4) in syndrome form (k_records_syn,
-// rs_decode.hip): the present data go through the compile-time encode
-// network, V_j = E_j ^ parity_j is each present parity's syndrome, and
-// every output is a run-time GF combination of the e survivor-parity
-// syndromes (e = lost data shards) — the same linear system the survivors
-// define, so bit-identical to the table kernel.  Host plan in rsgpu.cpp.
-constexpr uint32_t kSynAbsent = 0xFFu;
-struct SynParams {
-    uint8_t* out_base;           // stores: out_base + stripe*out_stripe_stride + out_off[r] (+ column)
-    uint64_t out_stripe_stride;
-    uint64_t out_off[4];         // store rows (targets / lost data), r < n_store
-    uint64_t copy_off[8];        // GET: present data shard c copied to out (bit c of copy_mask)
-    uint32_t copy_mask;
-    uint32_t data_row[8];        // data shard c: its present-file index, or kSynAbsent
-    uint32_t par_row[4];         // parity j (shard 8+j): its present-file index, or kSynAbsent
-    uint32_t need_e;             // bit j: E_j in byte form is needed (present parity j, or a parity target)
-    uint32_t e;                  // survivor-parity syndromes (= lost data shards), <= 4
-    uint32_t syn_par[4];         // syndrome i is V of parity syn_par[i]
-    uint32_t R, n_store;         // rows; rows r < n_store store, rows r >= n_store compare
-    uint32_t base[4];            // store row r: value starts from E_base[r] (parity target) or 0 (kSynAbsent);
-                                 // compare row r: compared against V_base[r]
-    uint32_t tab[4][4][5];       // row r, syndrome i: v_perm tables (coef_tables)
-    uint8_t* ok_flags;           // compare rows: stripe verdict (written whole)
-    uint32_t units;              // S / 1024
-    uint32_t wave_prio;
-};
-bool syn_supported(int k, int m, int nf, int targets, uint64_t shard_len);
-hipError_t launch_records_syn(SynParams p, HashParams h, int nf, int targets, bool copy, uint64_t n_stripes,
-                              hipStream_t stream);
 
 // Ring variant (one stripe per workgroup, E encoder waves, E KiB chunks,
 // double-buffered LDS rows) for batches of few large stripes.  Requires

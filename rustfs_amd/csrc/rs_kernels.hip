@@ -493,6 +493,30 @@ void k_encode_hash_fused(const GfApplyParams p,
 // read with asm ds_read_b64 (the compiler adds no vmcnt(0) for them).  Dead
 // stripes (past n) re-read stripe 0 and store nothing.
 namespace dma {
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+}
+
+// 8x8 bit transpose of 8 dwords (bs::transpose) with two shifts and two
+// v_bfi_b32 per masked swap; its own inverse
+__device__ __forceinline__ void swap_bfi(uint32_t& lo, uint32_t& hi, int s, uint32_t mask) {
+    const uint32_t a = lo, b = hi;
+    lo = bfi(mask, a, b << s);
+    hi = bfi(mask, a >> s, b);
+}
+__device__ __forceinline__ void transpose(uint32_t (&w)[8], uint32_t m4, uint32_t m2, uint32_t m1) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) swap_bfi(w[d], w[d + 4], 4, m4);
+    swap_bfi(w[0], w[2], 2, m2);
+    swap_bfi(w[1], w[3], 2, m2);
+    swap_bfi(w[4], w[6], 2, m2);
+    swap_bfi(w[5], w[7], 2, m2);
+#pragma unroll
+    for (int d = 0; d < 8; d += 2) swap_bfi(w[d], w[d + 1], 1, m1);
+}
+
 // acc[r][i] (^)= XOR of the planes P[c][j] with bit j of mask[R0+r][C0+c][i]
 // (rows [R0, R0+RN), shards [C0, C0+NC)), folded two terms at a time by
 // the three-input XOR.
@@ -782,7 +806,13 @@ struct Shape {
     static constexpr uint32_t LDS = D * DSLOT + NP * PSLOT;
     static constexpr int LAG = SPLIT ? 2 : 1;        // steps the parity hasher trails the DMA
 };
-using dma::read32;
+// 32 packets of one stream (8 B per lane, 32 B apart) from LDS
+__device__ __forceinline__ void read32(uint32_t a, uint64_t (&w)[32]) {
+    uint64_t (&lo)[16] = *reinterpret_cast<uint64_t(*)[16]>(&w[0]);
+    uint64_t (&hi)[16] = *reinterpret_cast<uint64_t(*)[16]>(&w[16]);
+    dma::read16(a, lo);
+    dma::read16(a + 512, hi);
+}
 // Planes of stripe pair e (16 B of each per lane) from a ring slot.
 __device__ __forceinline__ void load_planes(const uint8_t* slot, uint32_t e, uint32_t (&P)[64], uint32_t m4,
                                             uint32_t m2, uint32_t m1) {
@@ -1132,7 +1162,6 @@ const Tuning& tuning() {
         v.dma_nt = num("RSG_DMA_NT", 3, 0, 3);
         v.dma_spw = num("RSG_DMA_SPW", 8, 4, 8) == 4 ? 4 : 8;
         v.get_prio = num("RSG_DMA_PRIO", 2, 0, 3);
-        v.syn = flag("RSG_SYN", false);
         v.test_fail_subbatch = num("RSG_TEST_FAIL_SUBBATCH", -1, 0, 1 << 30);
         return v;
     }();

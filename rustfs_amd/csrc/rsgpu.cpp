@@ -1214,15 +1214,6 @@ int verify_gather(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64_t n, co
     return flags_to_host(ctx, d_flags + (size_t)k * n, (size_t)m * n, flags.data() + (size_t)k * n, s);
 }
 
-// The syndrome-form one-pass kernel (k_records_syn, RS(8,4)) instead of the
-// table kernel: forced by RSG_RECORD_ENGINE_SYNDROME / ONE_PASS, by default
-// per Tuning::syn.
-bool syn_enabled(const rsg_ctx* ctx) {
-    if (ctx->record_engine == RSG_RECORD_ENGINE_SYNDROME) return true;
-    if (ctx->record_engine == RSG_RECORD_ENGINE_ONE_PASS) return false;
-    return rsg::tuning().syn;
-}
-
 // One-pass GET/heal (k_decode_records_dma) for a batch of n stripes.  A
 // workgroup walks its 8 stripes front to back (~0.6 ms for 1 MiB RS(8,4)
 // stripes), so below ~1024 stripes, where the grid does not fill the CUs,
@@ -1231,8 +1222,7 @@ bool syn_enabled(const rsg_ctx* ctx) {
 // record-engine setting (rsg_set_record_engine: tests and A/B runs) forces
 // either path.
 bool get_dma_enabled(const rsg_ctx* ctx, uint64_t n) {
-    if (ctx->record_engine == RSG_RECORD_ENGINE_ONE_PASS || ctx->record_engine == RSG_RECORD_ENGINE_SYNDROME)
-        return true;
+    if (ctx->record_engine == RSG_RECORD_ENGINE_ONE_PASS) return true;
     if (ctx->record_engine == RSG_RECORD_ENGINE_TWO_PASS) return false;
     return n >= 1024;
 }
@@ -1356,151 +1346,6 @@ int launch_heal_one_pass(Codec& cd, const std::vector<uint8_t>& present, const s
                                      shard_len, n, s));
 }
 
-// Syndrome-form plan (k_records_syn, RS(8,4)) for the erasure pattern
-// `present` (files = the present shard indices, ascending): stores =
-// the shards to write (GET: the lost data; heal: the targets, all absent
-// from the sources), then (compare_surplus) one compare row per present
-// parity that is not a survivor.  Survivors are the present data plus the
-// first e present parities (e = lost data shards): the reference's first k
-// present shards, so the rows solve the same system as plan_row.
-int plan_syn(const Codec& cd, const std::vector<uint8_t>& present, const std::vector<int>& files,
-             const std::vector<int>& stores, bool compare_surplus, rsg::SynParams& sp) {
-    const int k = cd.k, m = cd.m;
-    if (k != 8 || m != 4) return RSG_ERR_UNSUPPORTED;
-    const Gf& g = gf();
-    std::memset(&sp, 0, sizeof(sp));
-    for (int c = 0; c < 8; ++c) sp.data_row[c] = rsg::kSynAbsent;
-    for (int j = 0; j < 4; ++j) sp.par_row[j] = rsg::kSynAbsent;
-    for (int b = 0; b < 4; ++b) sp.base[b] = rsg::kSynAbsent;
-    for (size_t f = 0; f < files.size(); ++f) {
-        if (files[f] < 8) sp.data_row[files[f]] = (uint32_t)f;
-        else sp.par_row[files[f] - 8] = (uint32_t)f;
-    }
-    std::vector<int> lost, pp;  // lost data (ascending), present parity (ascending)
-    for (int c = 0; c < 8; ++c)
-        if (!present[c]) lost.push_back(c);
-    for (int j = 0; j < 4; ++j)
-        if (present[8 + j]) pp.push_back(j);
-    const int e = (int)lost.size();
-    if ((int)pp.size() < e) return RSG_ERR_TOO_FEW_SHARDS;
-    // V_{Ps_i} = sum_jj P[Ps_i][lost_jj] d_{lost_jj}: A (e x e), d = A^-1 V
-    Mat a((size_t)e * e);
-    for (int i = 0; i < e; ++i)
-        for (int jj = 0; jj < e; ++jj) a[(size_t)i * e + jj] = cd.matrix[(size_t)(8 + pp[i]) * 8 + lost[jj]];
-    if (e && !invert(e, a)) return RSG_ERR_TOO_FEW_SHARDS;  // a is now A^-1: d_jj = sum_i a[jj][i] V_i
-    sp.e = (uint32_t)e;
-    for (int i = 0; i < e; ++i) sp.syn_par[i] = (uint32_t)pp[i];
-    // coefficients over the syndromes of parity row j restricted to the lost data: P_j[lost] A^-1
-    auto parity_coefs = [&](int j, uint8_t* out) {
-        for (int i = 0; i < e; ++i) {
-            uint8_t acc = 0;
-            for (int jj = 0; jj < e; ++jj) acc ^= g.mul(cd.matrix[(size_t)(8 + j) * 8 + lost[jj]], a[(size_t)jj * e + i]);
-            out[i] = acc;
-        }
-    };
-    int R = 0;
-    std::vector<uint8_t> coef(16, 0);
-    auto add_row = [&](const uint8_t* c, uint32_t base) {
-        for (int i = 0; i < e; ++i) coef_tables(c[i], sp.tab[R][i]);
-        sp.base[R] = base;
-        ++R;
-    };
-    uint32_t need = 0;
-    for (int j : pp) need |= 1u << j;
-    for (int x : stores) {
-        if (R >= 4) return RSG_ERR_UNSUPPORTED;
-        uint8_t c[4] = {0, 0, 0, 0};
-        if (x < 8) {
-            const auto it = std::find(lost.begin(), lost.end(), x);
-            if (it == lost.end()) return RSG_ERR_INVALID_ARG;  // a store target must be absent
-            const int jj = (int)(it - lost.begin());
-            for (int i = 0; i < e; ++i) c[i] = a[(size_t)jj * e + i];
-            add_row(c, rsg::kSynAbsent);
-        } else {
-            if (present[x]) return RSG_ERR_INVALID_ARG;
-            parity_coefs(x - 8, c);
-            add_row(c, (uint32_t)(x - 8));
-            need |= 1u << (x - 8);
-        }
-    }
-    sp.n_store = (uint32_t)R;
-    if (compare_surplus)
-        for (size_t i = (size_t)e; i < pp.size(); ++i) {
-            if (R >= 4) return RSG_ERR_UNSUPPORTED;
-            uint8_t c[4] = {0, 0, 0, 0};
-            parity_coefs(pp[i], c);
-            add_row(c, (uint32_t)pp[i]);
-        }
-    sp.R = (uint32_t)R;
-    sp.need_e = need;
-    return RSG_OK;
-}
-
-// The record view of the present files for the DMA kernels (h.base: record
-// 0 body of present file f, flags per file).
-void record_hash_params(const std::vector<int>& files, const uint8_t* const* d_files, uint8_t* d_flags, uint64_t n,
-                        uint64_t shard_len, const uint64_t* key, rsg::HashParams& h) {
-    std::memset(&h, 0, sizeof(h));
-    h.len = shard_len;
-    h.stripe_stride = 32 + shard_len;
-    std::memcpy(h.key, key, sizeof(h.key));
-    h.nbases = (uint32_t)files.size();
-    h.digest_off = -32;
-    for (size_t f = 0; f < files.size(); ++f) {
-        h.base[f] = d_files[files[f]] + 32;
-        h.flag_base[f] = d_flags + (size_t)files[f] * n;
-    }
-}
-
-// Syndrome-form one-pass GET (see plan_syn): lost data to d_out, present
-// data copied through, surplus parity compared (verify_surplus).
-int launch_get_syn(Codec& cd, const std::vector<uint8_t>& present, const std::vector<int>& files,
-                   const uint8_t* const* d_files, uint8_t* d_flags, uint8_t* d_ok, int k, uint64_t shard_len,
-                   uint64_t n, const uint64_t* key, bool verify_surplus, uint8_t* d_out, bool& any_verify,
-                   hipStream_t s) {
-    std::vector<int> lost;
-    for (int c = 0; c < k; ++c)
-        if (!present[c]) lost.push_back(c);
-    rsg::SynParams sp;
-    int st = plan_syn(cd, present, files, lost, verify_surplus, sp);
-    if (st) return st;
-    sp.out_base = d_out;
-    sp.out_stripe_stride = (uint64_t)k * shard_len;
-    for (size_t r = 0; r < lost.size(); ++r) sp.out_off[r] = (uint64_t)lost[r] * shard_len;
-    for (int c = 0; c < k; ++c)
-        if (present[c]) {
-            sp.copy_mask |= 1u << c;
-            sp.copy_off[c] = (uint64_t)c * shard_len;
-        }
-    sp.ok_flags = d_ok;
-    sp.units = (uint32_t)(shard_len / 1024);
-    if (sp.R > sp.n_store) any_verify = true;
-    rsg::HashParams h;
-    record_hash_params(files, d_files, d_flags, n, shard_len, key, h);
-    return hip_status(rsg::launch_records_syn(sp, h, (int)files.size(), 0, true, n, s));
-}
-
-// Syndrome-form one-pass heal: every target record (body + digest), the
-// surplus parity compared (heal.rs:180-196).
-int launch_heal_syn(Codec& cd, const std::vector<uint8_t>& present, const std::vector<int>& files,
-                    const std::vector<int>& targets, const uint8_t* const* d_files, uint8_t* const* d_targets,
-                    uint8_t* d_flags, uint8_t* d_ok, uint64_t shard_len, uint64_t n, const uint64_t* key,
-                    bool& any_verify, hipStream_t s) {
-    rsg::SynParams sp;
-    int st = plan_syn(cd, present, files, targets, true, sp);
-    if (st) return st;
-    sp.out_base = d_targets[targets[0]] + 32;
-    sp.out_stripe_stride = 32 + shard_len;
-    for (size_t r = 0; r < targets.size(); ++r)
-        sp.out_off[r] = (uint64_t)(uintptr_t)(d_targets[targets[r]] + 32) - (uint64_t)(uintptr_t)sp.out_base;
-    sp.ok_flags = d_ok;
-    sp.units = (uint32_t)(shard_len / 1024);
-    if (sp.R > sp.n_store) any_verify = true;
-    rsg::HashParams h;
-    record_hash_params(files, d_files, d_flags, n, shard_len, key, h);
-    return hip_status(rsg::launch_records_syn(sp, h, (int)files.size(), (int)targets.size(), false, n, s));
-}
-
 // GET engine body (ctx->mu held): verify records, copy/rebuild the k data
 // shards of every stripe into d_out (n x k*S), optional surplus-parity check.
 // Uses ctx->d_scratch[0, (t+1)*n).  `flags` returns the verified-shard map.
@@ -1615,19 +1460,7 @@ int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64
         bool one_pass = get_dma_enabled(ctx, n) && rsg::decode_dma_supported(k, m, nfiles, shard_len) &&
                         rec % 16 == 0;
         for (int i : all_idx) one_pass = one_pass && (uintptr_t)(d_files[i] + 32) % 16 == 0;
-        const bool syn = one_pass && syn_enabled(ctx) && rsg::syn_supported(k, m, nfiles, 0, shard_len) &&
-                         (uintptr_t)d_out % 16 == 0;
-        if (syn) {
-            // RS(8,4) in syndrome form: the same single pass, with the
-            // present data through the compile-time encode network
-            ctx->tmark(s);
-            if ((st = launch_get_syn(*cd, present0, all_idx, d_files, d_flags, d_ok, k, shard_len, n, key,
-                                     verify_surplus, d_out, any_verify, s)))
-                return st;
-            ctx->tmark(s);
-            if (!any_verify && (st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
-            for (uint64_t x = 0; x < n; ++x) h_status[x] = RSG_OK;
-        } else if (one_pass) {
+        if (one_pass) {
             // RS(8,4): verify every present record, rebuild, gather and check
             // the surplus parity in ONE pass (k_decode_records_dma); the kernel
             // writes every present file's flags and, with surplus rows, every
@@ -1733,7 +1566,7 @@ int rsg_set_kernel_timing(rsg_ctx* ctx, int on) {
 int rsg_set_record_engine(rsg_ctx* ctx, int engine) {
     int st = enter(ctx);
     if (st) return st;
-    if (engine < RSG_RECORD_ENGINE_AUTO || engine > RSG_RECORD_ENGINE_SYNDROME) return RSG_ERR_INVALID_ARG;
+    if (engine < RSG_RECORD_ENGINE_AUTO || engine > RSG_RECORD_ENGINE_TWO_PASS) return RSG_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> g(ctx->mu);
     ctx->record_engine = engine;
     return RSG_OK;
@@ -1864,19 +1697,7 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
                         rec % 16 == 0;
         for (int i : all_idx) one_pass = one_pass && (uintptr_t)(d_files[i] + 32) % 16 == 0;
         for (int i : tg_idx) one_pass = one_pass && !d_files[i] && (uintptr_t)(d_targets[i] + 32) % 8 == 0;
-        bool syn = one_pass && syn_enabled(ctx) &&
-                   rsg::syn_supported(k, m, (int)all_idx.size(), (int)tg_idx.size(), shard_len);
-        for (int i : tg_idx) syn = syn && (uintptr_t)(d_targets[i] + 32) % 16 == 0;
-        if (syn) {
-            // RS(8,4) in syndrome form (k_records_syn)
-            ctx->tmark(s);
-            if ((st = launch_heal_syn(*cd, present0, all_idx, tg_idx, d_files, d_targets, d_flags, d_ok, shard_len,
-                                      n, key, any_verify, s)))
-                return st;
-            ctx->tmark(s);
-            if (!any_verify && (st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
-            for (uint64_t x = 0; x < n; ++x) h_status[x] = RSG_OK;
-        } else if (one_pass) {
+        if (one_pass) {
             // RS(8,4): verify every source record, write every target record
             // (body + digest) and compare the surplus parity in ONE pass
             // (the kernel writes every source's flags and, with surplus rows,

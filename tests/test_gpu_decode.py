@@ -8,18 +8,15 @@ import pytest
 pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("engine_path")]
 
 
-@pytest.fixture(params=["one_pass", "two_pass", "syndrome"], autouse=False)
+@pytest.fixture(params=["one_pass", "two_pass"], autouse=False)
 def engine_path(request, gpu):
-    """Every test runs through every lost-disk engine: the one-pass table
-    kernel (forced at any batch size where the geometry has one), the
-    syndrome-form one-pass kernel (RS(8,4) with whole 1 KiB steps; other
-    shapes fall back to the table kernel) and the two-pass path, selected on
-    the device-0 context with rsg_set_record_engine (by default a one-pass
-    kernel takes >= 1024 stripes)."""
+    """Every test runs through both lost-disk engines: the one-pass kernel
+    (forced at any batch size where the geometry has one) and the two-pass
+    path, selected on the device-0 context with rsg_set_record_engine (by
+    default the one-pass kernel takes >= 1024 stripes)."""
     from rustfs_amd import _lib
     L = _lib.load()
-    want = {"one_pass": _lib.RSG_RECORD_ENGINE_ONE_PASS, "two_pass": _lib.RSG_RECORD_ENGINE_TWO_PASS,
-            "syndrome": _lib.RSG_RECORD_ENGINE_SYNDROME}[request.param]
+    want = _lib.RSG_RECORD_ENGINE_ONE_PASS if request.param == "one_pass" else _lib.RSG_RECORD_ENGINE_TWO_PASS
     _lib.check(L.rsg_set_record_engine(gpu.handle, want))
     yield request.param
     _lib.check(L.rsg_set_record_engine(gpu.handle, _lib.RSG_RECORD_ENGINE_AUTO))
