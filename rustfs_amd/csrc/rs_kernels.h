@@ -35,7 +35,7 @@ struct Tuning {
     int fused_kind = 0;           // RSG_FUSED_KIND=packed|ring|dma|wide2|wide4|split2|split4 (0: by batch size)
     bool fused_spw1 = false;      // RSG_FUSED_SPW1=1: one stripe per packed workgroup
     int enc_prio = 0;             // RSG_ENC_PRIO=<0..3>: wave priorities of the fused DMA kernel
-    int dma_ew = 2;               // RSG_DMA_EW=4: two encoder waves per stripe group
+    int dma_ew = 2;               // RSG_DMA_EW=4: two encoder waves per stripe group (split, alternate steps)
     int dma_nt = 3;               // RSG_DMA_NT=<0..3>: non-temporal loads (bit 0) / stores (bit 1)
     int dma_spw = 8;              // RSG_DMA_SPW=4: four stripes per fused DMA workgroup
     int get_prio = 2;             // RSG_DMA_PRIO=<0..3>: wave priorities of the one-pass GET/heal

@@ -517,33 +517,6 @@ __device__ __forceinline__ void transpose(uint32_t (&w)[8], uint32_t m4, uint32_
     for (int d = 0; d < 8; d += 2) swap_bfi(w[d], w[d + 1], 1, m1);
 }
 
-// acc[r][i] (^)= XOR of the planes P[c][j] with bit j of mask[R0+r][C0+c][i]
-// (rows [R0, R0+RN), shards [C0, C0+NC)), folded two terms at a time by
-// the three-input XOR.
-template <int K, int M, int R0, int RN, int C0, int NC, bool FIRST>
-__device__ __forceinline__ void fold(uint32_t (&acc)[RN][8], const uint32_t (&P)[NC][8]) {
-    constexpr bs::PlaneMasks<K, M> PM{};
-#pragma unroll
-    for (int r = 0; r < RN; ++r) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            uint32_t t[1 + 8 * NC];
-            int n = 0;
-            if (!FIRST) t[n++] = acc[r][i];
-#pragma unroll
-            for (int c = 0; c < NC; ++c)
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    if ((PM.mask[R0 + r][C0 + c][i] >> j) & 1u) t[n++] = P[c][j];
-            uint32_t v = n ? t[0] : 0u;
-            int k = 1;
-            for (; k + 1 < n; k += 2) v = x3(v, t[k], t[k + 1]);
-            if (k < n) v ^= t[k];
-            acc[r][i] = v;
-        }
-    }
-}
-
 template <int K, int M, int NE = EW, int SP = SPW>
 struct Shape {
     static constexpr int SPW = SP, HS = SP / 2;       // stripes per workgroup, per DMA half
@@ -552,63 +525,9 @@ struct Shape {
     static constexpr uint32_t PSLOT = SPW * M * PP;   // one step of all parity rows
     static constexpr int DATA = (SPW * K) / 16;       // data-hasher waves
     static constexpr int PAR = (SPW * M + 15) / 16;   // parity-hasher waves
-    static constexpr int ENC = NE;                    // encoder waves: 2 per stripe group (EW) or 1 (XOR network)
+    static constexpr int ENC = NE;                    // encoder waves: 1 per stripe group, or 2 (split, alternate steps)
     static constexpr int WAVES = NE + DATA + PAR;
 };
-
-// Encoder wave: stripe group g, parity rows [R0, R0 + M/2) (two waves per group)
-template <int K, int M, int H>
-__device__ __forceinline__ void encoder(const GfApplyParams& p, uint64_t n, uint32_t steps, uint64_t s0, uint32_t g,
-                                        const uint8_t* ring, uint8_t* prow) {
-    using L = Shape<K, M>;
-    constexpr int RPW = M / 2;
-    constexpr int R0 = H * RPW;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t m4 = vgpr_const(0x0f0f0f0fu), m2 = vgpr_const(0x33333333u), m1 = vgpr_const(0x55555555u);
-    const uint32_t mys[4] = {2 * g, 2 * g + 1, 2 * g + HS, 2 * g + HS + 1};
-    uint8_t* const base = p.out_base;
-    uint64_t pdst[4];
-    bool live[4];  // wave-uniform: a dead stripe (past n) computes stripe 0's rows and stores nothing
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        live[j] = s0 + mys[j] < n;
-        pdst[j] = (live[j] ? s0 + mys[j] : 0) * p.stripe_stride + lane * 8u;
-    }
-    lds_barrier();  // B(0): slot 0 landed
-#pragma unroll 1
-    for (uint32_t s = 0; s < steps; ++s) {
-        const uint8_t* slot = ring + (s % D) * L::DSLOT + 2 * g * IP + lane * 8u;
-        uint32_t acc[RPW][8];
-#pragma unroll
-        for (int c = 0; c < K; c += 2) {
-            uint32_t P[2][8];
-#pragma unroll
-            for (int cc = 0; cc < 2; ++cc) {
-                const uint8_t* row = slot + HS * (c + cc) * IP;
-                const uint2 a0 = *(const uint2*)row, a1 = *(const uint2*)(row + IP);
-                const uint2 a2 = *(const uint2*)(row + CH), a3 = *(const uint2*)(row + IP + CH);
-                P[cc][0] = a0.x; P[cc][1] = a0.y; P[cc][2] = a1.x; P[cc][3] = a1.y;
-                P[cc][4] = a2.x; P[cc][5] = a2.y; P[cc][6] = a3.x; P[cc][7] = a3.y;
-                transpose(P[cc], m4, m2, m1);
-            }
-            if (c == 0) fold<K, M, R0, RPW, 0, 2, true>(acc, P);
-            else if (c == 2) fold<K, M, R0, RPW, (K > 2 ? 2 : 0), 2, false>(acc, P);
-            else if (c == 4) fold<K, M, R0, RPW, (K > 4 ? 4 : 0), 2, false>(acc, P);
-            else fold<K, M, R0, RPW, (K > 6 ? 6 : 0), 2, false>(acc, P);
-        }
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) {
-            transpose(acc[r], m4, m2, m1);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint2 v = make_uint2(acc[r][2 * j], acc[r][2 * j + 1]);
-                if (live[j]) *(uint2*)(base + pdst[j] + p.out_off[R0 + r] + (uint64_t)s * CH) = v;
-                *(uint2*)(prow + (s % NP) * L::PSLOT + ((R0 + r) * SPW + mys[j]) * PP + lane * 8u) = v;
-            }
-        }
-        lds_barrier();  // B(s+1): parity rows of step s published
-    }
-}
 
 // One encoder wave per stripe group computing all four RS(8,4) parity rows:
 // the 64 input planes go through the generated common-subexpression XOR
@@ -616,12 +535,13 @@ __device__ __forceinline__ void encoder(const GfApplyParams& p, uint64_t n, uint
 // shard is bit-transposed once per group instead of once per row pair
 // (per group and step: 8 + 4 transposes + 239 XORs, against 2 x (8 + 2)
 // transposes + 504 XORs for two encoder() waves).
-template <int K, int M, int NT, int SP>
+template <int K, int M, int NT, int SP, bool SPLIT>
 __device__ __forceinline__ void encoder_net(const GfApplyParams& p, uint64_t n, uint32_t steps, uint64_t s0,
-                                            uint32_t g, const uint8_t* ring, uint8_t* prow) {
+                                            uint32_t g, uint32_t ph, const uint8_t* ring, uint8_t* prow) {
     static_assert(K == 8 && M == 4, "the XOR network is RS(8,4)'s");
-    using L = Shape<K, M, SP / 4, SP>;
+    using L = Shape<K, M, SPLIT ? SP / 2 : SP / 4, SP>;
     constexpr int SPW = L::SPW, HS = L::HS;
+    constexpr uint32_t LAG = SPLIT ? 2 : 1;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t m4 = vgpr_const(0x0f0f0f0fu), m2 = vgpr_const(0x33333333u), m1 = vgpr_const(0x55555555u);
     const uint32_t mys[4] = {2 * g, 2 * g + 1, 2 * g + HS, 2 * g + HS + 1};
@@ -633,11 +553,10 @@ __device__ __forceinline__ void encoder_net(const GfApplyParams& p, uint64_t n, 
         live[j] = s0 + mys[j] < n;
         pdst[j] = (live[j] ? s0 + mys[j] : 0) * p.stripe_stride + lane * 8u;
     }
-    lds_barrier();  // B(0): slot 0 landed
-#pragma unroll 1
-    for (uint32_t s = 0; s < steps; ++s) {
+    uint32_t P[64];
+    // step s's data rows, bit-transposed into the 64 planes
+    auto load = [&](uint32_t s) {
         const uint8_t* slot = ring + (s % D) * L::DSLOT + 2 * g * IP + lane * 8u;
-        uint32_t P[64];
 #pragma unroll
         for (int c = 0; c < K; ++c) {
             const uint8_t* row = slot + HS * c * IP;
@@ -648,6 +567,9 @@ __device__ __forceinline__ void encoder_net(const GfApplyParams& p, uint64_t n, 
 #pragma unroll
             for (int j = 0; j < 8; ++j) P[8 * c + j] = w[j];
         }
+    };
+    // step s's parity: network, planes back to bytes, HBM + parity-row area
+    auto emit = [&](uint32_t s) {
         uint32_t O[32];
         xn::rs84_encode_planes(P, O);
 #pragma unroll
@@ -666,7 +588,22 @@ __device__ __forceinline__ void encoder_net(const GfApplyParams& p, uint64_t n, 
                 *(uint2*)(prow + (s % NP) * L::PSLOT + (r * SPW + mys[j]) * PP + lane * 8u) = v;
             }
         }
-        lds_barrier();  // B(s+1): parity rows of step s published
+    };
+    const uint32_t intervals = steps + LAG;  // interval t: between B(t) and B(t+1)
+    lds_barrier();  // B(0): slot 0 landed
+#pragma unroll 1
+    for (uint32_t t = 0; t < intervals; ++t) {
+        if constexpr (SPLIT) {
+            // two waves per group on alternate steps; a step straddles one
+            // barrier: its rows are read while in the ring (interval s), its
+            // parity emitted in interval s+1 (published by B(s+2))
+            if (t < steps && t % 2 == ph) load(t);
+            else if (t >= 1 && t - 1 < steps && (t - 1) % 2 == ph) emit(t - 1);
+        } else if (t < steps) {
+            load(t);
+            emit(t);  // published by B(t+1)
+        }
+        if (t + 1 < intervals) lds_barrier();  // B(t+1)
     }
 }
 }  // namespace dma
@@ -675,8 +612,10 @@ template <int K, int M, int NE = dma::EW, int NT = 0, int SP = dma::SPW>
 __global__ __launch_bounds__((64 * dma::Shape<K, M, NE, SP>::WAVES)) void k_encode_hash_dma(const GfApplyParams p,
                                                                                           const HashParams h) {
     using namespace dma;
-    static_assert(K % 2 == 0 && M % 2 == 0 && K <= 8 && M <= 4 && M >= 2, "pairs of shards per wave");
-    static_assert((NE == 4 && SP == 8) || NE == SP / 4, "two encoder waves per stripe group, or one with the XOR network");
+    static_assert(K == 8 && M == 4, "the XOR network is RS(8,4)'s");
+    static_assert(NE == SP / 4 || NE == SP / 2, "one encoder wave per stripe group, or two (split)");
+    constexpr bool SPLIT = NE == SP / 2;
+    constexpr uint32_t LAG = SPLIT ? 2 : 1;  // steps the parity hashers trail the DMA'd data
     using L = Shape<K, M, NE, SP>;
     constexpr int SPW = L::SPW, HS = L::HS;
     __shared__ __attribute__((aligned(16))) uint8_t ring[D * L::DSLOT];
@@ -687,12 +626,11 @@ __global__ __launch_bounds__((64 * dma::Shape<K, M, NE, SP>::WAVES)) void k_enco
     const uint64_t s0 = (uint64_t)blockIdx.x * SPW;
     const uint32_t ring_base = (uint32_t)(uintptr_t)ring;
 
+    const uint32_t intervals = steps + LAG;  // interval t: between B(t) and B(t+1)
     if (wave < (uint32_t)NE) {
         if (p.wave_prio & kPrioGf) __builtin_amdgcn_s_setprio(2);
-        const uint32_t g = wave % 2;
-        if constexpr (NE == SP / 4) encoder_net<K, M, NT, SP>(p, n, steps, s0, g, ring, prow);
-        else if (wave < 2) encoder<K, M, 0>(p, n, steps, s0, g, ring, prow);
-        else encoder<K, M, 1>(p, n, steps, s0, g, ring, prow);
+        const uint32_t g = SPLIT ? wave / 2 : wave, ph = SPLIT ? wave % 2 : 0;
+        encoder_net<K, M, NT, SP, SPLIT>(p, n, steps, s0, g, ph, ring, prow);
         return;
     }
     // ---------------------------------- hashers ----------------------------------
@@ -752,18 +690,21 @@ __global__ __launch_bounds__((64 * dma::Shape<K, M, NE, SP>::WAVES)) void k_enco
         __builtin_amdgcn_s_waitcnt(vmcnt_imm((D - 2) * NDI));  // DMA(0) landed
         lds_barrier();  // B(0)
 #pragma unroll 1
-        for (uint32_t s = 0; s < steps; ++s) {
-            dma(s + D - 1 < steps ? s + D - 1 : steps - 1);  // into the slot step s-1 used
-            hash16(ring_base + (s % D) * L::DSLOT + roff);
-            __builtin_amdgcn_s_waitcnt(vmcnt_imm((D - 2) * NDI));  // DMA(s+1) landed
-            lds_barrier();  // B(s+1)
+        for (uint32_t t = 0; t < intervals; ++t) {
+            if (t < steps) {
+                dma(t + D - 1 < steps ? t + D - 1 : steps - 1);  // into the slot step t-1 used
+                hash16(ring_base + (t % D) * L::DSLOT + roff);
+                __builtin_amdgcn_s_waitcnt(vmcnt_imm((D - 2) * NDI));  // DMA(t+1) landed
+            }
+            if (t + 1 < intervals) lds_barrier();  // B(t+1)
         }
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // the clamped tail DMA has landed
     } else {
         lds_barrier();  // B(0)
 #pragma unroll 1
-        for (uint32_t s = 0; s <= steps; ++s) {
-            if (s > 0) hash16((uint32_t)(uintptr_t)prow + ((s - 1) % NP) * L::PSLOT + roff);  // published by B(s)
-            if (s < steps) lds_barrier();  // B(s+1)
+        for (uint32_t t = 0; t < intervals; ++t) {
+            if (t >= LAG) hash16((uint32_t)(uintptr_t)prow + ((t - LAG) % NP) * L::PSLOT + roff);  // published by B(t)
+            if (t + 1 < intervals) lds_barrier();  // B(t+1)
         }
     }
     if (live) hhq_finish(st, h.out + ((s0 + stripe_l) * (K + M) + shard) * 32u, q);
@@ -1388,8 +1329,8 @@ static bool dma_supported(const GfApplyParams& p, uint64_t shard_len, uint64_t n
 static hipError_t launch_encode_hash_dma(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                          hipStream_t stream) {
     // Tuning (A/B runs only): enc_prio = wave priorities (default none);
-    // dma_ew = 4: two encoder waves per stripe group (per-row XOR folds)
-    // instead of one running the generated XOR network; dma_nt: non-temporal
+    // dma_ew = 4: two encoder waves per stripe group taking alternate steps
+    // (split, as the wide kernel) instead of one; dma_nt: non-temporal
     // data loads (bit 0) and parity stores (bit 1), default both: 1.30 ->
     // 1.28 ms at n = 4096 (profiles/r02/ab_nt/); dma_spw = 4: four stripes
     // per workgroup, two workgroups per CU — measured slower (n = 4096: 1.39
@@ -1405,8 +1346,8 @@ static hipError_t launch_encode_hash_dma(GfApplyParams p, HashParams h, uint64_t
         hipLaunchKernelGGL((k_encode_hash_dma<8, 4, 1, 3, 4>), g4, b4, 0, stream, p, h);
         return hipGetLastError();
     }
-    if (ew == 4)
-        hipLaunchKernelGGL((k_encode_hash_dma<8, 4, 4>), grid, dim3(64 * dma::Shape<8, 4, 4>::WAVES), 0, stream, p,
+    if (ew == 4)  // split encoders: two waves per stripe group on alternate steps
+        hipLaunchKernelGGL((k_encode_hash_dma<8, 4, 4, 3>), grid, dim3(64 * dma::Shape<8, 4, 4>::WAVES), 0, stream, p,
                            h);
     else if (nt == 1) hipLaunchKernelGGL((k_encode_hash_dma<8, 4, 2, 1>), grid, blk2, 0, stream, p, h);
     else if (nt == 2) hipLaunchKernelGGL((k_encode_hash_dma<8, 4, 2, 2>), grid, blk2, 0, stream, p, h);
