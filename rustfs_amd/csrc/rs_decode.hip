@@ -187,18 +187,26 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_re
     const bool live = quad_on && s0 + stripe_l < n;
     HHQuad st;
     hhq_init(st, h.key, q);
-    uint64_t dsrc[HS];
+    // record sources as a wave-uniform base (SGPRs) + a 32-bit per-lane
+    // offset (the upper half's stripe, or the lower one again past n): the
+    // loads take the saddr form, a step costs HS VALU adds
+    uint64_t ubo[HS];
+    uint32_t vlane[HS];
 #pragma unroll
     for (int i = 0; i < HS; ++i) {
-        const uint64_t sg = s0 + i + (lane >> 5) * HS;
-        dsrc[i] = (sg < n ? sg : 0) * h.stripe_stride + (lane & 31u) * 16u;
+        const uint64_t lo = s0 + i, hi = lo + HS;
+        ubo[i] = (lo < n ? lo : 0) * h.stripe_stride;
+        vlane[i] = (lane & 31u) * 16u + ((lane >> 5) && hi < n ? (uint32_t)(HS * h.stripe_stride) : 0u);
     }
     auto dma_step = [&](uint32_t step) {
+        uint32_t voff[HS];
+#pragma unroll
+        for (int i = 0; i < HS; ++i) voff[i] = vlane[i] + step * CH;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             if (k >= ndi) break;  // wave-uniform
             const uint32_t ins = 8 * hw + k;
-            const uint8_t* src = h.base[ins / HS] + dsrc[k % HS] + (uint64_t)step * CH;
+            const uint8_t* src = h.base[ins / HS] + ubo[k % HS] + (uint64_t)voff[k % HS];
             __builtin_amdgcn_global_load_lds(
                 (const void*)src, (__attribute__((address_space(3))) void*)(ring + (step % D) * L::DSLOT + ins * IP), 16,
                 0, 0);
@@ -312,7 +320,8 @@ bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len) {
 static bool dma_records_aligned(const HashParams& h, int nf) {
     for (int f = 0; f < nf; ++f)
         if ((uintptr_t)h.base[f] % 16) return false;
-    return h.stripe_stride % 16 == 0;
+    // 32-bit per-lane DMA offsets: up to G/2 records on plus a record body
+    return h.stripe_stride % 16 == 0 && 5 * h.stripe_stride < (1ull << 32);
 }
 
 hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, int nf, int targets,

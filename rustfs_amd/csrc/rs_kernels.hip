@@ -667,18 +667,27 @@ __global__ __launch_bounds__((64 * dma::Shape<K, M, NE, SP>::WAVES)) void k_enco
     if (is_data) {
         // DMA instruction 8 hw + k: shard c = (8 hw + k) / 4, stripe pair
         // i = k % 4: lanes 0-31 stripe i, lanes 32-63 stripe i + 4
-        uint64_t dsrc[HS];
+        // Sources as a wave-uniform base (the lower half's stripe, SGPRs) +
+        // a 32-bit per-lane offset (the upper half's stripe HS stripes on,
+        // or the lower one again when that is past n), so every
+        // global_load_lds takes the saddr form and a step costs HS VALU adds
+        const uint8_t* base = p.out_base;
+        const uint8_t* ub[HS];
+        uint32_t vlane[HS];
 #pragma unroll
         for (int i = 0; i < HS; ++i) {
-            const uint64_t sg = s0 + i + (lane >> 5) * HS;
-            dsrc[i] = (sg < n ? sg : 0) * p.stripe_stride + (lane & 31u) * 16u;
+            const uint64_t lo = s0 + i, hi = lo + HS;
+            ub[i] = base + (lo < n ? lo : 0) * p.stripe_stride;
+            vlane[i] = (lane & 31u) * 16u + ((lane >> 5) && hi < n ? (uint32_t)(HS * p.stripe_stride) : 0u);
         }
-        const uint8_t* base = p.out_base;
         auto dma = [&](uint32_t step) {
+            uint32_t voff[HS];
+#pragma unroll
+            for (int i = 0; i < HS; ++i) voff[i] = vlane[i] + step * CH;
 #pragma unroll
             for (int k = 0; k < NDI; ++k) {
                 const uint32_t c = (NDI * hw + k) / HS;  // wave-uniform
-                const uint8_t* src = base + dsrc[k % HS] + p.in_off[c] + (uint64_t)step * CH;
+                const uint8_t* src = ub[k % HS] + p.in_off[c] + (uint64_t)voff[k % HS];
                 __builtin_amdgcn_global_load_lds(
                     (const void*)src,
                     (__attribute__((address_space(3))) void*)(ring + (step % D) * L::DSLOT + (NDI * hw + k) * IP),
@@ -845,17 +854,21 @@ __global__ __launch_bounds__((64 * wide::Shape<SPW, SPLIT>::WAVES)) void k_encod
         const uint32_t w = wave - L::ENC;
         const uint32_t stripe_l = 2 * w + j / 8, shard = j % 8;
         const bool live = s0 + stripe_l < n;
-        uint64_t src[2];
+        // row sources as a wave-uniform base (SGPRs) + a 32-bit per-lane
+        // offset, so each global_load_lds takes the saddr form and a step
+        // costs one VALU add for all 16 rows (the hash chain's wave issues it)
+        const uint8_t* ub[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const uint64_t sg = s0 + 2 * w + i;
-            src[i] = (sg < n ? sg : 0) * p.stripe_stride + lane * 16u;
+            ub[i] = base + (sg < n ? sg : 0) * p.stripe_stride;
         }
         const uint32_t row_of = (stripe_l * 8 + shard) * RP + 8 * q;
         auto dma = [&](uint32_t step) {
+            const uint32_t voff = lane * 16u + step * CH;
 #pragma unroll
             for (int k = 0; k < 16; ++k) {  // row k: stripe 2w + k/8, shard k%8 (wave-uniform)
-                const uint8_t* g = base + src[k / 8] + p.in_off[k % 8] + (uint64_t)step * CH;
+                const uint8_t* g = ub[k / 8] + p.in_off[k % 8] + (uint64_t)voff;
                 __builtin_amdgcn_global_load_lds(
                     (const void*)g,
                     (__attribute__((address_space(3))) void*)(ring + (step % D) * L::DSLOT +
@@ -1319,6 +1332,7 @@ static bool dma_supported(const GfApplyParams& p, uint64_t shard_len, uint64_t n
         return false;
     if (shard_len < dma::CH || shard_len % dma::CH || shard_len / dma::CH > 0xffffffffull) return false;
     if ((uintptr_t)p.base % 16 || p.stripe_stride % 16) return false;
+    if (dma::SPW / 2 * p.stripe_stride + shard_len >= (1ull << 32)) return false;  // 32-bit per-lane DMA offsets
     for (int c = 0; c < 8; ++c)
         if (p.in_off[c] % 16) return false;
     for (int r = 0; r < 4; ++r)
