@@ -93,6 +93,13 @@ def launch_ranks(a, argv, script=None, devices=None) -> int:
     if why:
         print(f"bench.py: {why}", file=sys.stderr, flush=True)
         return 2
+    import signal
+
+    def stop(signum, frame):  # a launcher killed by its caller takes its ranks along
+        raise SystemExit(128 + signum)
+
+    for sig in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP):
+        signal.signal(sig, stop)
     procs = []
     script = script or os.path.abspath(__file__)
     for r, env in enumerate(rank_plan(a.gpus, free_port(), os.environ)):

@@ -96,3 +96,43 @@ def test_bench_refuses_without_gpu_or_matching_world():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"], env=env,
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 2 and "2 rank(s) were launched" in p.stderr and p.stdout == ""
+
+
+SLEEPER = r'''
+import os, sys, time
+open(os.path.join(sys.argv[-1], "rank%s.pid" % os.environ["RANK"]), "w").write(str(os.getpid()))
+time.sleep(300)
+'''
+
+
+def test_launcher_terminated_takes_ranks_along(tmp_path):
+    """SIGTERM to `bench.py --gpus N` (a driver's time limit) ends its rank
+    processes too: none is left holding a GPU."""
+    import signal
+    import time
+    script = tmp_path / "rank.py"
+    script.write_text(SLEEPER)
+    code = ("import sys; sys.path.insert(0, %r); import bench; "
+            "a = bench.parse(['--gpus', '2']); "
+            "sys.exit(bench.launch_ranks(a, ['--gpus', '2', %r], script=%r, devices=2))"
+            % (ROOT, str(tmp_path), str(script)))
+    p = subprocess.Popen([sys.executable, "-c", code])
+    pids = []
+    for _ in range(200):
+        pids = [tmp_path / f"rank{r}.pid" for r in range(2)]
+        if all(f.exists() and f.read_text() for f in pids):
+            break
+        time.sleep(0.05)
+    pids = [int(f.read_text()) for f in pids]
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(timeout=30) != 0
+    for pid in pids:
+        for _ in range(100):
+            try:
+                os.kill(pid, 0)
+            except ProcessLookupError:
+                break
+            time.sleep(0.05)
+        else:
+            os.kill(pid, signal.SIGKILL)
+            raise AssertionError(f"rank process {pid} outlived the launcher")
