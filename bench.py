@@ -243,6 +243,18 @@ def random_stripes(dev, k, m, S, n, seed):
     return st
 
 
+def pmc_traffic(k, m, S, n, digests):
+    """HBM bytes per launch of this configuration's kernel from the committed
+    PMC passes (profiles/pmc_traffic.json: FETCH_SIZE x 2 + WRITE_SIZE, the
+    microarch guide's gfx950 correction; tools/pmc.sh, tools/pmc_traffic.py),
+    or None when no pass covered it."""
+    prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        return json.load(open(prof)).get(f"rs{k}{m}_S{S}_n{n}{'_hash' if digests else ''}", {}).get("bytes_per_launch")
+    except Exception:
+        return None
+
+
 def time_encode(e, stripes, digests, stream, reps, warm=3, warm_seconds=0.3):
     """Average device time (ms) of one rsg_encode_batch_dev over `reps`
     launches: HIP events on the launch stream around each, after `warm`
@@ -274,6 +286,7 @@ def encode_extra(name_workload, e, stripes, digests, k, m, S, n, stream, reps):
     avg, mn = time_encode(e, stripes, digests, stream, reps)
     alg = n * (k + m) * S + (n * (k + m) * 32 if digests is not None else 0)
     return {"workload": name_workload, "k": k, "m": m, "shard_bytes": S, "stripes": n,
+            "traffic": pmc_traffic(k, m, S, n, digests is not None),
             "kernel_ms": round(avg, 4), "kernel_ms_min": round(mn, 4), "launches": reps,
             "GiB_s_payload": round(n * k * S / (avg * 1e-3) / GiB, 2),
             "alg_bytes": alg, "achieved_GB_s": round(alg / (avg * 1e-3) / 1e9, 1),
@@ -519,14 +532,7 @@ def main(argv=None):
         if not a.no_config_extras and world == 1:
             extras.update(config_extras(a, e, stripes, k, m, dev, stream, rank))
 
-    traffic = None
-    prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    key = f"rs{k}{m}_S{S}_n{n}{'_hash' if a.digests else ''}"
-    if os.path.exists(prof):
-        try:
-            traffic = json.load(open(prof)).get(key, {}).get("bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic = pmc_traffic(k, m, S, n, a.digests)
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
