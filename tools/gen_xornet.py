@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
-"""Generate rustfs_amd/csrc/rs84_xornet.h: the RS(8,4) bit-sliced encode as a
-short straight-line program of three-input XORs (v_bitop3_b32).
+"""Generate rustfs_amd/csrc/rs84_xornet.h (the RS(8,4) bit-sliced encode as a
+short straight-line program of three-input XORs, v_bitop3_b32) and
+rs164_xornet.h (RS(16,4): two networks over data shards 0-7 and 8-15, the
+second XOR-accumulating into the first's output planes, so a lane needs only
+64 input planes live at a time).
 
 The bit-sliced encoder (gf_bitslice.h) computes each of the 32 output planes
 (4 parity rows x 8 bits) as the XOR of the input planes (8 data shards x 8
@@ -14,7 +17,7 @@ use saves the most ops, counting ceil((t-1)/2) ops for a t-term row) finds a
 network about half that size.  The search is seeded and deterministic; the
 program is checked here on random planes against the plain matrix product.
 
-Usage: python tools/gen_xornet.py [seeds]  (writes the header)
+Usage: python tools/gen_xornet.py [seeds]  (writes both headers)
 """
 import collections
 import itertools
@@ -70,13 +73,22 @@ def _dot(k, r, c, w):
     return a
 
 
-def plane_rows(g):
-    """Output plane r*8+i = XOR of input planes c*8+j with bit i of g[r][c]*2^j."""
+def plane_rows(g, cols=range(K), acc=False):
+    """Output plane r*8+i = XOR of input planes c*8+j with bit i of g[r][c]*2^j
+    over the data shards `cols` (renumbered from 0).  acc: each row also takes
+    its own previous value (variable ACC + r*8+i, unique to the row, so never
+    shared)."""
     rows = []
-    for r in range(M):
+    for r in range(len(g)):
         for i in range(8):
-            rows.append({c * 8 + j for c in range(K) for j in range(8) if (gmul(g[r][c], 1 << j) >> i) & 1})
+            s = {ci * 8 + j for ci, c in enumerate(cols) for j in range(8) if (gmul(g[r][c], 1 << j) >> i) & 1}
+            if acc:
+                s.add(ACC + r * 8 + i)
+            rows.append(s)
     return rows
+
+
+ACC = 1 << 16  # previous-output variables of an accumulating network
 
 
 def cost(t):
@@ -114,8 +126,38 @@ def search(rows, seed):
     return len(temps) + sum(cost(len(s)) for s in rr), temps, rr
 
 
+def name(v):
+    return f"O[{v - ACC}]" if v >= ACC else f"P[{v}]" if v < 64 else f"t{v}"
+
+
+def body(fn, temps, rr, acc=False):
+    out = []
+    args = "const uint32_t (&P)[64], uint32_t (&O)[32]"
+    out.append(f"__device__ __forceinline__ void {fn}({args}) {{")
+    for v, *t in temps:
+        if len(t) == 3:
+            out.append(f"    const uint32_t t{v} = x3({name(t[0])}, {name(t[1])}, {name(t[2])});")
+        else:
+            out.append(f"    const uint32_t t{v} = {name(t[0])} ^ {name(t[1])};")
+    for o, s in enumerate(rr):
+        # an accumulating row starts from its own previous value
+        terms = [name(v) for v in sorted(s, key=lambda v: (v < ACC, v))]
+        if not terms:
+            out.append(f"    O[{o}] = 0u;")
+            continue
+        e = terms[0]
+        k = 1
+        while k + 1 < len(terms):
+            e = f"x3({e}, {terms[k]}, {terms[k + 1]})"
+            k += 2
+        if k < len(terms):
+            e = f"({e} ^ {terms[k]})"
+        out.append(f"    O[{o}] = {e};")
+    out.append("}")
+    return out
+
+
 def emit(temps, rr, total, seed, g):
-    name = lambda v: f"P[{v}]" if v < 64 else f"t{v}"
     out = []
     out.append("// rs84_xornet.h — GENERATED by tools/gen_xornet.py (do not edit).")
     out.append("// RS(8,4) bit-sliced encode as a straight-line three-input XOR network:")
@@ -130,26 +172,7 @@ def emit(temps, rr, total, seed, g):
     out.append("")
     out.append("namespace xn {")
     out.append("")
-    out.append("__device__ __forceinline__ void rs84_encode_planes(const uint32_t (&P)[64], uint32_t (&O)[32]) {")
-    for v, *t in temps:
-        if len(t) == 3:
-            out.append(f"    const uint32_t t{v} = x3({name(t[0])}, {name(t[1])}, {name(t[2])});")
-        else:
-            out.append(f"    const uint32_t t{v} = {name(t[0])} ^ {name(t[1])};")
-    for o, s in enumerate(rr):
-        terms = [name(v) for v in sorted(s)]
-        if not terms:
-            out.append(f"    O[{o}] = 0u;")
-            continue
-        e = terms[0]
-        k = 1
-        while k + 1 < len(terms):
-            e = f"x3({e}, {terms[k]}, {terms[k + 1]})"
-            k += 2
-        if k < len(terms):
-            e = f"({e} ^ {terms[k]})"
-        out.append(f"    O[{o}] = {e};")
-    out.append("}")
+    out += body("rs84_encode_planes", temps, rr)
     out.append("")
     out.append("}  // namespace xn")
     return "\n".join(out) + "\n"
@@ -158,13 +181,13 @@ def emit(temps, rr, total, seed, g):
 def check(rows, temps, rr):
     rng = random.Random(1)
     for _ in range(8):
-        val = {v: rng.getrandbits(32) for v in range(64)}
+        val = {v: rng.getrandbits(32) for s in rows for v in s}
         for v, *t in temps:
             x = 0
             for a in t:
                 x ^= val[a]
             val[v] = x
-        for o in range(32):
+        for o in range(len(rows)):
             want = 0
             for v in rows[o]:
                 want ^= val[v]
@@ -174,23 +197,63 @@ def check(rows, temps, rr):
             assert got == want, o
 
 
-def main():
-    seeds = int(sys.argv[1]) if len(sys.argv) > 1 else 16
-    g = encode_rows(K, M)
-    rows = plane_rows(g)
-    assert sum(len(s) for s in rows) == 1040
+def best_network(rows, seeds, label):
     best = None
     for seed in range(seeds):
         total, temps, rr = search(rows, seed)
-        print(f"seed {seed}: {total} ops", flush=True)
+        print(f"{label} seed {seed}: {total} ops", flush=True)
         if best is None or total < best[0]:
             best = (total, temps, rr, seed)
-    total, temps, rr, seed = best
-    check(rows, temps, rr)
-    path = os.path.join(os.path.dirname(__file__), "..", "rustfs_amd", "csrc", "rs84_xornet.h")
+    check(rows, *best[1:3])
+    return best
+
+
+def emit164(lo, hi, g, ones):
+    out = []
+    out.append("// rs164_xornet.h — GENERATED by tools/gen_xornet.py (do not edit).")
+    out.append("// RS(16,4) bit-sliced encode as two straight-line three-input XOR networks:")
+    out.append(f"// data shards 0-7 ({lo[0]} ops, search seed {lo[3]}) and 8-15 XOR-accumulated into the")
+    out.append(f"// same 32 output planes ({hi[0]} ops, seed {hi[3]}), against {ones // 2} for folding each")
+    out.append(f"// output plane separately ({ones} ones in the 32 x 128 GF(2) matrix).  Parity rows")
+    out.append("// (erasure.rs:448-470 construction):")
+    for r in range(len(g)):
+        out.append(f"//   row {r}: {g[r]}")
+    out.append("// P[c*8+j] = bit plane j of data shard c (c < 8) or c + 8 (hi), O[r*8+i] = bit")
+    out.append("// plane i of parity row r.  Included by rs_kernels.hip inside namespace rsg, after x3().")
+    out.append("#pragma once")
+    out.append("")
+    out.append("namespace xn {")
+    out.append("")
+    out += body("rs164_planes_lo", lo[1], lo[2])
+    out.append("")
+    out += body("rs164_planes_hi", hi[1], hi[2])
+    out.append("")
+    out.append("}  // namespace xn")
+    return "\n".join(out) + "\n"
+
+
+def main():
+    seeds = int(sys.argv[1]) if len(sys.argv) > 1 else 16
+    here = os.path.join(os.path.dirname(__file__), "..", "rustfs_amd", "csrc")
+    g = encode_rows(K, M)
+    rows = plane_rows(g)
+    assert sum(len(s) for s in rows) == 1040
+    total, temps, rr, seed = best_network(rows, seeds, "RS(8,4)")
+    path = os.path.join(here, "rs84_xornet.h")
     with open(path, "w") as f:
         f.write(emit(temps, rr, total, seed, g))
     print(f"wrote {os.path.normpath(path)}: {total} ops (seed {seed})")
+
+    g = encode_rows(16, 4)
+    lo_rows = plane_rows(g, range(8))
+    hi_rows = plane_rows(g, range(8, 16), acc=True)
+    ones = sum(len(s) for s in lo_rows) + sum(len(s) - 1 for s in hi_rows)
+    lo = best_network(lo_rows, seeds, "RS(16,4) lo")
+    hi = best_network(hi_rows, seeds, "RS(16,4) hi")
+    path = os.path.join(here, "rs164_xornet.h")
+    with open(path, "w") as f:
+        f.write(emit164(lo, hi, g, ones))
+    print(f"wrote {os.path.normpath(path)}: {lo[0]} + {hi[0]} ops")
 
 
 if __name__ == "__main__":
