@@ -91,13 +91,6 @@ __device__ __forceinline__ void st16_nt(uint8_t* p, const uint4& v) {
     __builtin_nontemporal_store(w, (v4u_any*)p);
 }
 
-// Non-temporal 16-byte load (16-byte aligned): input read once by the pass.
-__device__ __forceinline__ uint4 ld16_nt(const uint8_t* p) {
-    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    const v4u w = __builtin_nontemporal_load((const v4u*)p);
-    return make_uint4(w.x, w.y, w.z, w.w);
-}
-
 // Output row r of a launch: its effective mode and address.
 __device__ __forceinline__ uint8_t* gf_dst(const GfApplyParams& p, uint8_t* obase, uint64_t off, int r, uint32_t stripe,
                                           uint32_t& mode) {

@@ -39,11 +39,6 @@ struct Tuning {
     int dma_nt = 3;               // RSG_DMA_NT=<0..3>: non-temporal loads (bit 0) / stores (bit 1)
     int dma_spw = 8;              // RSG_DMA_SPW=4: four stripes per fused DMA workgroup
     int get_prio = 2;             // RSG_DMA_PRIO=<0..3>: wave priorities of the one-pass GET/heal
-    int bitslice = -1;            // RSG_BITSLICE=0: no bit-sliced encode; 1: also for RS(8,4) (-1: RS(16,4))
-    int bs_nt = 0;                // RSG_BS_NT=<0..3>: bit-sliced encode non-temporal loads / stores
-    int bs_occ = 0;               // RSG_BS_OCC=<3..5>: bit-sliced encode register budget (waves per SIMD)
-    int bs_pipe = 0;              // RSG_BS_PIPE=<waves>: persistent pipelined bit-sliced encode with that many waves
-    bool bs_seq = false;          // RSG_BS_SEQ=1: RS(16,4) bit-sliced encode fetches shards 8-15 after the first network
     // fault injection (tests only): RSG_TEST_FAIL_SUBBATCH=<i> makes sub-batch
     // i of every rsg_encode_batch_host_submit fail to enqueue (-1: never)
     int test_fail_subbatch = -1;

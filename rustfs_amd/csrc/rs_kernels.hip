@@ -20,7 +20,6 @@
 // the HBM op budget).
 #include <hip/hip_runtime.h>
 
-#include <algorithm>
 #include <array>
 #include <string>
 #include <stdint.h>
@@ -31,8 +30,7 @@
 
 namespace rsg {
 
-#include "rs84_xornet.h"   // generated (tools/gen_xornet.py); uses x3
-#include "rs164_xornet.h"  // generated, RS(16,4)
+#include "rs84_xornet.h"  // generated (tools/gen_xornet.py); uses x3
 
 // PRE: the launch has XOR / COMPARE rows, whose read-back operands are loaded
 // with the inputs, or copy-through inputs (a separate instantiation: the
@@ -610,212 +608,6 @@ __device__ __forceinline__ void encoder_net(const GfApplyParams& p, uint64_t n, 
 }
 }  // namespace dma
 
-// ---------------------------------------------------------------------------
-// Bit-sliced encode for a compile-time matrix (RS(8,4), RS(16,4); the launcher
-// checks that the launch's tables are that matrix's, gf_bitslice.h).  One wave
-// per 2 KiB column chunk of one stripe: lane l holds 32 bytes of every data
-// shard (16 at l*16 and 16 at 1024 + l*16, so every load and store is a fully
-// coalesced 1 KiB dwordx4 access), bit-transposes each shard into 8 planes and
-// runs the generated XOR network (rs84_xornet.h / rs164_xornet.h: 239 / 495
-// three-input XORs for all four parity rows); the parity planes are
-// transposed back and stored.  Per 32-byte lane column of RS(16,4): 20
-// transposes (48 VALU each) + 495 XORs, against 16 x 8 x ~23 VALU for the
-// v_perm table kernel (k_gf_apply_loop), which is VALU-bound at this
-// geometry.  Data shards 8-15 are loaded together with 0-7 and transposed
-// after the first network, so only 64 planes are live at a time.
-template <int K, int NT, int OCC, bool SEQ>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void k_encode_bs(const GfApplyParams p) {
-    static_assert(K == 8 || K == 16, "compile-time networks: RS(8,4), RS(16,4)");
-    static_assert(!SEQ || K == 16, "sequenced fetch: RS(16,4)");
-    constexpr int M = 4;
-    const uint32_t stripe = blockIdx.x / p.chunks_per_stripe;
-    const uint32_t chunk = blockIdx.x - stripe * p.chunks_per_stripe;
-    const uint8_t* sbase = p.base + (uint64_t)stripe * p.stripe_stride;
-    uint8_t* obase = p.out_base + (uint64_t)stripe * p.out_stripe_stride;
-    // HOFF: lane l holds bytes l*16 and 1024 + l*16 (1024) or l*32 .. l*32 + 31 (16)
-    const uint32_t HOFF = p.n_store ? 16u : 1024u;
-    const uint64_t off = (uint64_t)chunk * 2048u + threadIdx.x * (HOFF == 16u ? 32u : 16u);
-    uint4 a[K], b[K];
-    auto fetch = [&](int c0, int c1) {
-#pragma unroll
-        for (int c = c0; c < c1; ++c) {
-            if constexpr (NT & 1) {
-                a[c] = ld16_nt(sbase + p.in_off[c] + off);
-                b[c] = ld16_nt(sbase + p.in_off[c] + off + HOFF);
-            } else {
-                a[c] = ld16(sbase + p.in_off[c] + off);
-                b[c] = ld16(sbase + p.in_off[c] + off + HOFF);
-            }
-        }
-    };
-    // SEQ (RS(16,4)): shards 8-15 are fetched only after the first network
-    // (the compiler may not hoist loads over the asm memory clobber), so 64
-    // loaded registers are live at a time instead of 128
-    fetch(0, SEQ ? 8 : K);
-    const uint32_t m4 = vgpr_const(0x0f0f0f0fu), m2 = vgpr_const(0x33333333u), m1 = vgpr_const(0x55555555u);
-    uint32_t P[64], O[32];
-    auto planes = [&](int c0) {
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            uint32_t w[8] = {a[c0 + c].x, a[c0 + c].y, a[c0 + c].z, a[c0 + c].w,
-                             b[c0 + c].x, b[c0 + c].y, b[c0 + c].z, b[c0 + c].w};
-            dma::transpose(w, m4, m2, m1);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) P[8 * c + j] = w[j];
-        }
-    };
-    planes(0);
-    if constexpr (K == 8) {
-        xn::rs84_encode_planes(P, O);
-    } else {
-        xn::rs164_planes_lo(P, O);
-        if constexpr (SEQ) {
-            asm volatile("" ::: "memory");
-            fetch(8, 16);
-        }
-        planes(8);
-        xn::rs164_planes_hi(P, O);
-    }
-#pragma unroll
-    for (int r = 0; r < M; ++r) {
-        uint32_t w[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) w[i] = O[8 * r + i];
-        dma::transpose(w, m4, m2, m1);
-        uint8_t* dst = obase + p.out_off[r] + off;
-        if constexpr (NT & 2) {
-            st16_nt(dst, make_uint4(w[0], w[1], w[2], w[3]));
-            st16_nt(dst + HOFF, make_uint4(w[4], w[5], w[6], w[7]));
-        } else {
-            st16(dst, make_uint4(w[0], w[1], w[2], w[3]));
-            st16(dst + HOFF, make_uint4(w[4], w[5], w[6], w[7]));
-        }
-    }
-}
-
-
-// Persistent, software-pipelined form of k_encode_bs: a grid of at most
-// Tuning::bs_pipe waves (one per workgroup), wave w encoding chunks w, w + G, ...
-// (G = grid size, chunk = 2 KiB column of one stripe), with the next half
-// (RS(16,4): shards 8-15 of this chunk, then 0-7 of the next) or the next
-// chunk (RS(8,4)) in flight while the current one is computed: 64 loaded
-// registers per lane stream continuously instead of one burst per wave.
-template <int K, int NT>
-__global__ __launch_bounds__(64) void k_encode_bs_pipe(const GfApplyParams p, uint64_t total) {
-    static_assert(K == 8 || K == 16, "compile-time networks: RS(8,4), RS(16,4)");
-    constexpr int M = 4;
-    const uint32_t lane = threadIdx.x;
-    const uint32_t m4 = vgpr_const(0x0f0f0f0fu), m2 = vgpr_const(0x33333333u), m1 = vgpr_const(0x55555555u);
-    const uint64_t G = gridDim.x;
-    auto at = [&](uint64_t t, const uint8_t*& src, uint8_t*& dst) {
-        const uint64_t stripe = t / p.chunks_per_stripe, chunk = t - stripe * p.chunks_per_stripe;
-        const uint64_t off = chunk * 2048u + lane * 16u;
-        src = p.base + stripe * p.stripe_stride + off;
-        dst = p.out_base + stripe * p.out_stripe_stride + off;
-    };
-    auto fetch = [&](const uint8_t* src, int c0, uint4 (&a)[8], uint4 (&b)[8]) {
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            if constexpr (NT & 1) {
-                a[c] = ld16_nt(src + p.in_off[c0 + c]);
-                b[c] = ld16_nt(src + p.in_off[c0 + c] + 1024);
-            } else {
-                a[c] = ld16(src + p.in_off[c0 + c]);
-                b[c] = ld16(src + p.in_off[c0 + c] + 1024);
-            }
-        }
-    };
-    auto planes = [&](const uint4 (&a)[8], const uint4 (&b)[8], uint32_t (&P)[64]) {
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            uint32_t w[8] = {a[c].x, a[c].y, a[c].z, a[c].w, b[c].x, b[c].y, b[c].z, b[c].w};
-            dma::transpose(w, m4, m2, m1);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) P[8 * c + j] = w[j];
-        }
-    };
-    auto store = [&](uint8_t* dst, const uint32_t (&O)[32]) {
-#pragma unroll
-        for (int r = 0; r < M; ++r) {
-            uint32_t w[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) w[i] = O[8 * r + i];
-            dma::transpose(w, m4, m2, m1);
-            uint8_t* d = dst + p.out_off[r];
-            if constexpr (NT & 2) {
-                st16_nt(d, make_uint4(w[0], w[1], w[2], w[3]));
-                st16_nt(d + 1024, make_uint4(w[4], w[5], w[6], w[7]));
-            } else {
-                st16(d, make_uint4(w[0], w[1], w[2], w[3]));
-                st16(d + 1024, make_uint4(w[4], w[5], w[6], w[7]));
-            }
-        }
-    };
-    uint64_t t = blockIdx.x;
-    if (t >= total) return;
-    const uint8_t* src;
-    uint8_t* dst;
-    at(t, src, dst);
-    uint4 a0[8], b0[8], a1[8], b1[8];
-    fetch(src, 0, a0, b0);
-    if constexpr (K == 16) {
-#pragma unroll 1
-        for (;;) {
-            fetch(src, 8, a1, b1);  // this chunk's shards 8-15, in flight during the first network
-            uint32_t P[64], O[32];
-            planes(a0, b0, P);
-            xn::rs164_planes_lo(P, O);
-            const uint64_t tn = t + G;
-            const uint8_t* srcn = src;
-            uint8_t* dstn = dst;
-            if (tn < total) {  // wave-uniform
-                at(tn, srcn, dstn);
-                fetch(srcn, 0, a0, b0);  // the next chunk's shards 0-7, in flight during the second
-            }
-            planes(a1, b1, P);
-            xn::rs164_planes_hi(P, O);
-            store(dst, O);
-            if (tn >= total) break;
-            t = tn;
-            src = srcn;
-            dst = dstn;
-        }
-    } else {
-        // two chunks per iteration, alternating register sets
-#pragma unroll 1
-        for (;;) {
-            const uint64_t t1 = t + G;
-            const uint8_t* src1 = src;
-            uint8_t* dst1 = dst;
-            if (t1 < total) {
-                at(t1, src1, dst1);
-                fetch(src1, 0, a1, b1);
-            }
-            {
-                uint32_t P[64], O[32];
-                planes(a0, b0, P);
-                xn::rs84_encode_planes(P, O);
-                store(dst, O);
-            }
-            if (t1 >= total) break;
-            const uint64_t t2 = t1 + G;
-            if (t2 < total) {
-                at(t2, src, dst);
-                fetch(src, 0, a0, b0);
-            }
-            {
-                uint32_t P[64], O[32];
-                planes(a1, b1, P);
-                xn::rs84_encode_planes(P, O);
-                store(dst1, O);
-            }
-            if (t2 >= total) break;
-            t = t2;
-        }
-    }
-}
-
-
 template <int K, int M, int NE = dma::EW, int NT = 0, int SP = dma::SPW>
 __global__ __launch_bounds__((64 * dma::Shape<K, M, NE, SP>::WAVES)) void k_encode_hash_dma(const GfApplyParams p,
                                                                                           const HashParams h) {
@@ -1325,11 +1117,6 @@ const Tuning& tuning() {
         v.dma_spw = num("RSG_DMA_SPW", 8, 4, 8) == 4 ? 4 : 8;
         v.get_prio = num("RSG_DMA_PRIO", 2, 0, 3);
         v.test_fail_subbatch = num("RSG_TEST_FAIL_SUBBATCH", -1, 0, 1 << 30);
-        v.bitslice = num("RSG_BITSLICE", -1, 0, 1);
-        v.bs_nt = num("RSG_BS_NT", 0, 0, 3);
-        v.bs_occ = num("RSG_BS_OCC", 0, 0, 5);
-        v.bs_seq = flag("RSG_BS_SEQ", false);
-        v.bs_pipe = num("RSG_BS_PIPE", 0, 0, 1 << 20);
         return v;
     }();
     return t;
@@ -1412,72 +1199,7 @@ static GfKernel pick_byte(int R) {
     return nullptr;
 }
 
-template <int K>
-static bool tables_match(const GfApplyParams& p);
-
-// Bit-sliced encode (k_encode_bs): plain STORE launches of a compile-time
-// matrix in whole 2 KiB column chunks, 16-byte aligned.  Tuning::bitslice:
-// -1 (default) RS(16,4) only, 0 never, 1 also RS(8,4) (A/B runs).
-static bool bs_supported(const GfApplyParams& p, uint64_t n_stripes) {
-    const int sel = tuning().bitslice;
-    if (sel == 0 || p.R != 4 || !(p.C == 16 || (sel == 1 && p.C == 8))) return false;
-    if (p.mode != GF_MODE_STORE || p.copy_mask || p.units == 0 || p.units % 128 || n_stripes == 0) return false;
-    if ((uint64_t)(p.units / 128) * n_stripes > 0x7fffffffull) return false;
-    if ((uintptr_t)p.base % 16 || (uintptr_t)p.out_base % 16 || p.stripe_stride % 16 || p.out_stripe_stride % 16)
-        return false;
-    for (uint32_t c = 0; c < p.C; ++c)
-        if (p.in_off[c] % 16) return false;
-    for (int r = 0; r < 4; ++r)
-        if (p.out_off[r] % 16) return false;
-    return p.C == 16 ? tables_match<16>(p) : tables_match<8>(p);
-}
-
-template <int K, int OCC, bool SEQ>
-static GfKernel pick_bs_nt(int nt) {
-    switch (nt) {
-        case 1: return k_encode_bs<K, 1, OCC, SEQ>;
-        case 2: return k_encode_bs<K, 2, OCC, SEQ>;
-        case 3: return k_encode_bs<K, 3, OCC, SEQ>;
-    }
-    return k_encode_bs<K, 0, OCC, SEQ>;
-}
-
-template <int K, bool SEQ>
-static GfKernel pick_bs(int nt, int occ) {
-    switch (occ) {
-        case 3: return pick_bs_nt<K, 3, SEQ>(nt);
-        case 4: return pick_bs_nt<K, 4, SEQ>(nt);
-        case 5: return pick_bs_nt<K, 5, SEQ>(nt);
-    }
-    return pick_bs_nt<K, 1, SEQ>(nt);
-}
-
-static hipError_t launch_encode_bs(GfApplyParams p, uint64_t n_stripes, hipStream_t stream) {
-    p.chunks_per_stripe = p.units / 128;
-    p.n_store = getenv("RSG_BS_CONTIG") ? 1u : 0u;  // experiment: lane-contiguous 32 bytes
-    if (tuning().bs_pipe > 0) {  // persistent, pipelined: bs_pipe waves at most
-        const uint64_t total = (uint64_t)p.chunks_per_stripe * n_stripes;
-        const dim3 g((uint32_t)std::min<uint64_t>(total, (uint64_t)tuning().bs_pipe));
-        const int nt = tuning().bs_nt;
-        using PipeKernel = void (*)(const GfApplyParams, uint64_t);
-        PipeKernel k;
-        if (p.C == 16) k = nt == 3 ? k_encode_bs_pipe<16, 3> : nt == 2 ? k_encode_bs_pipe<16, 2> :
-                           nt == 1 ? k_encode_bs_pipe<16, 1> : k_encode_bs_pipe<16, 0>;
-        else k = nt == 3 ? k_encode_bs_pipe<8, 3> : nt == 2 ? k_encode_bs_pipe<8, 2> :
-                 nt == 1 ? k_encode_bs_pipe<8, 1> : k_encode_bs_pipe<8, 0>;
-        hipLaunchKernelGGL(k, g, dim3(64), 0, stream, p, total);
-        return hipGetLastError();
-    }
-    const dim3 grid((uint32_t)(p.chunks_per_stripe * n_stripes));
-    const int nt = tuning().bs_nt, occ = tuning().bs_occ;
-    const GfKernel k = p.C == 8 ? pick_bs<8, false>(nt, occ)
-                       : tuning().bs_seq ? pick_bs<16, true>(nt, occ) : pick_bs<16, false>(nt, occ);
-    hipLaunchKernelGGL(k, grid, dim3(64), 0, stream, p);
-    return hipGetLastError();
-}
-
 hipError_t launch_gf_apply_vec(GfApplyParams p, uint64_t n_stripes, hipStream_t stream) {
-    if (bs_supported(p, n_stripes)) return launch_encode_bs(p, n_stripes, stream);
     const bool pre = p.mode != GF_MODE_STORE || p.copy_mask != 0;
     GfKernel k = pick_vec((int)p.C, (int)p.R, pre);
     if (!k || p.units == 0 || n_stripes == 0) return hipErrorInvalidValue;
@@ -1576,37 +1298,34 @@ bool fused_supported(int C, int R, uint64_t shard_len) {
            shard_len % kFusedChunk == 0 && shard_len / kFusedChunk <= 0xffffffffull;
 }
 
-// The compile-time-matrix kernels (DMA, wide, bit-sliced encode) bake a
-// geometry's encode matrix in: they are selected only when the launch's
-// coefficient tables are exactly EncodeRows<K, 4>'s (an encode launch).
-template <int K>
-static bool tables_match(const GfApplyParams& p) {
+// The DMA kernel bakes the RS(8,4) encode matrix in at compile time: it is
+// selected only when the launch's coefficient tables are exactly that
+// matrix's (an encode launch, in place, a3-style layout), 16-byte aligned
+// (LDS-DMA moves 16 B per lane) and whole 512-byte steps.
+static bool dma_tables_match(const GfApplyParams& p) {
     static const auto want = [] {
-        constexpr bs::EncodeRows<K, 4> E{};
-        std::array<uint32_t, 4 * K * 5> t{};
+        constexpr bs::EncodeRows<8, 4> E{};
+        std::array<uint32_t, 4 * 8 * 5> t{};
         for (int r = 0; r < 4; ++r)
-            for (int c = 0; c < K; ++c) {
+            for (int c = 0; c < 8; ++c) {
                 const uint8_t co = E.g[r][c];
                 auto pack = [&](int sh, int f) {
                     uint32_t v = 0;
                     for (int i = 0; i < 4; ++i) v |= (uint32_t)bs::gmul(co, (uint8_t)((f + i) << sh)) << (8 * i);
                     return v;
                 };
-                uint32_t* d = &t[(r * K + c) * 5];
+                uint32_t* d = &t[(r * 8 + c) * 5];
                 d[0] = pack(0, 0); d[1] = pack(0, 4); d[2] = pack(3, 0); d[3] = pack(3, 4); d[4] = pack(6, 0);
             }
         return t;
     }();
-    if (p.C != (uint32_t)K || p.R != 4) return false;
     for (int r = 0; r < 4; ++r)
-        for (int c = 0; c < K; ++c)
+        for (int c = 0; c < 8; ++c)
             for (int q = 0; q < 5; ++q)
-                if (p.tab[r][c][q] != want[(r * K + c) * 5 + q]) return false;
+                if (p.tab[r][c][q] != want[(r * 8 + c) * 5 + q]) return false;
     return true;
 }
 
-// The DMA kernel: an in-place RS(8,4) encode (a3-style layout), 16-byte
-// aligned (LDS-DMA moves 16 B per lane), whole 512-byte steps.
 static bool dma_supported(const GfApplyParams& p, uint64_t shard_len, uint64_t n_stripes) {
     if (p.C != 8 || p.R != 4 || p.mode != GF_MODE_STORE || p.copy_mask || p.base != p.out_base ||
         p.stripe_stride != p.out_stripe_stride || n_stripes == 0 || n_stripes > 0x7fffffffull * dma::SPW)
@@ -1618,7 +1337,7 @@ static bool dma_supported(const GfApplyParams& p, uint64_t shard_len, uint64_t n
         if (p.in_off[c] % 16) return false;
     for (int r = 0; r < 4; ++r)
         if (p.out_off[r] % 8) return false;
-    return tables_match<8>(p);
+    return dma_tables_match(p);
 }
 
 static hipError_t launch_encode_hash_dma(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,

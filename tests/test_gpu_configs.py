@@ -187,48 +187,6 @@ def test_dma_kernel_ab_variants(gpu, oracle, env):
         assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (env, n, r.stdout[-500:], r.stderr[-2000:])
 
 
-_BS_SNIPPET = r"""
-import sys, numpy as np, torch
-sys.path.insert(0, {root!r})
-from rustfs_amd import Erasure
-from oracle import oracle as O
-for k, m, S, n in {cases!r}:
-    g = torch.Generator(device="cuda").manual_seed(S + n + k)
-    st = torch.zeros((n, k + m, S), dtype=torch.uint8, device="cuda")
-    st[:, :k] = torch.randint(0, 256, (n, k, S), dtype=torch.uint8, device="cuda", generator=g)
-    st[:, k:] = 0xA5
-    Erasure(k, m, k * S).encode_batch(st)
-    torch.cuda.synchronize()
-    for s in sorted({{0, 1, n // 2, n - 1}}):
-        got = st[s].cpu().numpy(); ref = got.copy(); ref[k:] = 0
-        O.encode(k, m, ref)
-        assert np.array_equal(got[k:], ref[k:]), (k, m, S, n, s)
-print("ok")
-"""
-
-# shard lengths: whole 2 KiB chunks (the bit-sliced kernel), one chunk, and
-# lengths it must leave to the table kernels (a 16-byte tail, 1 KiB steps)
-_BS_CASES = [(16, 4, 65536, 37), (16, 4, 2048, 5), (16, 4, 6144, 300), (16, 4, 2064, 3), (16, 4, 1024, 9),
-             (8, 4, 131072, 33), (8, 4, 2048, 7), (8, 4, 4112, 5)]
-
-
-@pytest.mark.parametrize("env", [{}, {"RSG_BITSLICE": "1"}, {"RSG_BITSLICE": "1", "RSG_BS_NT": "3"},
-                                 {"RSG_BITSLICE": "0"}, {"RSG_BITSLICE": "1", "RSG_BS_PIPE": "37"},
-                                 {"RSG_BS_SEQ": "1", "RSG_BS_OCC": "3"}, {"RSG_BITSLICE": "1", "RSG_BS_CONTIG": "1"}])
-def test_bitsliced_encode_variants(gpu, oracle, env):
-    """The bit-sliced encode (k_encode_bs: RS(16,4) by default, RS(8,4) too
-    with RSG_BITSLICE=1, non-temporal with RSG_BS_NT=3) and the table kernels
-    it replaces, parity vs the oracle on sampled stripes; each knob setting
-    runs in its own process (read once per process)."""
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-c", _BS_SNIPPET.format(root=root, cases=_BS_CASES)],
-                       env={**os.environ, **env}, capture_output=True, text=True, timeout=150)
-    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (env, r.stdout[-500:], r.stderr[-2000:])
-
-
 _WIDE_SNIPPET = r"""
 import sys, numpy as np, torch
 sys.path.insert(0, {root!r})
