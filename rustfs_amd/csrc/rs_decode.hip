@@ -45,7 +45,7 @@ namespace rsg {
 // profiles/r02/ab_prio/).  Tuning::get_prio overrides it for A/B runs.
 static uint32_t dma_prio() { return (uint32_t)tuning().get_prio; }
 
-template <int NF, int G, int TH = 0, int GS = 1>
+template <int NF, int G, int TH = 0>
 struct GetShape {
     static constexpr int SPW = G, HS = G / 2;             // stripes per workgroup, per DMA half
     static constexpr int NI = HS * NF;                    // DMA instructions per step
@@ -54,23 +54,20 @@ struct GetShape {
     static constexpr int LAST = NI - 8 * (HW - 1);        // instructions of the last one
     static constexpr uint32_t TSLOT = SPW * (TH ? TH : 1) * dma::PP;  // one step of target rows
     static constexpr int TW = (SPW * TH + 15) / 16;       // target-hasher waves
-    static constexpr int GW = SPW * GS;                   // GF waves (GS per stripe)
-    static constexpr int WAVES = HW + GW + TW;
+    static constexpr int WAVES = HW + SPW + TW;
 };
 
-template <int C, int NF, int G, int TH, int GS>
-__global__ __launch_bounds__((64 * GetShape<NF, G, TH, GS>::WAVES)) void k_decode_records_dma(const GfApplyParams p,
-                                                                                              const HashParams h) {
+template <int C, int NF, int G, int TH>
+__global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_records_dma(const GfApplyParams p,
+                                                                                          const HashParams h) {
     static_assert(C >= 1 && C <= kMaxC && NF >= C && NF <= C + 4 && TH <= 4 && NF + TH <= C + 4, "RS(C, <= 4)");
-    static_assert(GS == 1 || GS == 2, "one or two GF waves per stripe");
-    static_assert(GetShape<NF, G, TH, GS>::WAVES <= 16, "a workgroup holds at most 16 waves");
     using dma::CH;
     using dma::D;
     using dma::IP;
     using dma::read16;
     using dma::vmcnt_imm;
     using dma::PP;
-    using L = GetShape<NF, G, TH, GS>;
+    using L = GetShape<NF, G, TH>;
     constexpr int SPW = L::SPW, HS = L::HS;
     constexpr int RM = 4;
     __shared__ __attribute__((aligned(16))) uint8_t ring[D * L::DSLOT];
@@ -88,10 +85,10 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH, GS>::WAVES)) void k_decod
     }
     // (the tables are published by B(0), which every wave passes before use)
 
-    if (TH && wave >= (uint32_t)(L::HW + L::GW)) {
+    if (TH && wave >= (uint32_t)(L::HW + SPW)) {
         // ------------- target hasher: quad j hashes target row stream -------------
         if (p.wave_prio & kPrioHash) __builtin_amdgcn_s_setprio(2);
-        const uint32_t pi = 16 * (wave - L::HW - L::GW) + (lane >> 2);  // r * SPW + stripe
+        const uint32_t pi = 16 * (wave - L::HW - SPW) + (lane >> 2);  // r * SPW + stripe
         const bool on = pi < (uint32_t)(SPW * TH);
         const uint32_t r = on ? pi / SPW : 0, e = pi % SPW;
         const bool live = on && s0 + e < n;
@@ -113,29 +110,13 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH, GS>::WAVES)) void k_decod
         return;
     }
     if (wave >= (uint32_t)L::HW) {
-        // ---------------- GF wave: one stripe (GS = 2: half its rows) ----------------
+        // ------------------------- GF wave: one stripe -------------------------
         if (p.wave_prio & kPrioGf) __builtin_amdgcn_s_setprio(2);
-        const uint32_t gi = wave - L::HW, e = gi / GS, half_id = gi % GS;
+        const uint32_t e = wave - L::HW;
         const uint64_t stripe = s0 + e;
         const bool live = stripe < n;
         uint8_t* ob = p.out_base + (live ? stripe : 0) * p.out_stripe_stride + lane * 8u;
-        const uint32_t R = p.R, nst = p.n_store;
-        // GS = 2: the stripe's two GF waves split its rows — stored rows on
-        // wave 0 and compared rows on wave 1 when there are both (so one wave
-        // owns the stripe's surplus verdict), else alternate rows — and its
-        // copy-through survivors (alternate); each still extracts the fields
-        // of all C survivors
-        uint32_t rmask = (1u << R) - 1u;
-        uint32_t cmask = p.copy_mask;
-        bool owns_verdict = true;
-        if constexpr (GS == 2) {
-            const uint32_t stored = (1u << nst) - 1u;
-            if (nst > 0 && nst < R) rmask = half_id ? rmask & ~stored : stored;
-            else if (nst == 0) rmask = half_id ? 0u : rmask;
-            else rmask &= half_id ? 0xAu : 0x5u;
-            owns_verdict = (nst > 0 && nst < R) ? half_id == 1 : half_id == 0;
-            cmask &= half_id ? 0xAAAAu : 0x5555u;
-        }
+        const uint32_t R = p.R, nst = p.n_store, cmask = p.copy_mask;
         const uint32_t m7 = vgpr_const(0x07070707u), m3 = vgpr_const(0x03030303u);
         // row of present file f for this stripe: instruction f*HS + e%HS, half e/HS
         const uint32_t roff = (e % HS) * IP + (e / HS) * CH + lane * 8u;
@@ -161,7 +142,6 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH, GS>::WAVES)) void k_decod
 #pragma unroll
                 for (int r = 0; r < RM; ++r) {
                     if ((uint32_t)r >= R) break;  // wave-uniform
-                    if (GS > 1 && !((rmask >> r) & 1u)) continue;
                     const uint8_t* tp = tb + (c * RM + r) * 32;
                     const uint4 t4 = *(const uint4*)tp;
                     const uint32_t t2 = *(const uint32_t*)(tp + 16);
@@ -174,7 +154,6 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH, GS>::WAVES)) void k_decod
 #pragma unroll
             for (int r = 0; r < RM; ++r) {
                 if ((uint32_t)r >= R) break;
-                if (GS > 1 && !((rmask >> r) & 1u)) continue;
                 const uint2 v = make_uint2(acc[r][0], acc[r][1]);
                 if ((uint32_t)r < nst) {
                     if (live) st16_nt_half(ob + p.out_off[r] + (uint64_t)s * CH, v);
@@ -194,7 +173,7 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH, GS>::WAVES)) void k_decod
         }
         // the stripe's surplus verdict, written whole (no memset before the launch)
         const bool any_bad = __builtin_amdgcn_ballot_w64(bad) != 0;
-        if (live && nst < R && owns_verdict && lane == 0) p.ok_flags[stripe] = any_bad ? 0 : 1;
+        if (live && nst < R && lane == 0) p.ok_flags[stripe] = any_bad ? 0 : 1;
         return;
     }
     // ------------------------- DMA + verify-hash wave -------------------------
@@ -271,60 +250,50 @@ static_assert(dma::D * (get_group(16) / 2) * 19 * dma::IP + 16 * 4 * 32 + 2 * 4 
               "RS(16,4) one-pass ring fits the LDS");
 static_assert(dma::D * (get_group(8) / 2) * 11 * dma::IP + 8 * 4 * 32 <= 160 * 1024, "RS(8,4) ring fits the LDS");
 
-template <int C, int NF, int G, int TH, int GS>
+template <int C, int NF, int G, int TH = 0>
 static void launch_get(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
-    hipLaunchKernelGGL((k_decode_records_dma<C, NF, G, TH, GS>), dim3((uint32_t)blocks),
-                       dim3(64 * GetShape<NF, G, TH, GS>::WAVES), 0, stream, p, h);
+    hipLaunchKernelGGL((k_decode_records_dma<C, NF, G, TH>), dim3((uint32_t)blocks),
+                       dim3(64 * GetShape<NF, G, TH>::WAVES), 0, stream, p, h);
 }
 
-// nf present files -> the k_decode_records_dma<C, NF, G, TH, GS> instantiation
-template <int C, int G, int TH, int GS, int NF>
+// nf present files -> the k_decode_records_dma<C, NF, G, TH> instantiation
+template <int C, int G, int TH, int NF>
 static bool launch_get_nf(int nf, uint64_t n_stripes, const GfApplyParams& p, const HashParams& h,
                           hipStream_t stream) {
     if constexpr (NF + (TH ? TH : 1) > C + 4) {
         return false;
     } else {
-        if (nf != NF) return launch_get_nf<C, G, TH, GS, NF + 1>(nf, n_stripes, p, h, stream);
+        if (nf != NF) return launch_get_nf<C, G, TH, NF + 1>(nf, n_stripes, p, h, stream);
         const uint64_t blocks = (n_stripes + G - 1) / G;
         if (blocks > 0x7fffffffull) return false;
-        launch_get<C, NF, G, TH, GS>(blocks, p, h, stream);
+        launch_get<C, NF, G, TH>(blocks, p, h, stream);
         return true;
     }
 }
 
-template <int C, int G, int GS>
+template <int C, int G>
 static bool launch_get_th(int nf, int th, uint64_t n_stripes, const GfApplyParams& p, const HashParams& h,
                           hipStream_t stream) {
+    if constexpr (C > 8) {  // no one-pass heal above 8 survivors (heal_dma_supported)
+        return th == 0 && launch_get_nf<C, G, 0, C>(nf, n_stripes, p, h, stream);
+    }
     switch (th) {
-        case 0: return launch_get_nf<C, G, 0, GS, C>(nf, n_stripes, p, h, stream);
-        case 1: return launch_get_nf<C, G, 1, GS, C>(nf, n_stripes, p, h, stream);
-        case 2: return launch_get_nf<C, G, 2, GS, C>(nf, n_stripes, p, h, stream);
-        case 3: return launch_get_nf<C, G, 3, GS, C>(nf, n_stripes, p, h, stream);
-        case 4: return launch_get_nf<C, G, 4, GS, C>(nf, n_stripes, p, h, stream);
+        case 0: return launch_get_nf<C, G, 0, C>(nf, n_stripes, p, h, stream);
+        case 1: return launch_get_nf<C, G, 1, C>(nf, n_stripes, p, h, stream);
+        case 2: return launch_get_nf<C, G, 2, C>(nf, n_stripes, p, h, stream);
+        case 3: return launch_get_nf<C, G, 3, C>(nf, n_stripes, p, h, stream);
+        case 4: return launch_get_nf<C, G, 4, C>(nf, n_stripes, p, h, stream);
     }
     return false;
-}
-
-// GF waves per stripe: 2 at RS(16,4) (16 survivors per wave otherwise set
-// the step time), 1 below; Tuning::get_gs forces one (GS = 2 at RS(8,4)
-// runs four stripes per workgroup: 16 waves at most per workgroup).
-static int get_gs(int k) {
-    const int f = tuning().get_gs;
-    if (k < 8) return 1;
-    return f ? f : (k > 8 ? 2 : 1);
 }
 
 static bool launch_get_any(int k, int nf, int th, uint64_t n_stripes, const GfApplyParams& p, const HashParams& h,
                            hipStream_t stream) {
     switch (k) {
-        case 2: return launch_get_th<2, get_group(2), 1>(nf, th, n_stripes, p, h, stream);
-        case 4: return launch_get_th<4, get_group(4), 1>(nf, th, n_stripes, p, h, stream);
-        case 8:
-            return get_gs(8) == 2 ? launch_get_th<8, 4, 2>(nf, th, n_stripes, p, h, stream)
-                                  : launch_get_th<8, get_group(8), 1>(nf, th, n_stripes, p, h, stream);
-        case 16:
-            return get_gs(16) == 2 ? launch_get_th<16, get_group(16), 2>(nf, th, n_stripes, p, h, stream)
-                                   : launch_get_th<16, get_group(16), 1>(nf, th, n_stripes, p, h, stream);
+        case 2: return launch_get_th<2, get_group(2)>(nf, th, n_stripes, p, h, stream);
+        case 4: return launch_get_th<4, get_group(4)>(nf, th, n_stripes, p, h, stream);
+        case 8: return launch_get_th<8, get_group(8)>(nf, th, n_stripes, p, h, stream);
+        case 16: return launch_get_th<16, get_group(16)>(nf, th, n_stripes, p, h, stream);
     }
     return false;
 }
@@ -340,13 +309,12 @@ bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len) {
     return one_pass_geometry(k, m, shard_len) && nf >= k && nf < k + m;
 }
 
-// One-pass heal: k <= 8, and RS(16,4) with two GF waves per stripe (with
-// one, its four GF waves per workgroup — 16 survivors x 4 rows each — set the
-// pace and the two-pass path was faster: one data + one parity disk, n =
-// 4096, 2.14 ms one-pass against 1.98 ms; profiles/r03/eng_ab/).
+// One-pass heal for k <= 8: at RS(16,4) its four GF waves per workgroup (16
+// survivors x 4 rows each) set the pace and the two-pass path is faster
+// (n = 4096, one data + one parity disk: 2.14 ms one-pass, 1.98 ms two-pass;
+// profiles/r03/eng_ab/).
 bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len) {
-    return one_pass_geometry(k, m, shard_len) && (k <= 8 || get_gs(k) == 2) && nf >= k && targets >= 1 &&
-           nf + targets <= k + m;
+    return one_pass_geometry(k, m, shard_len) && k <= 8 && nf >= k && targets >= 1 && nf + targets <= k + m;
 }
 
 static bool dma_records_aligned(const HashParams& h, int nf) {

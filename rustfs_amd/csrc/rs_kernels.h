@@ -39,7 +39,6 @@ struct Tuning {
     int dma_nt = 3;               // RSG_DMA_NT=<0..3>: non-temporal loads (bit 0) / stores (bit 1)
     int dma_spw = 8;              // RSG_DMA_SPW=4: four stripes per fused DMA workgroup
     int get_prio = 2;             // RSG_DMA_PRIO=<0..3>: wave priorities of the one-pass GET/heal
-    int get_gs = 0;               // RSG_GET_GS=1|2: GF waves per stripe of the one-pass GET/heal at k >= 8 (0: by k)
     // fault injection (tests only): RSG_TEST_FAIL_SUBBATCH=<i> makes sub-batch
     // i of every rsg_encode_batch_host_submit fail to enqueue (-1: never)
     int test_fail_subbatch = -1;

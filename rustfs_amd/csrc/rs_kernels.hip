@@ -1116,7 +1116,6 @@ const Tuning& tuning() {
         v.dma_nt = num("RSG_DMA_NT", 3, 0, 3);
         v.dma_spw = num("RSG_DMA_SPW", 8, 4, 8) == 4 ? 4 : 8;
         v.get_prio = num("RSG_DMA_PRIO", 2, 0, 3);
-        v.get_gs = num("RSG_GET_GS", 0, 1, 2);
         v.test_fail_subbatch = num("RSG_TEST_FAIL_SUBBATCH", -1, 0, 1 << 30);
         return v;
     }();

@@ -238,58 +238,3 @@ def test_heal_one_pass_many_workgroups(gpu, oracle, k, m, lost):
             ok[b] = False
             assert not bool(got[b, :32].any())  # digest zeroed: never verifies
         assert torch.equal(got[ok], ref[ok]), f"shard {i}"
-
-
-_GS_SNIPPET = r"""
-import sys, torch
-sys.path.insert(0, {root!r})
-from rustfs_amd import Erasure
-S, n = 4096, 2051
-rec = 32 + S
-for k, m, heal_lost, get_lost in ((8, 4, (1, 8), (0, 3)), (8, 4, (0, 5, 9), (2,)), (16, 4, (3, 16), (0, 7)),
-                                  (16, 4, (0, 7, 15, 19), (5,))):
-    e = Erasure(k, m, k * S)
-    g = torch.Generator(device="cuda").manual_seed(k * 100 + len(heal_lost))
-    st = torch.zeros((n, k + m, S), dtype=torch.uint8, device="cuda")
-    st[:, :k] = torch.randint(0, 256, (n, k, S), dtype=torch.uint8, device="cuda", generator=g)
-    dig = torch.zeros((n, k + m, 32), dtype=torch.uint8, device="cuda")
-    e.encode_batch(st, dig)
-    files = [torch.cat([dig[:, i], st[:, i]], dim=1).contiguous().reshape(-1) for i in range(k + m)]
-    src = [None if i in heal_lost else files[i] for i in range(k + m)]
-    tgt = [torch.zeros(n * rec, dtype=torch.uint8, device="cuda") if i in heal_lost else None for i in range(k + m)]
-    assert e.heal_records_batch(src, tgt, S, n) == [0] * n, (k, m, heal_lost)
-    for i in heal_lost:
-        assert torch.equal(tgt[i], files[i]), (k, m, heal_lost, i)
-    # an inconsistent (re-hashed) surplus parity fails its stripe alone
-    bad = [f.clone() for f in files]
-    body = bad[k + m - 1].view(n, rec)[777, 32:]
-    body[9] ^= 0x11
-    from oracle import oracle as O
-    bad[k + m - 1].view(n, rec)[777, :32] = torch.frombuffer(bytearray(O.hh256s(body.cpu().numpy().tobytes())),
-                                                              dtype=torch.uint8).cuda()
-    out, status = e.decode_records_batch([None if i in get_lost else bad[i] for i in range(k + m)], S, n)
-    assert [i for i, x in enumerate(status) if x] == [777], (k, m, get_lost)
-    good = torch.ones(n, dtype=torch.bool, device="cuda")
-    good[777] = False
-    assert torch.equal(out.view(n, k, S)[good], st[:, :k][good]), (k, m, get_lost)
-print("ok")
-"""
-
-
-@pytest.mark.parametrize("env", [{}, {"RSG_GET_GS": "2"}, {"RSG_GET_GS": "1"}])
-def test_one_pass_gf_waves_per_stripe(gpu, engine_path, env):
-    """The one-pass GET/heal kernel with one or two GF waves per stripe
-    (RSG_GET_GS; default two at RS(16,4), one at RS(8,4); two at RS(8,4)
-    runs four stripes per workgroup): healed records identical to the
-    originals, GET output identical to the data, a re-hashed inconsistent
-    surplus parity failing its stripe alone; each setting in its own process
-    (read once per process).  The engine_path parameter only repeats it."""
-    import os
-    import subprocess
-    import sys
-    if engine_path != "one_pass":
-        pytest.skip("runs once")
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-c", _GS_SNIPPET.format(root=root)], env={**os.environ, **env},
-                       capture_output=True, text=True, timeout=160)
-    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (env, r.stdout[-500:], r.stderr[-2000:])
