@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include "rs_device.h"
+#include "rs_records.h"
 
 namespace rsg {
 
@@ -46,15 +47,8 @@ namespace rsg {
 static uint32_t dma_prio() { return (uint32_t)tuning().get_prio; }
 
 template <int NF, int G, int TH = 0>
-struct GetShape {
-    static constexpr int SPW = G, HS = G / 2;             // stripes per workgroup, per DMA half
-    static constexpr int NI = HS * NF;                    // DMA instructions per step
-    static constexpr uint32_t DSLOT = NI * dma::IP;
-    static constexpr int HW = (NI + 7) / 8;               // DMA/hash waves
-    static constexpr int LAST = NI - 8 * (HW - 1);        // instructions of the last one
-    static constexpr uint32_t TSLOT = SPW * (TH ? TH : 1) * dma::PP;  // one step of target rows
-    static constexpr int TW = (SPW * TH + 15) / 16;       // target-hasher waves
-    static constexpr int WAVES = HW + SPW + TW;
+struct GetShape : RecRing<NF, G, TH> {
+    static constexpr int WAVES = RecRing<NF, G, TH>::HW + G + RecRing<NF, G, TH>::TW;
 };
 
 template <int C, int NF, int G, int TH>
@@ -64,8 +58,6 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_re
     using dma::CH;
     using dma::D;
     using dma::IP;
-    using dma::read16;
-    using dma::vmcnt_imm;
     using dma::PP;
     using L = GetShape<NF, G, TH>;
     constexpr int SPW = L::SPW, HS = L::HS;
@@ -73,11 +65,10 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_re
     __shared__ __attribute__((aligned(16))) uint8_t ring[D * L::DSLOT];
     __shared__ __attribute__((aligned(16))) uint8_t tabs[C * RM * 32];
     __shared__ __attribute__((aligned(16))) uint8_t trow[TH ? 2 * L::TSLOT : 16];
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u, q = lane & 3u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     const uint64_t n = h.n;
     const uint32_t steps = p.units;
     const uint64_t s0 = (uint64_t)blockIdx.x * SPW;
-    const uint32_t ring_base = (uint32_t)(uintptr_t)ring;
     for (uint32_t i = threadIdx.x; i < (uint32_t)(C * RM); i += blockDim.x) {
         const int c = i / RM, r = i % RM;
         *(uint4*)(tabs + i * 32) = make_uint4(p.tab[r][c][0], p.tab[r][c][1], p.tab[r][c][2], p.tab[r][c][3]);
@@ -86,27 +77,7 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_re
     // (the tables are published by B(0), which every wave passes before use)
 
     if (TH && wave >= (uint32_t)(L::HW + SPW)) {
-        // ------------- target hasher: quad j hashes target row stream -------------
-        if (p.wave_prio & kPrioHash) __builtin_amdgcn_s_setprio(2);
-        const uint32_t pi = 16 * (wave - L::HW - SPW) + (lane >> 2);  // r * SPW + stripe
-        const bool on = pi < (uint32_t)(SPW * TH);
-        const uint32_t r = on ? pi / SPW : 0, e = pi % SPW;
-        const bool live = on && s0 + e < n;
-        const uint32_t roff = (on ? pi : 0) * PP + 8 * q;
-        HHQuad st;
-        hhq_init(st, h.key, q);
-        lds_barrier();  // B(0)
-#pragma unroll 1
-        for (uint32_t s = 0; s <= steps; ++s) {
-            if (s > 0) {  // target rows of step s-1, published by B(s)
-                uint64_t w[16];
-                read16((uint32_t)(uintptr_t)trow + ((s - 1) & 1) * L::TSLOT + roff, w);
-#pragma unroll
-                for (int t = 0; t < 16; ++t) hhq_update(st, w[t]);
-            }
-            if (s < steps) lds_barrier();  // B(s+1)
-        }
-        if (live) hhq_finish(st, p.out_base + (s0 + e) * p.out_stripe_stride + p.out_off[r] - 32, q);
+        records_target_hasher<G, TH>(p, h, trow, wave - L::HW - SPW, steps, s0);
         return;
     }
     if (wave >= (uint32_t)L::HW) {
@@ -177,75 +148,9 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_re
         return;
     }
     // ------------------------- DMA + verify-hash wave -------------------------
-    if (p.wave_prio & kPrioHash) __builtin_amdgcn_s_setprio(2);
-    const uint32_t hw = wave, j = lane >> 2;
-    const int ndi = (hw == (uint32_t)(L::HW - 1)) ? L::LAST : 8;  // instructions this wave owns
-    const uint32_t idx = 8 * hw + (j & 7u), half = j >> 3;
-    const bool quad_on = (int)(j & 7u) < ndi;
-    const uint32_t file = quad_on ? idx / HS : 0, stripe_l = (idx % HS) + HS * half;
-    const uint32_t roff = (quad_on ? idx : 0) * IP + half * CH + 8 * q;
-    const bool live = quad_on && s0 + stripe_l < n;
-    HHQuad st;
-    hhq_init(st, h.key, q);
-    // record sources as a wave-uniform base (SGPRs) + a 32-bit per-lane
-    // offset (the upper half's stripe, or the lower one again past n): the
-    // loads take the saddr form, a step costs HS VALU adds
-    uint64_t ubo[HS];
-    uint32_t vlane[HS];
-#pragma unroll
-    for (int i = 0; i < HS; ++i) {
-        const uint64_t lo = s0 + i, hi = lo + HS;
-        ubo[i] = (lo < n ? lo : 0) * h.stripe_stride;
-        vlane[i] = (lane & 31u) * 16u + ((lane >> 5) && hi < n ? (uint32_t)(HS * h.stripe_stride) : 0u);
-    }
-    auto dma_step = [&](uint32_t step) {
-        uint32_t voff[HS];
-#pragma unroll
-        for (int i = 0; i < HS; ++i) voff[i] = vlane[i] + step * CH;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            if (k >= ndi) break;  // wave-uniform
-            const uint32_t ins = 8 * hw + k;
-            const uint8_t* src = h.base[ins / HS] + ubo[k % HS] + (uint64_t)voff[k % HS];
-            __builtin_amdgcn_global_load_lds(
-                (const void*)src, (__attribute__((address_space(3))) void*)(ring + (step % D) * L::DSLOT + ins * IP), 16,
-                0, 0);
-        }
-    };
-    auto wait_next = [&]() {  // DMA of the next step landed (D - 2 steps younger in flight)
-        if (ndi == 8) __builtin_amdgcn_s_waitcnt(vmcnt_imm((D - 2) * 8));
-        else __builtin_amdgcn_s_waitcnt(vmcnt_imm((D - 2) * L::LAST));
-    };
-#pragma unroll
-    for (int d = 0; d < D - 1; ++d) dma_step(d < (int)steps ? d : steps - 1);
-    wait_next();  // DMA(0) landed
-    lds_barrier();  // B(0)
-#pragma unroll 1
-    for (uint32_t s = 0; s < steps; ++s) {
-        dma_step(s + D - 1 < steps ? s + D - 1 : steps - 1);  // into the slot step s-1 used
-        uint64_t w[16];
-        read16(ring_base + (s % D) * L::DSLOT + roff, w);
-#pragma unroll
-        for (int t = 0; t < 16; ++t) hhq_update(st, w[t]);
-        wait_next();
-        lds_barrier();  // B(s+1)
-    }
-    __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // the clamped tail DMA has landed before the wave ends
-    // verify before use (split_and_verify, bitrot.rs:227-247): lane 0 of each
-    // live quad writes its record's flag whole (no memset before the launch)
-    const uint64_t d = hhq_digest(st, q);
-    bool mis = false;
-    if (live) mis = d != ld64_any(h.base[file] + (s0 + stripe_l) * h.stripe_stride - 32 + 8 * q);
-    const uint64_t bal = __builtin_amdgcn_ballot_w64(mis);
-    if (live && q == 0) h.flag_base[file][s0 + stripe_l] = ((bal >> lane) & 0xFull) ? 0 : 1;
+    records_hash_wave<NF, G>(h, p.wave_prio, ring, wave, steps, s0);
 }
 
-// Stripes per workgroup of the one-pass GET/heal kernel for C survivors: 8
-// (one workgroup of 13 waves per CU at RS(8,4)) while the ring of 3 x G/2 x
-// NF KiB-rows fits the LDS, 4 for C = 16 (RS(16,4): up to 19 present files).
-// (Four stripes per workgroup at RS(8,4) — two workgroups of 7 waves per CU —
-// measured no faster, profiles/r02/ab_eng/.)
-constexpr int get_group(int C) { return C > 8 ? 4 : 8; }
 static_assert(dma::D * (get_group(16) / 2) * 19 * dma::IP + 16 * 4 * 32 + 2 * 4 * 4 * dma::PP <= 160 * 1024,
               "RS(16,4) one-pass ring fits the LDS");
 static_assert(dma::D * (get_group(8) / 2) * 11 * dma::IP + 8 * 4 * 32 <= 160 * 1024, "RS(8,4) ring fits the LDS");
@@ -317,6 +222,26 @@ bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len) {
     return one_pass_geometry(k, m, shard_len) && k <= 8 && nf >= k && targets >= 1 && nf + targets <= k + m;
 }
 
+// RS(8,4) patterns with a compile-time XOR network (rs_decode_net.hip): the
+// launch's coefficient rows are matched byte for byte against the generated
+// table; a listed pattern runs k_decode_records_net, anything else the
+// run-time-table kernel above.  Tuning::decode_net = false (RSG_DECODE_NET=0)
+// keeps the table kernel for A/B runs.
+static bool launch_net_if_listed(int heal, int k, int m, int nf, const uint8_t* coef, uint64_t n_stripes,
+                                 const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
+    if (k != 8 || m != 4 || !coef || !tuning().decode_net || p.C != 8) return false;
+    const int pid = records_net_pattern(heal, nf, (int)p.R, (int)p.n_store, coef);
+    if (pid < 0) return false;
+    const uint64_t blocks = (n_stripes + 7) / 8;
+    if (blocks > 0x7fffffffull) return false;
+    using Part = bool (*)(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+    static const Part parts[RSG_NET_PARTS] = {launch_records_net_part0, launch_records_net_part1,
+                                              launch_records_net_part2, launch_records_net_part3,
+                                              launch_records_net_part4, launch_records_net_part5,
+                                              launch_records_net_part6, launch_records_net_part7};
+    return parts[pid % RSG_NET_PARTS](pid, blocks, p, h, stream);
+}
+
 static bool dma_records_aligned(const HashParams& h, int nf) {
     for (int f = 0; f < nf; ++f)
         if ((uintptr_t)h.base[f] % 16) return false;
@@ -325,7 +250,7 @@ static bool dma_records_aligned(const HashParams& h, int nf) {
 }
 
 hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, int nf, int targets,
-                                   uint64_t shard_len, uint64_t n_stripes, hipStream_t stream) {
+                                   uint64_t shard_len, uint64_t n_stripes, const uint8_t* coef, hipStream_t stream) {
     p.wave_prio = dma_prio();
     if (!heal_dma_supported(k, m, nf, targets, shard_len) || (int)p.C != k || n_stripes == 0 || p.R > 4 ||
         p.n_store != (uint32_t)targets || p.copy_mask || !dma_records_aligned(h, nf) ||
@@ -333,18 +258,20 @@ hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, 
         return hipErrorInvalidValue;
     p.units = (uint32_t)(shard_len / dma::CH);
     h.n = n_stripes;
+    if (launch_net_if_listed(1, k, m, nf, coef, n_stripes, p, h, stream)) return hipGetLastError();
     if (!launch_get_any(k, nf, targets, n_stripes, p, h, stream)) return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
 hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int k, int m, int nf, uint64_t shard_len,
-                                     uint64_t n_stripes, hipStream_t stream) {
+                                     uint64_t n_stripes, const uint8_t* coef, hipStream_t stream) {
     p.wave_prio = dma_prio();
     if (!decode_dma_supported(k, m, nf, shard_len) || (int)p.C != k || n_stripes == 0 || p.R > 4 ||
         p.n_store > p.R || !dma_records_aligned(h, nf))
         return hipErrorInvalidValue;
     p.units = (uint32_t)(shard_len / dma::CH);
     h.n = n_stripes;
+    if (launch_net_if_listed(0, k, m, nf, coef, n_stripes, p, h, stream)) return hipGetLastError();
     if (!launch_get_any(k, nf, 0, n_stripes, p, h, stream)) return hipErrorInvalidValue;
     return hipGetLastError();
 }

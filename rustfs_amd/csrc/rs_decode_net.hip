@@ -1,0 +1,209 @@
+// rs_decode_net.hip — the one-pass GET / heal kernel for RS(8,4) with its
+// rows as a compile-time XOR network per erasure pattern
+// (k_decode_records_net<PID>; the networks in the generated
+// rs84_decode_nets.h, tools/gen_decode_nets.py).  Compiled RSG_NET_PARTS
+// times (Makefile), part RSG_NET_PART instantiating the patterns with
+// PID % RSG_NET_PARTS == RSG_NET_PART, so the ~150 kernels build in parallel.
+//
+// Same workgroup as k_decode_records_dma (rs_decode.hip): 8 stripes, NF
+// present record files DMA'd into a 3-slot LDS ring per 512-byte step,
+// ceil(4 NF / 8) DMA + verify-hash waves (rs_records.h), heal's target rows
+// hashed one step behind by ceil(8 TH / 16) target hashers — but the 8
+// run-time-table GF waves (one per stripe: 3 v_perm + 1.5 XOR per word and
+// coefficient, v_perm at half the XOR issue rate) become 2 network waves,
+// one per 4-stripe group (stripes 2g, 2g+1, 2g+4, 2g+5: 8 bytes of each per
+// lane, as the fused encoder's k_encode_hash_dma groups): each step the wave
+// bit-transposes the 8 survivor rows into 64 planes, runs the pattern's
+// network (all R rows at once: ~250-300 three-input XORs), transposes the
+// rows back, stores the rebuilt rows (and heal's LDS row copies), compares
+// the surplus parity rows with the ring and copies GET's present data through.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include <array>
+#include <utility>
+
+#include "rs_device.h"
+#include "rs_kernels.h"
+#include "rs_records.h"
+
+#ifndef RSG_NET_PART
+#error "RSG_NET_PART (0 .. RSG_NET_PARTS-1) is set by the Makefile"
+#endif
+
+namespace rsg {
+
+#include "rs84_decode_nets.h"
+
+template <int NF, int TH>
+struct NetShape : RecRing<NF, 8, TH> {
+    static constexpr int NG = 2;  // network waves (4-stripe groups)
+    static constexpr int WAVES = RecRing<NF, 8, TH>::HW + NG + RecRing<NF, 8, TH>::TW;
+};
+
+// Network wave of 4-stripe group g (stripes 2g, 2g+1, 2g+HS, 2g+HS+1 of the
+// workgroup; lane = 8 bytes of each): pattern PID's R rows over the 8
+// survivors (present files 0..7 of the launch).
+template <int PID, int NF, int TH>
+__device__ __forceinline__ void net_wave(const GfApplyParams& p, uint64_t n, uint32_t steps, uint64_t s0, uint32_t g,
+                                         const uint8_t* ring, uint8_t* trow) {
+    using dma::CH;
+    using dma::D;
+    using dma::IP;
+    using dma::PP;
+    using L = NetShape<NF, TH>;
+    constexpr decnet::Pattern pat = decnet::kPatterns[PID];
+    constexpr int C = 8, R = pat.R, NST = pat.n_store, SPW = L::SPW, HS = L::HS;
+    static_assert(pat.nf == NF && (pat.heal ? NST : 0) == TH && R <= 4 && NST <= R, "pattern shape");
+    if (p.wave_prio & kPrioGf) __builtin_amdgcn_s_setprio(2);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t m4 = vgpr_const(0x0f0f0f0fu), m2 = vgpr_const(0x33333333u), m1 = vgpr_const(0x55555555u);
+    const uint32_t mys[4] = {2 * g, 2 * g + 1, 2 * g + HS, 2 * g + HS + 1};
+    const uint32_t cmask = p.copy_mask;
+    bool live[4];       // wave-uniform: a dead stripe (past n) computes stripe 0's rows and stores nothing
+    uint8_t* ob[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        live[j] = s0 + mys[j] < n;
+        ob[j] = p.out_base + (live[j] ? s0 + mys[j] : 0) * p.out_stripe_stride + lane * 8u;
+    }
+    // this group's 8-byte lane column of a ring row (file f: + f * HS * IP);
+    // the 4 stripes sit at +0, +IP, +CH, +IP+CH
+    const uint32_t goff = 2 * g * IP + lane * 8u;
+    bool bad[4] = {false, false, false, false};  // this lane saw a surplus-parity mismatch
+    lds_barrier();  // B(0)
+#pragma unroll 1
+    for (uint32_t s = 0; s < steps; ++s) {
+        const uint8_t* slot = ring + (s % D) * L::DSLOT + goff;
+        uint32_t P[64];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const uint8_t* row = slot + c * HS * IP;
+            const uint2 a0 = *(const uint2*)row, a1 = *(const uint2*)(row + IP);
+            const uint2 a2 = *(const uint2*)(row + CH), a3 = *(const uint2*)(row + IP + CH);
+            uint32_t w[8] = {a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y};
+            dma::transpose(w, m4, m2, m1);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) P[8 * c + j] = w[j];
+        }
+        uint32_t O[32];
+        decnet::net<PID>(P, O);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            uint32_t w[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) w[i] = O[8 * r + i];
+            dma::transpose(w, m4, m2, m1);
+            if (r < NST) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint2 v = make_uint2(w[2 * j], w[2 * j + 1]);
+                    if (live[j]) st16_nt_half(ob[j] + p.out_off[r] + (uint64_t)s * CH, v);
+                    if constexpr (TH > 0)
+                        *(uint2*)(trow + (s & 1) * L::TSLOT + (r * SPW + mys[j]) * PP + lane * 8u) = v;
+                }
+            } else {
+                const uint8_t* row = slot + (C + (r - NST)) * HS * IP;
+                const uint2 o[4] = {*(const uint2*)row, *(const uint2*)(row + IP), *(const uint2*)(row + CH),
+                                    *(const uint2*)(row + IP + CH)};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) bad[j] |= ((o[j].x ^ w[2 * j]) | (o[j].y ^ w[2 * j + 1])) != 0u;
+            }
+        }
+        if (!TH && cmask) {  // GET: the present data survivors copied through
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                if (!((cmask >> c) & 1u)) continue;  // wave-uniform
+                const uint8_t* row = slot + c * HS * IP;
+                const uint2 x[4] = {*(const uint2*)row, *(const uint2*)(row + IP), *(const uint2*)(row + CH),
+                                    *(const uint2*)(row + IP + CH)};
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (live[j]) st16_nt_half(ob[j] + p.copy_off[c] + (uint64_t)s * CH, x[j]);
+            }
+        }
+        lds_barrier();  // B(s+1): done with slot s % D
+    }
+    // each stripe's surplus verdict, written whole (no memset before the launch)
+    if constexpr (NST < R) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool any_bad = __builtin_amdgcn_ballot_w64(bad[j]) != 0;
+            if (live[j] && lane == 0) p.ok_flags[s0 + mys[j]] = any_bad ? 0 : 1;
+        }
+    }
+}
+
+template <int PID, int NF, int TH>
+__global__ __launch_bounds__((64 * NetShape<NF, TH>::WAVES)) void k_decode_records_net(const GfApplyParams p,
+                                                                                       const HashParams h) {
+    using L = NetShape<NF, TH>;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[dma::D * L::DSLOT];
+    __shared__ __attribute__((aligned(16))) uint8_t trow[TH ? 2 * L::TSLOT : 16];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t steps = p.units;
+    const uint64_t s0 = (uint64_t)blockIdx.x * L::SPW;
+    if (TH && wave >= (uint32_t)(L::HW + L::NG)) {
+        records_target_hasher<8, TH>(p, h, trow, wave - L::HW - L::NG, steps, s0);
+        return;
+    }
+    if (wave >= (uint32_t)L::HW) {
+        net_wave<PID, NF, TH>(p, h.n, steps, s0, wave - L::HW, ring, trow);
+        return;
+    }
+    records_hash_wave<NF, 8>(h, p.wave_prio, ring, wave, steps, s0);
+}
+
+using NetLaunch = void (*)(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream);
+
+template <int PID>
+static void launch_net(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
+    constexpr decnet::Pattern pat = decnet::kPatterns[PID];
+    constexpr int NF = pat.nf, TH = pat.heal ? pat.n_store : 0;
+    hipLaunchKernelGGL((k_decode_records_net<PID, NF, TH>), dim3((uint32_t)blocks), dim3(64 * NetShape<NF, TH>::WAVES),
+                       0, stream, p, h);
+}
+
+template <int PID>
+constexpr NetLaunch pick_net() {
+    if constexpr (PID % RSG_NET_PARTS == RSG_NET_PART) return &launch_net<PID>;
+    else return nullptr;
+}
+
+template <size_t... I>
+constexpr std::array<NetLaunch, sizeof...(I)> net_table(std::index_sequence<I...>) {
+    return {pick_net<(int)I>()...};
+}
+
+static const std::array<NetLaunch, decnet::kCount> kNetPart = net_table(std::make_index_sequence<decnet::kCount>{});
+
+#define RSG_NET_CAT2(a, b) a##b
+#define RSG_NET_CAT(a, b) RSG_NET_CAT2(a, b)
+
+// This part's launcher: false if pattern `pid` is instantiated elsewhere.
+bool RSG_NET_CAT(launch_records_net_part, RSG_NET_PART)(int pid, uint64_t blocks, const GfApplyParams& p,
+                                                        const HashParams& h, hipStream_t stream) {
+    if (pid < 0 || pid >= decnet::kCount || !kNetPart[pid]) return false;
+    kNetPart[pid](blocks, p, h, stream);
+    return true;
+}
+
+#if RSG_NET_PART == 0
+// The pattern whose coefficient rows equal the launch's (R x 8, row-major),
+// or -1: matched byte for byte, so a network is only ever run on exactly the
+// matrix it was generated for.
+int records_net_pattern(int heal, int nf, int R, int n_store, const uint8_t* coef) {
+    for (int i = 0; i < decnet::kCount; ++i) {
+        const decnet::Pattern& pt = decnet::kPatterns[i];
+        if (pt.heal != heal || pt.nf != nf || pt.R != R || pt.n_store != n_store) continue;
+        bool eq = true;
+        for (int r = 0; r < R && eq; ++r)
+            for (int c = 0; c < 8 && eq; ++c) eq = pt.coef[r][c] == coef[r * 8 + c];
+        if (eq) return i;
+    }
+    return -1;
+}
+#endif
+
+}  // namespace rsg

@@ -39,6 +39,7 @@ struct Tuning {
     int dma_nt = 3;               // RSG_DMA_NT=<0..3>: non-temporal loads (bit 0) / stores (bit 1)
     int dma_spw = 8;              // RSG_DMA_SPW=4: four stripes per fused DMA workgroup
     int get_prio = 2;             // RSG_DMA_PRIO=<0..3>: wave priorities of the one-pass GET/heal
+    bool decode_net = true;       // RSG_DECODE_NET=0: run-time-table GF waves for every one-pass pattern
     // fault injection (tests only): RSG_TEST_FAIL_SUBBATCH=<i> makes sub-batch
     // i of every rsg_encode_batch_host_submit fail to enqueue (-1: never)
     int test_fail_subbatch = -1;
@@ -118,14 +119,35 @@ bool fused_supported(int C, int R, uint64_t shard_len);
 // 16}, m <= 4, over nf (k..k+m-1) present record files: false if the shape
 // is not supported.
 bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len);
+// coef: the launch's R x k coefficient rows (host memory, row-major), matched
+// against the compile-time XOR-network patterns (rs_decode_net.hip); may be null.
 hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int k, int m, int nf, uint64_t shard_len,
-                                     uint64_t n_stripes, hipStream_t stream);
+                                     uint64_t n_stripes, const uint8_t* coef, hipStream_t stream);
 // One-pass heal (k_decode_records_dma with target hashing), the same
 // geometries with k <= 8: nf present source files, `targets` absent target
 // files written with digests (nf + targets <= k + m).
 bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len);
 hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, int nf, int targets,
-                                   uint64_t shard_len, uint64_t n_stripes, hipStream_t stream);
+                                   uint64_t shard_len, uint64_t n_stripes, const uint8_t* coef, hipStream_t stream);
+
+// The one-pass GET/heal kernel with compile-time XOR networks
+// (rs_decode_net.hip, k_decode_records_net): RS(8,4) patterns of one or two
+// lost shards (rs84_decode_nets.h), built in RSG_NET_PARTS translation units.
+#define RSG_NET_PARTS 8
+// pattern id whose (heal, nf, R, n_store, R x 8 rows) equal the launch's, or -1
+int records_net_pattern(int heal, int nf, int R, int n_store, const uint8_t* coef);
+#define RSG_NET_PART_DECL(i)                                                                               \
+    bool launch_records_net_part##i(int pid, uint64_t blocks, const GfApplyParams& p, const HashParams& h, \
+                                    hipStream_t stream);
+RSG_NET_PART_DECL(0)
+RSG_NET_PART_DECL(1)
+RSG_NET_PART_DECL(2)
+RSG_NET_PART_DECL(3)
+RSG_NET_PART_DECL(4)
+RSG_NET_PART_DECL(5)
+RSG_NET_PART_DECL(6)
+RSG_NET_PART_DECL(7)
+#undef RSG_NET_PART_DECL
 hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                     hipStream_t stream);
 

@@ -493,30 +493,6 @@ void k_encode_hash_fused(const GfApplyParams p,
 // read with asm ds_read_b64 (the compiler adds no vmcnt(0) for them).  Dead
 // stripes (past n) re-read stripe 0 and store nothing.
 namespace dma {
-__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
-    uint32_t r;
-    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
-    return r;
-}
-
-// 8x8 bit transpose of 8 dwords (bs::transpose) with two shifts and two
-// v_bfi_b32 per masked swap; its own inverse
-__device__ __forceinline__ void swap_bfi(uint32_t& lo, uint32_t& hi, int s, uint32_t mask) {
-    const uint32_t a = lo, b = hi;
-    lo = bfi(mask, a, b << s);
-    hi = bfi(mask, a >> s, b);
-}
-__device__ __forceinline__ void transpose(uint32_t (&w)[8], uint32_t m4, uint32_t m2, uint32_t m1) {
-#pragma unroll
-    for (int d = 0; d < 4; ++d) swap_bfi(w[d], w[d + 4], 4, m4);
-    swap_bfi(w[0], w[2], 2, m2);
-    swap_bfi(w[1], w[3], 2, m2);
-    swap_bfi(w[4], w[6], 2, m2);
-    swap_bfi(w[5], w[7], 2, m2);
-#pragma unroll
-    for (int d = 0; d < 8; d += 2) swap_bfi(w[d], w[d + 1], 1, m1);
-}
-
 template <int K, int M, int NE = EW, int SP = SPW>
 struct Shape {
     static constexpr int SPW = SP, HS = SP / 2;       // stripes per workgroup, per DMA half
@@ -1116,6 +1092,7 @@ const Tuning& tuning() {
         v.dma_nt = num("RSG_DMA_NT", 3, 0, 3);
         v.dma_spw = num("RSG_DMA_SPW", 8, 4, 8) == 4 ? 4 : 8;
         v.get_prio = num("RSG_DMA_PRIO", 2, 0, 3);
+        v.decode_net = flag("RSG_DECODE_NET", true);
         v.test_fail_subbatch = num("RSG_TEST_FAIL_SUBBATCH", -1, 0, 1 << 30);
         return v;
     }();

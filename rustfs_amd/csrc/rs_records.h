@@ -1,0 +1,149 @@
+// rs_records.h — the wave roles the one-pass GET / heal kernels share
+// (rs_decode.hip k_decode_records_dma with run-time-table GF waves,
+// rs_decode_net.hip k_decode_records_net with compile-time XOR-network
+// waves): the LDS-DMA + verify-hash waves that bring every present record
+// into the ring and check its digest (split_and_verify, bitrot.rs:227-247),
+// and the target hashers of the heal (BitrotWriter::write, bitrot.rs:464-510).
+// Internal; included once per translation unit after rs_device.h.
+#pragma once
+
+#include "rs_device.h"
+
+namespace rsg {
+
+// Ring of one workgroup: G stripes, NF present files, 512-byte steps.
+// Present file f of stripe e sits in DMA instruction f*HS + e%HS, half e/HS
+// (stripes e and e + HS share one 1 KiB LDS row pair of pitch IP).
+template <int NF, int G, int TH = 0>
+struct RecRing {
+    static constexpr int SPW = G, HS = G / 2;                     // stripes per workgroup, per DMA half
+    static constexpr int NI = HS * NF;                            // DMA instructions per step
+    static constexpr uint32_t DSLOT = NI * dma::IP;
+    static constexpr int HW = (NI + 7) / 8;                       // DMA/hash waves
+    static constexpr int LAST = NI - 8 * (HW - 1);                // instructions of the last one
+    static constexpr uint32_t TSLOT = SPW * (TH ? TH : 1) * dma::PP;  // one step of target rows
+    static constexpr int TW = (SPW * TH + 15) / 16;               // target-hasher waves
+};
+
+// DMA + verify-hash wave hw of a workgroup whose first stripe is s0: brings
+// its (up to) 8 DMA instructions of every step into the ring D-1 steps ahead
+// and hashes both halves of each straight out of the ring (quad j: instruction
+// 8 hw + (j & 7), half j >> 3); at the end lane 0 of each live quad writes its
+// record's verify flag whole (no memset before the launch).  One barrier per
+// step: B(0) before step 0, B(s+1) after step s.
+template <int NF, int G>
+__device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t wave_prio, uint8_t* ring,
+                                                  uint32_t hw, uint32_t steps, uint64_t s0) {
+    using dma::CH;
+    using dma::D;
+    using dma::IP;
+    using dma::vmcnt_imm;
+    using L = RecRing<NF, G>;
+    constexpr int HS = L::HS;
+    if (wave_prio & kPrioHash) __builtin_amdgcn_s_setprio(2);
+    const uint32_t lane = threadIdx.x & 63u, q = lane & 3u, j = lane >> 2;
+    const uint64_t n = h.n;
+    const uint32_t ring_base = (uint32_t)(uintptr_t)ring;
+    const int ndi = (hw == (uint32_t)(L::HW - 1)) ? L::LAST : 8;  // instructions this wave owns
+    const uint32_t idx = 8 * hw + (j & 7u), half = j >> 3;
+    const bool quad_on = (int)(j & 7u) < ndi;
+    const uint32_t file = quad_on ? idx / HS : 0, stripe_l = (idx % HS) + HS * half;
+    const uint32_t roff = (quad_on ? idx : 0) * IP + half * CH + 8 * q;
+    const bool live = quad_on && s0 + stripe_l < n;
+    HHQuad st;
+    hhq_init(st, h.key, q);
+    // record sources as a wave-uniform base (SGPRs) + a 32-bit per-lane
+    // offset (the upper half's stripe, or the lower one again past n): the
+    // loads take the saddr form, a step costs HS VALU adds
+    uint64_t ubo[HS];
+    uint32_t vlane[HS];
+#pragma unroll
+    for (int i = 0; i < HS; ++i) {
+        const uint64_t lo = s0 + i, hi = lo + HS;
+        ubo[i] = (lo < n ? lo : 0) * h.stripe_stride;
+        vlane[i] = (lane & 31u) * 16u + ((lane >> 5) && hi < n ? (uint32_t)(HS * h.stripe_stride) : 0u);
+    }
+    auto dma_step = [&](uint32_t step) {
+        uint32_t voff[HS];
+#pragma unroll
+        for (int i = 0; i < HS; ++i) voff[i] = vlane[i] + step * CH;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (k >= ndi) break;  // wave-uniform
+            const uint32_t ins = 8 * hw + k;
+            const uint8_t* src = h.base[ins / HS] + ubo[k % HS] + (uint64_t)voff[k % HS];
+            __builtin_amdgcn_global_load_lds(
+                (const void*)src, (__attribute__((address_space(3))) void*)(ring + (step % D) * L::DSLOT + ins * IP), 16,
+                0, 0);
+        }
+    };
+    auto wait_next = [&]() {  // DMA of the next step landed (D - 2 steps younger in flight)
+        if (ndi == 8) __builtin_amdgcn_s_waitcnt(vmcnt_imm((D - 2) * 8));
+        else __builtin_amdgcn_s_waitcnt(vmcnt_imm((D - 2) * L::LAST));
+    };
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d) dma_step(d < (int)steps ? d : steps - 1);
+    wait_next();  // DMA(0) landed
+    lds_barrier();  // B(0)
+#pragma unroll 1
+    for (uint32_t s = 0; s < steps; ++s) {
+        dma_step(s + D - 1 < steps ? s + D - 1 : steps - 1);  // into the slot step s-1 used
+        uint64_t w[16];
+        dma::read16(ring_base + (s % D) * L::DSLOT + roff, w);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) hhq_update(st, w[t]);
+        wait_next();
+        lds_barrier();  // B(s+1)
+    }
+    __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // the clamped tail DMA has landed before the wave ends
+    // verify before use (split_and_verify, bitrot.rs:227-247): lane 0 of each
+    // live quad writes its record's flag whole (no memset before the launch)
+    const uint64_t d = hhq_digest(st, q);
+    bool mis = false;
+    if (live) mis = d != ld64_any(h.base[file] + (s0 + stripe_l) * h.stripe_stride - 32 + 8 * q);
+    const uint64_t bal = __builtin_amdgcn_ballot_w64(mis);
+    if (live && q == 0) h.flag_base[file][s0 + stripe_l] = ((bal >> lane) & 0xFull) ? 0 : 1;
+}
+
+// Target-hasher wave tw of a heal workgroup: quad j hashes target row stream
+// pi = 16 tw + j (row r = pi / SPW of stripe pi % SPW) from the double-
+// buffered LDS row area one step behind the GF waves (step s-1's rows,
+// published by B(s)), and writes the target record's digest header in front
+// of its body at out_base + stripe * out_stripe_stride + out_off[r] - 32.
+template <int G, int TH>
+__device__ __forceinline__ void records_target_hasher(const GfApplyParams& p, const HashParams& h,
+                                                      const uint8_t* trow, uint32_t tw, uint32_t steps,
+                                                      uint64_t s0) {
+    constexpr int SPW = G;
+    constexpr uint32_t TSLOT = RecRing<1, G, TH>::TSLOT;
+    if (p.wave_prio & kPrioHash) __builtin_amdgcn_s_setprio(2);
+    const uint32_t lane = threadIdx.x & 63u, q = lane & 3u;
+    const uint32_t pi = 16 * tw + (lane >> 2);  // r * SPW + stripe
+    const bool on = pi < (uint32_t)(SPW * TH);
+    const uint32_t r = on ? pi / SPW : 0, e = pi % SPW;
+    const bool live = on && s0 + e < h.n;
+    const uint32_t roff = (on ? pi : 0) * dma::PP + 8 * q;
+    HHQuad st;
+    hhq_init(st, h.key, q);
+    lds_barrier();  // B(0)
+#pragma unroll 1
+    for (uint32_t s = 0; s <= steps; ++s) {
+        if (s > 0) {  // target rows of step s-1, published by B(s)
+            uint64_t w[16];
+            dma::read16((uint32_t)(uintptr_t)trow + ((s - 1) & 1) * TSLOT + roff, w);
+#pragma unroll
+            for (int t = 0; t < 16; ++t) hhq_update(st, w[t]);
+        }
+        if (s < steps) lds_barrier();  // B(s+1)
+    }
+    if (live) hhq_finish(st, p.out_base + (s0 + e) * p.out_stripe_stride + p.out_off[r] - 32, q);
+}
+
+// Stripes per workgroup of the one-pass GET/heal kernels for C survivors: 8
+// (one workgroup of 13 waves per CU at RS(8,4)) while the ring of 3 x G/2 x
+// NF KiB-rows fits the LDS, 4 for C = 16 (RS(16,4): up to 19 present files).
+// (Four stripes per workgroup at RS(8,4) — two workgroups of 7 waves per CU —
+// measured no faster, profiles/r02/ab_eng/.)
+constexpr int get_group(int C) { return C > 8 ? 4 : 8; }
+
+}  // namespace rsg

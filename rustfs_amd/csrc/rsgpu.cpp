@@ -1288,7 +1288,7 @@ int launch_get_one_pass(Codec& cd, const std::vector<uint8_t>& present, const st
     }
     (void)t;
     return hip_status(rsg::launch_decode_records_dma(p, h, k, (int)present.size() - k, (int)files.size(), shard_len,
-                                                     n, s));
+                                                     n, coef.data(), s));
 }
 
 // Launch the one-pass heal (k_decode_records_dma with target hashing) for
@@ -1343,7 +1343,7 @@ int launch_heal_one_pass(Codec& cd, const std::vector<uint8_t>& present, const s
     }
     return hip_status(
         rsg::launch_heal_records_dma(p, h, k, (int)present.size() - k, (int)files.size(), (int)targets.size(),
-                                     shard_len, n, s));
+                                     shard_len, n, coef.data(), s));
 }
 
 // GET engine body (ctx->mu held): verify records, copy/rebuild the k data

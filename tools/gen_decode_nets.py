@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""Generate rustfs_amd/csrc/rs84_decode_nets.h: compile-time XOR networks for
+the RS(8,4) one-pass GET / heal kernel (rs_decode_net.hip), one per erasure
+pattern of one or two lost shards.
+
+The one-pass GET/heal (k_decode_records_dma) computes R <= 4 rows — rebuilt
+data or parity, then surplus parity to compare — as GF(2^8) combinations of
+the k = 8 survivors (the first 8 present shards, DecodePlan order), with
+run-time v_perm tables: 3 v_perm + 1.5 XOR per word and coefficient, the
+v_perm at half the XOR issue rate.  For a FIXED pattern the R x 8 matrix is a
+constant, so, as for the encode (gen_xornet.py), the rows become a
+straight-line three-input XOR network over the 64 bit planes of the
+survivors, about half the issue cycles.  This script enumerates the patterns
+the engines see when one or two disks are lost — GET (a data shard among the
+lost: rows = missing data ascending, then the present non-survivor parity),
+heal (targets = the lost shards ascending, then the present non-survivor
+parity) — derives each matrix exactly as rsgpu.cpp does (Codec::plan and
+plan_row: survivors' rows of V * inv(V[0..k)) inverted; data row = inv[i],
+parity row = G[i] * inv), searches a network (gen_xornet.search, best of a
+few seeds), checks it on random planes, and writes the header: the pattern
+table (absent mask, mode, present files, R, stored rows, the coefficient
+rows) and one `net<PID>` specialisation per pattern.  The launcher matches a
+launch's coefficient rows against the table byte for byte, so a pattern not
+listed (or any disagreement) keeps the run-time-table kernel.
+
+Usage: python tools/gen_decode_nets.py [seeds]   (writes the header)
+"""
+import multiprocessing
+import os
+import random
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import gen_xornet as gx  # noqa: E402
+
+K, M = 8, 4
+T = K + M
+
+
+def invert(a):
+    n = len(a)
+    w = [list(r) + [1 if i == j else 0 for j in range(n)] for i, r in enumerate(a)]
+    for c in range(n):
+        p = c
+        while w[p][c] == 0:
+            p += 1
+        w[p], w[c] = w[c], w[p]
+        iv = gx.gpow(w[c][c], 254)
+        w[c] = [gx.gmul(x, iv) for x in w[c]]
+        for r in range(n):
+            if r != c and w[r][c]:
+                f = w[r][c]
+                w[r] = [x ^ gx.gmul(f, y) for x, y in zip(w[r], w[c])]
+    return [r[n:] for r in w]
+
+
+def full_matrix():
+    g = gx.encode_rows(K, M)
+    return [[1 if i == j else 0 for j in range(K)] for i in range(K)] + g
+
+
+def plan(present):
+    """rsgpu.cpp Codec::plan: survivors = first K present; inv of their rows."""
+    mat = full_matrix()
+    surv = [i for i in range(T) if present[i]][:K]
+    inv = invert([mat[s] for s in surv])
+    return mat, surv, inv
+
+
+def plan_row(mat, inv, idx):
+    """rsgpu.cpp plan_row: inv[idx] for data, G[idx] * inv for parity."""
+    if idx < K:
+        return list(inv[idx])
+    row = []
+    for c in range(K):
+        a = 0
+        for i in range(K):
+            a ^= gx.gmul(mat[idx][i], inv[i][c])
+        row.append(a)
+    return row
+
+
+def patterns():
+    """(absent mask, heal, nf, R, n_store, coef rows) for 1 and 2 lost shards."""
+    out, seen = [], set()
+    losses = [(a,) for a in range(T)] + [(a, b) for a in range(T) for b in range(a + 1, T)]
+    for heal in (0, 1):
+        for lost in losses:
+            present = [0 if i in lost else 1 for i in range(T)]
+            files = [i for i in range(T) if present[i]]
+            mat, surv, inv = plan(present)
+            assert surv == files[:K]
+            if heal:
+                store = list(lost)  # every lost shard is a target (launch_heal_one_pass)
+            else:
+                store = [i for i in lost if i < K]  # launch_get_one_pass: missing data
+                if not store:
+                    continue  # no data lost: the GET needs no rebuild
+            rows = [plan_row(mat, inv, i) for i in store] + [plan_row(mat, inv, f) for f in files[K:]]
+            assert len(rows) <= 4
+            key = (heal, len(files), len(rows), len(store), tuple(map(tuple, rows)))
+            if key in seen:
+                continue
+            seen.add(key)
+            mask = sum(1 << i for i in lost)
+            out.append((mask, heal, len(files), len(rows), len(store), rows))
+    return out
+
+
+def plane_rows(rows):
+    return [{c * 8 + j for c in range(K) for j in range(8) if (gx.gmul(rows[r][c], 1 << j) >> i) & 1}
+            for r in range(len(rows)) for i in range(8)]
+
+
+def best_network(args):
+    rows, seeds = args
+    pr = plane_rows(rows)
+    best = None
+    for seed in range(seeds):
+        total, temps, rr = gx.search(pr, seed)
+        if best is None or total < best[0]:
+            best = (total, temps, rr, seed)
+    check(pr, best[1], best[2])
+    return best
+
+
+def check(pr, temps, rr):
+    rng = random.Random(7)
+    for _ in range(8):
+        val = {v: rng.getrandbits(32) for v in range(64)}
+        for v, *t in temps:
+            x = 0
+            for a in t:
+                x ^= val[a]
+            val[v] = x
+        for o in range(len(pr)):
+            want = got = 0
+            for v in pr[o]:
+                want ^= val[v]
+            for v in rr[o]:
+                got ^= val[v]
+            assert got == want, o
+
+
+def emit_net(pid, pat, net):
+    mask, heal, nf, R, nst, rows = pat
+    total, temps, rr, seed = net
+    name = lambda v: f"P[{v}]" if v < 64 else f"t{v}"
+    lost = [i for i in range(T) if mask >> i & 1]
+    out = [f"// pattern {pid}: {'heal' if heal else 'GET'}, lost {lost}, {nf} present, R = {R} "
+           f"({nst} stored), {total} ops (seed {seed})",
+           "template <>",
+           f"__device__ __forceinline__ void net<{pid}>(const uint32_t (&P)[64], uint32_t (&O)[32]) {{"]
+    for v, *t in temps:
+        if len(t) == 3:
+            out.append(f"    const uint32_t t{v} = x3({name(t[0])}, {name(t[1])}, {name(t[2])});")
+        else:
+            out.append(f"    const uint32_t t{v} = {name(t[0])} ^ {name(t[1])};")
+    for o, s in enumerate(rr):
+        terms = [name(v) for v in sorted(s)]
+        if not terms:
+            out.append(f"    O[{o}] = 0u;")
+            continue
+        e = terms[0]
+        k = 1
+        while k + 1 < len(terms):
+            e = f"x3({e}, {terms[k]}, {terms[k + 1]})"
+            k += 2
+        if k < len(terms):
+            e = f"({e} ^ {terms[k]})"
+        out.append(f"    O[{o}] = {e};")
+    out.append("}")
+    return out
+
+
+def main():
+    seeds = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    pats = patterns()
+    with multiprocessing.Pool(min(8, os.cpu_count() or 1)) as pool:
+        nets = pool.map(best_network, [(p[5], seeds) for p in pats])
+    ops = [n[0] for n in nets]
+    hdr = [
+        "// rs84_decode_nets.h — GENERATED by tools/gen_decode_nets.py (do not edit).",
+        "// RS(8,4) one-pass GET / heal rows as compile-time three-input XOR networks,",
+        f"// one per erasure pattern of one or two lost shards: {len(pats)} patterns,",
+        f"// {min(ops)}-{max(ops)} ops each (mean {sum(ops) / len(ops):.0f}).  P[c*8+j] = bit plane j of",
+        "// survivor c (the first 8 present shards), O[r*8+i] = bit plane i of row r",
+        "// (rows [0, n_store) stored, the rest compared with the present",
+        "// non-survivor parity in ascending order).  Included by rs_decode_net.hip",
+        "// inside namespace rsg, after x3().",
+        "#pragma once",
+        "",
+        "namespace decnet {",
+        "",
+        "struct Pattern {",
+        "    uint16_t absent;  // bit i: shard i lost",
+        "    uint8_t heal;     // 1: heal (every lost shard a target), 0: GET",
+        "    uint8_t nf;       // present files",
+        "    uint8_t R;        // rows",
+        "    uint8_t n_store;  // stored rows (the rest compared)",
+        "    uint8_t coef[4][8];",
+        "};",
+        "",
+        f"constexpr int kCount = {len(pats)};",
+        "constexpr Pattern kPatterns[kCount] = {",
+    ]
+    for pid, (mask, heal, nf, R, nst, rows) in enumerate(pats):
+        rr = rows + [[0] * K] * (4 - R)
+        cs = ", ".join("{" + ", ".join(str(x) for x in r) + "}" for r in rr)
+        hdr.append(f"    {{0x{mask:03x}, {heal}, {nf}, {R}, {nst}, {{{cs}}}}},  // {pid}")
+    hdr += ["};", "", "template <int PID>", "__device__ void net(const uint32_t (&P)[64], uint32_t (&O)[32]);", ""]
+    for pid, (pat, net) in enumerate(zip(pats, nets)):
+        hdr += emit_net(pid, pat, net)
+        hdr.append("")
+    hdr.append("}  // namespace decnet")
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "rustfs_amd", "csrc", "rs84_decode_nets.h")
+    with open(path, "w") as f:
+        f.write("\n".join(hdr) + "\n")
+    print(f"wrote {os.path.normpath(path)}: {len(pats)} patterns, {min(ops)}-{max(ops)} ops")
+
+
+if __name__ == "__main__":
+    main()
