@@ -232,6 +232,8 @@ static bool launch_net_if_listed(int heal, int k, int m, int nf, const uint8_t* 
     if (k != 8 || m != 4 || !coef || !tuning().decode_net || p.C != 8) return false;
     const int pid = records_net_pattern(heal, nf, (int)p.R, (int)p.n_store, coef);
     if (pid < 0) return false;
+    GfApplyParams q = p;
+    q.cached_stores = tuning().get_cached ? 1u : 0u;
     const uint64_t blocks = (n_stripes + 7) / 8;
     if (blocks > 0x7fffffffull) return false;
     using Part = bool (*)(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
@@ -239,7 +241,7 @@ static bool launch_net_if_listed(int heal, int k, int m, int nf, const uint8_t* 
                                               launch_records_net_part2, launch_records_net_part3,
                                               launch_records_net_part4, launch_records_net_part5,
                                               launch_records_net_part6, launch_records_net_part7};
-    return parts[pid % RSG_NET_PARTS](pid, blocks, p, h, stream);
+    return parts[pid % RSG_NET_PARTS](pid, blocks, q, h, stream);
 }
 
 static bool dma_records_aligned(const HashParams& h, int nf) {

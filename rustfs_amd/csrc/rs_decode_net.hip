@@ -36,6 +36,15 @@ namespace rsg {
 
 #include "rs84_decode_nets.h"
 
+// 8 output bytes per lane: plain (cached) stores by default — the L2 gathers
+// the walk's 512-byte rows before they reach HBM (RS(8,4), n = 4096, GET with
+// 2 data lost 2.01 -> 1.97 ms, heal neutral; profiles/r03/ab_net/) — or
+// non-temporal (RSG_GET_CACHED=0)
+__device__ __forceinline__ void put8(uint8_t* p, const uint2& v, bool cached) {
+    if (cached) *(uint2*)p = v;
+    else st16_nt_half(p, v);
+}
+
 template <int NF, int TH>
 struct NetShape : RecRing<NF, 8, TH> {
     static constexpr int NG = 2;  // network waves (4-stripe groups)
@@ -61,6 +70,7 @@ __device__ __forceinline__ void net_wave(const GfApplyParams& p, uint64_t n, uin
     const uint32_t m4 = vgpr_const(0x0f0f0f0fu), m2 = vgpr_const(0x33333333u), m1 = vgpr_const(0x55555555u);
     const uint32_t mys[4] = {2 * g, 2 * g + 1, 2 * g + HS, 2 * g + HS + 1};
     const uint32_t cmask = p.copy_mask;
+    const bool cached = p.cached_stores != 0;
     bool live[4];       // wave-uniform: a dead stripe (past n) computes stripe 0's rows and stores nothing
     uint8_t* ob[4];
 #pragma unroll
@@ -99,7 +109,7 @@ __device__ __forceinline__ void net_wave(const GfApplyParams& p, uint64_t n, uin
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const uint2 v = make_uint2(w[2 * j], w[2 * j + 1]);
-                    if (live[j]) st16_nt_half(ob[j] + p.out_off[r] + (uint64_t)s * CH, v);
+                    if (live[j]) put8(ob[j] + p.out_off[r] + (uint64_t)s * CH, v, cached);
                     if constexpr (TH > 0)
                         *(uint2*)(trow + (s & 1) * L::TSLOT + (r * SPW + mys[j]) * PP + lane * 8u) = v;
                 }
@@ -120,7 +130,7 @@ __device__ __forceinline__ void net_wave(const GfApplyParams& p, uint64_t n, uin
                                     *(const uint2*)(row + IP + CH)};
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    if (live[j]) st16_nt_half(ob[j] + p.copy_off[c] + (uint64_t)s * CH, x[j]);
+                    if (live[j]) put8(ob[j] + p.copy_off[c] + (uint64_t)s * CH, x[j], cached);
             }
         }
         lds_barrier();  // B(s+1): done with slot s % D

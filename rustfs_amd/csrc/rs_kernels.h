@@ -40,6 +40,7 @@ struct Tuning {
     int dma_spw = 8;              // RSG_DMA_SPW=4: four stripes per fused DMA workgroup
     int get_prio = 2;             // RSG_DMA_PRIO=<0..3>: wave priorities of the one-pass GET/heal
     bool decode_net = true;       // RSG_DECODE_NET=0: run-time-table GF waves for every one-pass pattern
+    bool get_cached = true;       // RSG_GET_CACHED=0: non-temporal output stores in the network GET/heal kernel
     // fault injection (tests only): RSG_TEST_FAIL_SUBBATCH=<i> makes sub-batch
     // i of every rsg_encode_batch_host_submit fail to enqueue (-1: never)
     int test_fail_subbatch = -1;
@@ -72,6 +73,7 @@ struct GfApplyParams {
     uint32_t copy_mask;
     uint64_t copy_off[kMaxC];
     uint32_t wave_prio;  // DMA kernels: kPrioHash | kPrioGf (set by the launcher)
+    uint32_t cached_stores;  // k_decode_records_net: 1 = plain (cached) output stores instead of non-temporal
 };
 
 constexpr int kMaxHashBases = 32;

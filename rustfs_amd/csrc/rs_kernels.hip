@@ -1093,6 +1093,7 @@ const Tuning& tuning() {
         v.dma_spw = num("RSG_DMA_SPW", 8, 4, 8) == 4 ? 4 : 8;
         v.get_prio = num("RSG_DMA_PRIO", 2, 0, 3);
         v.decode_net = flag("RSG_DECODE_NET", true);
+        v.get_cached = flag("RSG_GET_CACHED", true);
         v.test_fail_subbatch = num("RSG_TEST_FAIL_SUBBATCH", -1, 0, 1 << 30);
         return v;
     }();
