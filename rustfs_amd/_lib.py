@@ -17,7 +17,9 @@ except Exception:  # pragma: no cover - torch is optional for the C ABI itself
     torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librsgpu.so")
+# RSG_LIB_PATH: an experiment build of the same library (tools/ab_*.sh A/B
+# runs); the default is the in-tree build.
+LIB_PATH = os.environ.get("RSG_LIB_PATH") or os.path.join(HERE, "librsgpu.so")
 
 # rsg_status (include/rsgpu.h)
 RSG_OK = 0

@@ -28,6 +28,9 @@
 #include "rs_kernels.h"
 #include "rs_records.h"
 
+#ifndef RSG_NET_ABLATE
+#define RSG_NET_ABLATE 0
+#endif
 #ifndef RSG_NET_PART
 #error "RSG_NET_PART (0 .. RSG_NET_PARTS-1) is set by the Makefile"
 #endif
@@ -93,18 +96,27 @@ __device__ __forceinline__ void net_wave(const GfApplyParams& p, uint64_t n, uin
             const uint2 a0 = *(const uint2*)row, a1 = *(const uint2*)(row + IP);
             const uint2 a2 = *(const uint2*)(row + CH), a3 = *(const uint2*)(row + IP + CH);
             uint32_t w[8] = {a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y};
+#if !RSG_NET_ABLATE
             dma::transpose(w, m4, m2, m1);
+#endif
 #pragma unroll
             for (int j = 0; j < 8; ++j) P[8 * c + j] = w[j];
         }
         uint32_t O[32];
+#if RSG_NET_ABLATE  // experiment builds only (exp/, tools/ab_ablate.sh): no arithmetic, rows = survivors
+#pragma unroll
+        for (int i = 0; i < 32; ++i) O[i] = P[i];
+#else
         decnet::net<PID>(P, O);
+#endif
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             uint32_t w[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) w[i] = O[8 * r + i];
+#if !RSG_NET_ABLATE
             dma::transpose(w, m4, m2, m1);
+#endif
             if (r < NST) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
