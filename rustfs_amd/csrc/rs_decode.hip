@@ -229,7 +229,20 @@ bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len) {
 // keeps the table kernel for A/B runs.
 static bool launch_net_if_listed(int heal, int k, int m, int nf, const uint8_t* coef, uint64_t n_stripes,
                                  const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
-    if (k != 8 || m != 4 || !coef || !tuning().decode_net || p.C != 8) return false;
+    if (m != 4 || !coef || !tuning().decode_net || p.C != (uint32_t)k) return false;
+    if (k == 16) {
+        const int pid = records_net16_pattern(heal, nf, (int)p.R, (int)p.n_store, coef);
+        if (pid < 0) return false;
+        const uint64_t blocks = (n_stripes + 3) / 4;
+        if (blocks > 0x7fffffffull) return false;
+        using Part16 = bool (*)(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+        static const Part16 parts16[RSG_NET_PARTS] = {launch_records_net16_part0, launch_records_net16_part1,
+                                                      launch_records_net16_part2, launch_records_net16_part3,
+                                                      launch_records_net16_part4, launch_records_net16_part5,
+                                                      launch_records_net16_part6, launch_records_net16_part7};
+        return parts16[pid % RSG_NET_PARTS](pid, blocks, p, h, stream);
+    }
+    if (k != 8) return false;
     const int pid = records_net_pattern(heal, nf, (int)p.R, (int)p.n_store, coef);
     if (pid < 0) return false;
     GfApplyParams q = p;
@@ -251,16 +264,25 @@ static bool dma_records_aligned(const HashParams& h, int nf) {
     return h.stripe_stride % 16 == 0 && 5 * h.stripe_stride < (1ull << 32);
 }
 
+bool heal_one_pass_shape(int k, int m, int nf, int targets, uint64_t shard_len) {
+    return heal_dma_supported(k, m, nf, targets, shard_len) ||
+           (k == 16 && m == 4 && tuning().decode_net && one_pass_geometry(k, m, shard_len) && nf >= k &&
+            targets >= 1 && nf + targets <= k + m);
+}
+
+// hipErrorNotSupported: no one-pass kernel for this pattern (RS(16,4) heal
+// not in the network table) — the caller takes the two-pass path.
 hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, int nf, int targets,
                                    uint64_t shard_len, uint64_t n_stripes, const uint8_t* coef, hipStream_t stream) {
     p.wave_prio = dma_prio();
-    if (!heal_dma_supported(k, m, nf, targets, shard_len) || (int)p.C != k || n_stripes == 0 || p.R > 4 ||
+    if (!heal_one_pass_shape(k, m, nf, targets, shard_len) || (int)p.C != k || n_stripes == 0 || p.R > 4 ||
         p.n_store != (uint32_t)targets || p.copy_mask || !dma_records_aligned(h, nf) ||
         p.out_stripe_stride != h.stripe_stride)
         return hipErrorInvalidValue;
     p.units = (uint32_t)(shard_len / dma::CH);
     h.n = n_stripes;
     if (launch_net_if_listed(1, k, m, nf, coef, n_stripes, p, h, stream)) return hipGetLastError();
+    if (!heal_dma_supported(k, m, nf, targets, shard_len)) return hipErrorNotSupported;
     if (!launch_get_any(k, nf, targets, n_stripes, p, h, stream)) return hipErrorInvalidValue;
     return hipGetLastError();
 }

@@ -150,6 +150,24 @@ RSG_NET_PART_DECL(5)
 RSG_NET_PART_DECL(6)
 RSG_NET_PART_DECL(7)
 #undef RSG_NET_PART_DECL
+// RS(16,4) (rs_decode_net16.hip, k_decode_records_net16): the same for R x 16 rows
+int records_net16_pattern(int heal, int nf, int R, int n_store, const uint8_t* coef);
+#define RSG_NET16_PART_DECL(i)                                                                                 \
+    bool launch_records_net16_part##i(int pid, uint64_t blocks, const GfApplyParams& p, const HashParams& h, \
+                                      hipStream_t stream);
+RSG_NET16_PART_DECL(0)
+RSG_NET16_PART_DECL(1)
+RSG_NET16_PART_DECL(2)
+RSG_NET16_PART_DECL(3)
+RSG_NET16_PART_DECL(4)
+RSG_NET16_PART_DECL(5)
+RSG_NET16_PART_DECL(6)
+RSG_NET16_PART_DECL(7)
+#undef RSG_NET16_PART_DECL
+// One-pass heal possible for this shape: the table kernel (k <= 8) or, for
+// RS(16,4), a listed network pattern (decided at launch: RSG_ERR_UNSUPPORTED
+// from the launcher then means "use the two-pass path").
+bool heal_one_pass_shape(int k, int m, int nf, int targets, uint64_t shard_len);
 hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                     hipStream_t stream);
 

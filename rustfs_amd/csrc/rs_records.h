@@ -31,7 +31,7 @@ struct RecRing {
 // 8 hw + (j & 7), half j >> 3); at the end lane 0 of each live quad writes its
 // record's verify flag whole (no memset before the launch).  One barrier per
 // step: B(0) before step 0, B(s+1) after step s.
-template <int NF, int G>
+template <int NF, int G, int XB = 0>
 __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t wave_prio, uint8_t* ring,
                                                   uint32_t hw, uint32_t steps, uint64_t s0) {
     using dma::CH;
@@ -96,6 +96,8 @@ __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t 
         lds_barrier();  // B(s+1)
     }
     __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // the clamped tail DMA has landed before the wave ends
+#pragma unroll
+    for (int b = 0; b < XB; ++b) lds_barrier();  // B(steps+1 ..): roles that trail the DMA by XB more steps
     // verify before use (split_and_verify, bitrot.rs:227-247): lane 0 of each
     // live quad writes its record's flag whole (no memset before the launch)
     const uint64_t d = hhq_digest(st, q);
@@ -107,10 +109,12 @@ __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t 
 
 // Target-hasher wave tw of a heal workgroup: quad j hashes target row stream
 // pi = 16 tw + j (row r = pi / SPW of stripe pi % SPW) from the double-
-// buffered LDS row area one step behind the GF waves (step s-1's rows,
-// published by B(s)), and writes the target record's digest header in front
-// of its body at out_base + stripe * out_stripe_stride + out_off[r] - 32.
-template <int G, int TH>
+// buffered LDS row area LAG steps behind the DMA (step t-LAG's rows,
+// published by B(t); LAG = 1: the GF waves write a step's rows in the
+// interval its data is in the ring), and writes the target record's digest
+// header in front of its body at out_base + stripe * out_stripe_stride +
+// out_off[r] - 32.  steps + LAG barriers.
+template <int G, int TH, int LAG = 1>
 __device__ __forceinline__ void records_target_hasher(const GfApplyParams& p, const HashParams& h,
                                                       const uint8_t* trow, uint32_t tw, uint32_t steps,
                                                       uint64_t s0) {
@@ -127,14 +131,14 @@ __device__ __forceinline__ void records_target_hasher(const GfApplyParams& p, co
     hhq_init(st, h.key, q);
     lds_barrier();  // B(0)
 #pragma unroll 1
-    for (uint32_t s = 0; s <= steps; ++s) {
-        if (s > 0) {  // target rows of step s-1, published by B(s)
+    for (uint32_t t = 0; t < steps + LAG; ++t) {
+        if (t >= (uint32_t)LAG) {  // target rows of step t-LAG, published by B(t)
             uint64_t w[16];
-            dma::read16((uint32_t)(uintptr_t)trow + ((s - 1) & 1) * TSLOT + roff, w);
+            dma::read16((uint32_t)(uintptr_t)trow + ((t - LAG) & 1) * TSLOT + roff, w);
 #pragma unroll
-            for (int t = 0; t < 16; ++t) hhq_update(st, w[t]);
+            for (int i = 0; i < 16; ++i) hhq_update(st, w[i]);
         }
-        if (s < steps) lds_barrier();  // B(s+1)
+        if (t + 1 < steps + LAG) lds_barrier();  // B(t+1)
     }
     if (live) hhq_finish(st, p.out_base + (s0 + e) * p.out_stripe_stride + p.out_off[r] - 32, q);
 }

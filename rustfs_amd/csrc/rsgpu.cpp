@@ -550,6 +550,9 @@ struct rsg_ctx {
         }
         (void)hipEventRecord(tev[tev_used++], s);
     }
+    void tunmark() {  // drop the last mark (a launch that did not happen)
+        if (timing && tev_used) --tev_used;
+    }
     // after the stream has been synchronised
     void tcollect() {
         if (!timing) return;
@@ -1341,9 +1344,9 @@ int launch_heal_one_pass(Codec& cd, const std::vector<uint8_t>& present, const s
         h.base[f] = d_files[files[f]] + 32;
         h.flag_base[f] = d_flags + (size_t)files[f] * n;
     }
-    return hip_status(
-        rsg::launch_heal_records_dma(p, h, k, (int)present.size() - k, (int)files.size(), (int)targets.size(),
-                                     shard_len, n, coef.data(), s));
+    const hipError_t e = rsg::launch_heal_records_dma(p, h, k, (int)present.size() - k, (int)files.size(),
+                                                      (int)targets.size(), shard_len, n, coef.data(), s);
+    return e == hipErrorNotSupported ? RSG_ERR_UNSUPPORTED : hip_status(e);  // unsupported: nothing launched
 }
 
 // GET engine body (ctx->mu held): verify records, copy/rebuild the k data
@@ -1693,7 +1696,7 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
             if (d_targets[i]) tg_idx.push_back(i);
         }
         bool one_pass = get_dma_enabled(ctx, n) &&
-                        rsg::heal_dma_supported(k, m, (int)all_idx.size(), (int)tg_idx.size(), shard_len) &&
+                        rsg::heal_one_pass_shape(k, m, (int)all_idx.size(), (int)tg_idx.size(), shard_len) &&
                         rec % 16 == 0;
         for (int i : all_idx) one_pass = one_pass && (uintptr_t)(d_files[i] + 32) % 16 == 0;
         for (int i : tg_idx) one_pass = one_pass && !d_files[i] && (uintptr_t)(d_targets[i] + 32) % 8 == 0;
@@ -1703,13 +1706,21 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
             // (the kernel writes every source's flags and, with surplus rows,
             // every stripe's verdict whole: no memsets before it)
             ctx->tmark(s);
-            if ((st = launch_heal_one_pass(*cd, present0, all_idx, tg_idx, d_files, d_targets, d_flags, d_ok, k,
-                                           shard_len, n, key, any_verify, s)))
+            st = launch_heal_one_pass(*cd, present0, all_idx, tg_idx, d_files, d_targets, d_flags, d_ok, k, shard_len,
+                                      n, key, any_verify, s);
+            if (st == RSG_ERR_UNSUPPORTED) {  // RS(16,4) pattern without a network: the two-pass path
+                ctx->tunmark();
+                one_pass = false;
+                any_verify = false;
+            } else if (st) {
                 return st;
-            ctx->tmark(s);
-            if (!any_verify && (st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
-            for (uint64_t x = 0; x < n; ++x) h_status[x] = RSG_OK;
-        } else {
+            } else {
+                ctx->tmark(s);
+                if (!any_verify && (st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
+                for (uint64_t x = 0; x < n; ++x) h_status[x] = RSG_OK;
+            }
+        }
+        if (!one_pass) {
             if ((st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
             ctx->tmark(s);
             if ((st = heal_run(0, n, present0))) return st;

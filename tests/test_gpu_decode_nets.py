@@ -1,15 +1,20 @@
-"""Every RS(8,4) erasure pattern of one or two lost shards through the one-pass
-GET / heal kernel with its compile-time XOR network (k_decode_records_net,
-one kernel per pattern; rs84_decode_nets.h): GET (a data shard lost) and heal
-(every lost shard a target), on oracle-built BitrotWriter records, over a
-ragged batch (19 stripes: two full 8-stripe workgroups and a partial one, so
-every 4-stripe network group meets live and dead stripes), bit-exact against
-the oracle's shards and digests; then the same pattern with one surplus
-parity record of one stripe altered and re-hashed must report
+"""Every erasure pattern with a compile-time XOR network through the one-pass
+GET / heal kernels (k_decode_records_net for RS(8,4): every pattern of one or
+two lost shards, one kernel per pattern, rs84_decode_nets.h;
+k_decode_records_net16 for RS(16,4), rs164_decode_nets.h — the patterns are
+read from the generated tables): GET (a data shard lost) and heal (every
+lost shard a target), on oracle-built BitrotWriter records, over a ragged
+batch (RS(8,4): 19 stripes = two full 8-stripe workgroups and a partial
+one, so every 4-stripe network group meets live and dead stripes; RS(16,4):
+11 stripes = two full 4-stripe workgroups and a partial one), bit-exact
+against the oracle's shards and digests; then the same pattern with one
+surplus parity record of one stripe altered and re-hashed must report
 "inconsistent sources" for that stripe only (erasure.rs:935-973,
 heal.rs:179-197).  The CPU test test_decode_nets.py pins the networks
 themselves."""
 import itertools
+import os
+import re
 
 import numpy as np
 import pytest
@@ -19,6 +24,17 @@ pytestmark = pytest.mark.gpu
 K, M, T = 8, 4, 12
 S, N = 1024, 19
 REC = 32 + S
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "rustfs_amd", "csrc")
+
+
+def _listed(header, t):
+    """(heal, lost tuple) of every pattern in a generated network table."""
+    src = open(os.path.join(CSRC, header)).read()
+    out = []
+    for m in re.finditer(r"\{0x([0-9a-f]+), (\d), \d+, \d, \d, \{", src):
+        mask = int(m.group(1), 16)
+        out.append((int(m.group(2)), tuple(i for i in range(t) if mask >> i & 1)))
+    return out
 
 
 @pytest.fixture(scope="module")
@@ -114,3 +130,81 @@ def test_heal_every_pattern(gpu, oracle, records, one_pass, lost):
             got = tgt2[i].cpu().numpy().reshape(N, REC)
             keep = [s for s in range(N) if s != stripe]
             assert np.array_equal(got[keep], recs[i][keep]), f"shard {i}"
+
+
+# ---------------------------------------------------------------- RS(16,4)
+K16, T16, N16 = 16, 20, 11
+LISTED16 = _listed("rs164_decode_nets.h", T16)
+
+
+@pytest.fixture(scope="module")
+def records16(gpu, oracle):
+    import torch
+    rng = np.random.default_rng(164)
+    shards = np.zeros((N16, T16, S), dtype=np.uint8)
+    recs = np.zeros((T16, N16, REC), dtype=np.uint8)
+    for s in range(N16):
+        shards[s, :K16] = rng.integers(0, 256, (K16, S), dtype=np.uint8)
+        oracle.encode(K16, 4, shards[s])
+        for i in range(T16):
+            recs[i, s, :32] = np.frombuffer(oracle.hh256s(shards[s, i].tobytes()), dtype=np.uint8)
+            recs[i, s, 32:] = shards[s, i]
+    files = [torch.from_numpy(recs[i].reshape(-1).copy()).cuda() for i in range(T16)]
+    return shards, recs, files
+
+
+@pytest.mark.parametrize("heal,lost", LISTED16, ids=lambda x: str(x))
+def test_rs16_every_listed_pattern(gpu, oracle, records16, one_pass, heal, lost):
+    import torch
+    from rustfs_amd import Erasure, _lib
+    shards, recs, files = records16
+    e = Erasure(K16, 4, K16 * S)
+    present = [i for i in range(T16) if i not in lost]
+    sur = present[K16:]
+    if not heal:
+        want = torch.from_numpy(shards[:, :K16].reshape(N16, K16 * S).copy()).cuda()
+        f = [None if i in lost else files[i] for i in range(T16)]
+        out, status = e.decode_records_batch(f, S, N16)
+        assert status == [0] * N16 and torch.equal(out, want)
+        if sur:
+            stripe = sum(lost) % N16
+            f2 = list(f)
+            f2[sur[-1]] = _rehashed(torch, oracle, files[sur[-1]], stripe, 3 * sum(lost) % S)
+            out, status = e.decode_records_batch(f2, S, N16)
+            assert [i for i, x in enumerate(status) if x] == [stripe]
+            assert status[stripe] == _lib.RSG_ERR_INCONSISTENT_SOURCES
+            ok = torch.ones(N16, dtype=torch.bool, device="cuda")
+            ok[stripe] = False
+            assert torch.equal(out[ok], want[ok])
+        return
+    src = [None if i in lost else files[i] for i in range(T16)]
+    tgt = [torch.zeros(N16 * REC, dtype=torch.uint8, device="cuda") if i in lost else None for i in range(T16)]
+    assert e.heal_records_batch(src, tgt, S, N16) == [0] * N16
+    for i in lost:
+        assert np.array_equal(tgt[i].cpu().numpy().reshape(N16, REC), recs[i]), f"shard {i}"
+    if sur:
+        stripe = (5 * sum(lost) + 1) % N16
+        src2 = list(src)
+        src2[sur[0]] = _rehashed(torch, oracle, files[sur[0]], stripe, 7 * sum(lost) % S)
+        tgt2 = [torch.zeros(N16 * REC, dtype=torch.uint8, device="cuda") if i in lost else None for i in range(T16)]
+        status = e.heal_records_batch(src2, tgt2, S, N16)
+        assert [i for i, x in enumerate(status) if x] == [stripe]
+        assert status[stripe] == _lib.RSG_ERR_INCONSISTENT_SOURCES
+        keep = [s for s in range(N16) if s != stripe]
+        for i in lost:
+            assert np.array_equal(tgt2[i].cpu().numpy().reshape(N16, REC)[keep], recs[i][keep]), f"shard {i}"
+
+
+def test_rs16_heal_unlisted_pattern_falls_back(gpu, oracle, records16, one_pass):
+    """A heal the network table does not list (three lost shards) takes the
+    two-pass path even with the one-pass engine forced: still bit-exact."""
+    import torch
+    from rustfs_amd import Erasure
+    shards, recs, files = records16
+    e = Erasure(K16, 4, K16 * S)
+    lost = (2, 9, 17)
+    src = [None if i in lost else files[i] for i in range(T16)]
+    tgt = [torch.zeros(N16 * REC, dtype=torch.uint8, device="cuda") if i in lost else None for i in range(T16)]
+    assert e.heal_records_batch(src, tgt, S, N16) == [0] * N16
+    for i in lost:
+        assert np.array_equal(tgt[i].cpu().numpy().reshape(N16, REC), recs[i]), f"shard {i}"

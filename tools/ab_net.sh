@@ -7,7 +7,7 @@ OUT=gpurun_out/$TAG; mkdir -p $OUT
 i=0
 for envs in "$@"; do
   i=$((i+1))
-  env $envs timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-config-extras --steps 5 > $OUT/ab$i.json 2> $OUT/ab$i.err || exit $?
+  env $envs timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-config-extras --steps 5 $BENCH_ARGS > $OUT/ab$i.json 2> $OUT/ab$i.err || exit $?
   python - $OUT/ab$i.json "$envs" <<'PY'
 import json,sys
 d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); g=d['extras']['engines']

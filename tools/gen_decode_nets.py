@@ -23,7 +23,13 @@ rows) and one `net<PID>` specialisation per pattern.  The launcher matches a
 launch's coefficient rows against the table byte for byte, so a pattern not
 listed (or any disagreement) keeps the run-time-table kernel.
 
-Usage: python tools/gen_decode_nets.py [seeds]   (writes the header)
+RS(16,4) (`--k 16`): the 16 survivors' 128 planes do not fit one wave's
+registers beside the rows, so each pattern gets TWO networks, one over
+survivors 0-7 and one over survivors 8-15, each producing all R rows; the
+kernel XORs the two halves (rs_decode_net16.hip) — header rs164_decode_nets.h.
+
+Usage: python tools/gen_decode_nets.py [seeds] [--k 16] [--only heal:1,16 get:0,3 ...]
+(writes the header)
 """
 import multiprocessing
 import os
@@ -35,6 +41,11 @@ import gen_xornet as gx  # noqa: E402
 
 K, M = 8, 4
 T = K + M
+
+
+def set_geometry(k, m):
+    global K, M, T
+    K, M, T = k, m, k + m
 
 
 def invert(a):
@@ -107,14 +118,16 @@ def patterns():
     return out
 
 
-def plane_rows(rows):
-    return [{c * 8 + j for c in range(K) for j in range(8) if (gx.gmul(rows[r][c], 1 << j) >> i) & 1}
+def plane_rows(rows, c0=0, cn=None):
+    """Output plane r*8+i over input planes (c-c0)*8+j, survivors c in [c0, c0+cn)."""
+    cn = K if cn is None else cn
+    return [{(c - c0) * 8 + j for c in range(c0, c0 + cn) for j in range(8) if (gx.gmul(rows[r][c], 1 << j) >> i) & 1}
             for r in range(len(rows)) for i in range(8)]
 
 
 def best_network(args):
-    rows, seeds = args
-    pr = plane_rows(rows)
+    rows, seeds, c0, cn = args
+    pr = plane_rows(rows, c0, cn)
     best = None
     for seed in range(seeds):
         total, temps, rr = gx.search(pr, seed)
@@ -142,15 +155,15 @@ def check(pr, temps, rr):
             assert got == want, o
 
 
-def emit_net(pid, pat, net):
+def emit_net(pid, pat, net, fn="net", what=""):
     mask, heal, nf, R, nst, rows = pat
     total, temps, rr, seed = net
     name = lambda v: f"P[{v}]" if v < 64 else f"t{v}"
     lost = [i for i in range(T) if mask >> i & 1]
     out = [f"// pattern {pid}: {'heal' if heal else 'GET'}, lost {lost}, {nf} present, R = {R} "
-           f"({nst} stored), {total} ops (seed {seed})",
+           f"({nst} stored){what}, {total} ops (seed {seed})",
            "template <>",
-           f"__device__ __forceinline__ void net<{pid}>(const uint32_t (&P)[64], uint32_t (&O)[32]) {{"]
+           f"__device__ __forceinline__ void {fn}<{pid}>(const uint32_t (&P)[64], uint32_t (&O)[32]) {{"]
     for v, *t in temps:
         if len(t) == 3:
             out.append(f"    const uint32_t t{v} = x3({name(t[0])}, {name(t[1])}, {name(t[2])});")
@@ -174,31 +187,49 @@ def emit_net(pid, pat, net):
 
 
 def main():
-    seeds = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    args = sys.argv[1:]
+    k = 8
+    if "--k" in args:
+        i = args.index("--k")
+        k = int(args[i + 1])
+        del args[i:i + 2]
+    only = None
+    if "--only" in args:
+        i = args.index("--only")
+        only = set(args[i + 1:])
+        del args[i:]
+    seeds = int(args[0]) if args else 4
+    set_geometry(k, 4)
     pats = patterns()
+    if only:  # prototype builds: e.g. heal:1,16 get:0,3
+        pats = [p for p in pats if f"{'heal' if p[1] else 'get'}:{','.join(str(i) for i in range(T) if p[0] >> i & 1)}" in only]
+    halves = [(0, 8)] if K == 8 else [(0, 8), (8, 8)]
+    tasks = [(p[5], seeds, c0, cn) for c0, cn in halves for p in pats]
     with multiprocessing.Pool(min(8, os.cpu_count() or 1)) as pool:
-        nets = pool.map(best_network, [(p[5], seeds) for p in pats])
-    ops = [n[0] for n in nets]
+        res = pool.map(best_network, tasks)
+    nets = [res[h * len(pats):(h + 1) * len(pats)] for h in range(len(halves))]
+    ops = [sum(n[i][0] for n in nets) for i in range(len(pats))]
+    name = "rs84_decode_nets.h" if K == 8 else f"rs{K}{M}_decode_nets.h"
     hdr = [
-        "// rs84_decode_nets.h — GENERATED by tools/gen_decode_nets.py (do not edit).",
-        "// RS(8,4) one-pass GET / heal rows as compile-time three-input XOR networks,",
+        f"// {name} — GENERATED by tools/gen_decode_nets.py (do not edit).",
+        f"// RS({K},{M}) one-pass GET / heal rows as compile-time three-input XOR networks,",
         f"// one per erasure pattern of one or two lost shards: {len(pats)} patterns,",
         f"// {min(ops)}-{max(ops)} ops each (mean {sum(ops) / len(ops):.0f}).  P[c*8+j] = bit plane j of",
-        "// survivor c (the first 8 present shards), O[r*8+i] = bit plane i of row r",
+        f"// survivor c (the first {K} present shards{'' if K == 8 else ', in two halves of 8'}), O[r*8+i] = bit plane i of row r",
         "// (rows [0, n_store) stored, the rest compared with the present",
         "// non-survivor parity in ascending order).  Included by rs_decode_net.hip",
         "// inside namespace rsg, after x3().",
         "#pragma once",
         "",
-        "namespace decnet {",
+        f"namespace decnet{'' if K == 8 else K} {{",
         "",
         "struct Pattern {",
-        "    uint16_t absent;  // bit i: shard i lost",
+        "    uint16_t absent;  // bit i: shard i lost" if T <= 16 else "    uint32_t absent;  // bit i: shard i lost",
         "    uint8_t heal;     // 1: heal (every lost shard a target), 0: GET",
         "    uint8_t nf;       // present files",
         "    uint8_t R;        // rows",
         "    uint8_t n_store;  // stored rows (the rest compared)",
-        "    uint8_t coef[4][8];",
+        f"    uint8_t coef[4][{K}];",
         "};",
         "",
         f"constexpr int kCount = {len(pats)};",
@@ -208,12 +239,22 @@ def main():
         rr = rows + [[0] * K] * (4 - R)
         cs = ", ".join("{" + ", ".join(str(x) for x in r) + "}" for r in rr)
         hdr.append(f"    {{0x{mask:03x}, {heal}, {nf}, {R}, {nst}, {{{cs}}}}},  // {pid}")
-    hdr += ["};", "", "template <int PID>", "__device__ void net(const uint32_t (&P)[64], uint32_t (&O)[32]);", ""]
-    for pid, (pat, net) in enumerate(zip(pats, nets)):
-        hdr += emit_net(pid, pat, net)
-        hdr.append("")
-    hdr.append("}  // namespace decnet")
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "rustfs_amd", "csrc", "rs84_decode_nets.h")
+    hdr += ["};", ""]
+    if K == 8:
+        hdr += ["template <int PID>", "__device__ void net(const uint32_t (&P)[64], uint32_t (&O)[32]);", ""]
+        for pid, pat in enumerate(pats):
+            hdr += emit_net(pid, pat, nets[0][pid])
+            hdr.append("")
+    else:
+        hdr += ["// net_lo: all rows over survivors 0-7 (planes P[0..64)); net_hi: over survivors 8-15",
+                "template <int PID>", "__device__ void net_lo(const uint32_t (&P)[64], uint32_t (&O)[32]);",
+                "template <int PID>", "__device__ void net_hi(const uint32_t (&P)[64], uint32_t (&O)[32]);", ""]
+        for pid, pat in enumerate(pats):
+            hdr += emit_net(pid, pat, nets[0][pid], "net_lo", ", survivors 0-7")
+            hdr += emit_net(pid, pat, nets[1][pid], "net_hi", ", survivors 8-15")
+            hdr.append("")
+    hdr.append(f"}}  // namespace decnet{'' if K == 8 else K}")
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "rustfs_amd", "csrc", name)
     with open(path, "w") as f:
         f.write("\n".join(hdr) + "\n")
     print(f"wrote {os.path.normpath(path)}: {len(pats)} patterns, {min(ops)}-{max(ops)} ops")
