@@ -41,8 +41,6 @@ struct Tuning {
     int get_prio = 2;             // RSG_DMA_PRIO=<0..3>: wave priorities of the one-pass GET/heal
     bool decode_net = true;       // RSG_DECODE_NET=0: run-time-table GF waves for every one-pass pattern
     bool get_cached = true;       // RSG_GET_CACHED=0: non-temporal output stores in the network GET/heal kernel
-    int xcd_map = 0;              // RSG_XCD_MAP=1: each XCD sweeps a contiguous 1/8 of the blocks; 2: each XCD
-                                  // whole stripes (stripe 8i+x on XCD x) — GF sweep kernels, A/B
     // fault injection (tests only): RSG_TEST_FAIL_SUBBATCH=<i> makes sub-batch
     // i of every rsg_encode_batch_host_submit fail to enqueue (-1: never)
     int test_fail_subbatch = -1;
@@ -76,7 +74,6 @@ struct GfApplyParams {
     uint64_t copy_off[kMaxC];
     uint32_t wave_prio;  // DMA kernels: kPrioHash | kPrioGf (set by the launcher)
     uint32_t cached_stores;  // k_decode_records_net: 1 = plain (cached) output stores instead of non-temporal
-    uint32_t xcd_map;        // k_gf_apply_vec/loop block order (Tuning::xcd_map; set by the launcher)
 };
 
 constexpr int kMaxHashBases = 32;

@@ -32,35 +32,13 @@ namespace rsg {
 
 #include "rs84_xornet.h"  // generated (tools/gen_xornet.py); uses x3
 
-// Block b's (stripe, chunk).  Blocks are dealt round-robin over the 8 XCDs
-// (MI355X_MICROARCH.md, workgroup dispatch), so b % 8 names the XCD group:
-// xcd_map 0 keeps the plain order (consecutive blocks = one stripe's
-// columns, spread over all XCDs); 1 gives each XCD group a contiguous 1/8 of
-// the blocks; 2 gives it whole stripes (stripe 8i + x to group x), so the 8
-// groups sweep 8 adjacent stripes at once (the launcher uses 1 and 2 only
-// when the grid divides evenly).
-__device__ __forceinline__ void block_coords(const GfApplyParams& p, uint32_t& stripe, uint32_t& chunk) {
-    uint32_t b = blockIdx.x;
-    const uint32_t cps = p.chunks_per_stripe;
-    if (p.xcd_map == 1) {
-        b = (b & 7u) * (gridDim.x >> 3) + (b >> 3);
-    } else if (p.xcd_map == 2) {
-        const uint32_t j = b >> 3, sl = j / cps;
-        stripe = sl * 8u + (b & 7u);
-        chunk = j - sl * cps;
-        return;
-    }
-    stripe = b / cps;
-    chunk = b - stripe * cps;
-}
-
 // PRE: the launch has XOR / COMPARE rows, whose read-back operands are loaded
 // with the inputs, or copy-through inputs (a separate instantiation: the
 // plain STORE encode and reconstruct kernels keep their register budget).
 template <int C, int R, int B, bool PRE>
 __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(2))) void k_gf_apply_vec(const GfApplyParams p) {
-    uint32_t stripe, chunk;
-    block_coords(p, stripe, chunk);
+    const uint32_t stripe = blockIdx.x / p.chunks_per_stripe;
+    const uint32_t chunk = blockIdx.x - stripe * p.chunks_per_stripe;
     const uint8_t* sbase = p.base + (uint64_t)stripe * p.stripe_stride;
     uint8_t* obase = p.out_base + (uint64_t)stripe * p.out_stripe_stride;
     const uint32_t u = chunk * (uint32_t)B + threadIdx.x;
@@ -100,8 +78,8 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(2))) void k_g
 template <int R, int B, bool PRE>
 __global__ __launch_bounds__(B) void k_gf_apply_loop(const GfApplyParams p) {
     constexpr int G = 8;
-    uint32_t stripe, chunk;
-    block_coords(p, stripe, chunk);
+    const uint32_t stripe = blockIdx.x / p.chunks_per_stripe;
+    const uint32_t chunk = blockIdx.x - stripe * p.chunks_per_stripe;
     const uint8_t* sbase = p.base + (uint64_t)stripe * p.stripe_stride;
     uint8_t* obase = p.out_base + (uint64_t)stripe * p.out_stripe_stride;
     const uint32_t u = chunk * (uint32_t)B + threadIdx.x;
@@ -1116,7 +1094,6 @@ const Tuning& tuning() {
         v.get_prio = num("RSG_DMA_PRIO", 2, 0, 3);
         v.decode_net = flag("RSG_DECODE_NET", true);
         v.get_cached = flag("RSG_GET_CACHED", true);
-        v.xcd_map = num("RSG_XCD_MAP", 0, 0, 2);
         v.test_fail_subbatch = num("RSG_TEST_FAIL_SUBBATCH", -1, 0, 1 << 30);
         return v;
     }();
@@ -1200,13 +1177,6 @@ static GfKernel pick_byte(int R) {
     return nullptr;
 }
 
-static uint32_t xcd_map_for(uint64_t blocks, uint64_t n_stripes) {
-    const int m = tuning().xcd_map;
-    if (m == 1 && blocks % 8 == 0) return 1;
-    if (m == 2 && n_stripes % 8 == 0) return 2;
-    return 0;
-}
-
 hipError_t launch_gf_apply_vec(GfApplyParams p, uint64_t n_stripes, hipStream_t stream) {
     const bool pre = p.mode != GF_MODE_STORE || p.copy_mask != 0;
     GfKernel k = pick_vec((int)p.C, (int)p.R, pre);
@@ -1215,7 +1185,6 @@ hipError_t launch_gf_apply_vec(GfApplyParams p, uint64_t n_stripes, hipStream_t 
     p.chunks_per_stripe = (p.units + B - 1) / B;
     const uint64_t blocks = (uint64_t)p.chunks_per_stripe * n_stripes;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    p.xcd_map = xcd_map_for(blocks, n_stripes);
     const int occ = vec_occupancy((int)p.C, (int)p.R, pre);
     const size_t lds = occ ? (size_t)(160 * 1024) / (size_t)(4 * occ * (B / 64)) / 16 * 16 : 0;
     hipLaunchKernelGGL(k, dim3((uint32_t)blocks), dim3(B), lds, stream, p);
