@@ -3,7 +3,7 @@
 // (k_decode_records_net<PID>; the networks in the generated
 // rs84_decode_nets.h, tools/gen_decode_nets.py).  Compiled RSG_NET_PARTS
 // times (Makefile), part RSG_NET_PART instantiating the patterns with
-// PID % RSG_NET_PARTS == RSG_NET_PART, so the ~150 kernels build in parallel.
+// PID % RSG_NET_PARTS == RSG_NET_PART, so the 146 kernels build in parallel.
 //
 // Same workgroup as k_decode_records_dma (rs_decode.hip): 8 stripes, NF
 // present record files DMA'd into a 3-slot LDS ring per 512-byte step,
@@ -14,7 +14,7 @@
 // one per 4-stripe group (stripes 2g, 2g+1, 2g+4, 2g+5: 8 bytes of each per
 // lane, as the fused encoder's k_encode_hash_dma groups): each step the wave
 // bit-transposes the 8 survivor rows into 64 planes, runs the pattern's
-// network (all R rows at once: ~250-300 three-input XORs), transposes the
+// network (all R rows at once: 173-244 three-input XORs), transposes the
 // rows back, stores the rebuilt rows (and heal's LDS row copies), compares
 // the surplus parity rows with the ring and copies GET's present data through.
 #include <hip/hip_runtime.h>
