@@ -208,3 +208,53 @@ def test_rs16_heal_unlisted_pattern_falls_back(gpu, oracle, records16, one_pass)
     assert e.heal_records_batch(src, tgt, S, N16) == [0] * N16
     for i in lost:
         assert np.array_equal(tgt[i].cpu().numpy().reshape(N16, REC), recs[i]), f"shard {i}"
+
+
+_TABLE_SNIPPET = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, {root!r})
+from rustfs_amd import Erasure, _lib
+from oracle import oracle as O
+L = _lib.load()
+_lib.check(L.rsg_set_record_engine(_lib.context(0).handle, _lib.RSG_RECORD_ENGINE_ONE_PASS))
+S = 1024
+REC = 32 + S
+for k, n, gets, heals in ((8, 19, [(0, 3), (2, 9), (5,)], [(1, 8), (0, 11), (4,)]), (16, 11, [(0, 3)], [(1, 16)])):
+    t = k + 4
+    rng = np.random.default_rng(k)
+    shards = np.zeros((n, t, S), dtype=np.uint8)
+    recs = np.zeros((t, n, REC), dtype=np.uint8)
+    for s in range(n):
+        shards[s, :k] = rng.integers(0, 256, (k, S), dtype=np.uint8)
+        O.encode(k, 4, shards[s])
+        for i in range(t):
+            recs[i, s, :32] = np.frombuffer(O.hh256s(shards[s, i].tobytes()), dtype=np.uint8)
+            recs[i, s, 32:] = shards[s, i]
+    files = [torch.from_numpy(recs[i].reshape(-1).copy()).cuda() for i in range(t)]
+    e = Erasure(k, 4, k * S)
+    want = torch.from_numpy(shards[:, :k].reshape(n, k * S).copy()).cuda()
+    for lost in gets:
+        out, status = e.decode_records_batch([None if i in lost else files[i] for i in range(t)], S, n)
+        assert status == [0] * n and torch.equal(out, want), (k, lost)
+    for lost in heals:
+        tgt = [torch.zeros(n * REC, dtype=torch.uint8, device="cuda") if i in lost else None for i in range(t)]
+        assert e.heal_records_batch([None if i in lost else files[i] for i in range(t)], tgt, S, n) == [0] * n
+        for i in lost:
+            assert np.array_equal(tgt[i].cpu().numpy().reshape(n, REC), recs[i]), (k, lost, i)
+print("ok")
+"""
+
+
+@pytest.mark.parametrize("env", [{"RSG_DECODE_NET": "0"}, {"RSG_GET_CACHED": "0"}])
+def test_network_knobs_in_own_process(gpu, oracle, env):
+    """The A/B knobs of the network GET/heal path (read once per process, so
+    each in its own process): RSG_DECODE_NET=0 sends listed RS(8,4) patterns
+    to the run-time-table one-pass kernel and RS(16,4) heal to the two-pass
+    path; RSG_GET_CACHED=0 makes the network kernels' stores non-temporal.
+    Bit-exact against the oracle either way."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _TABLE_SNIPPET.format(root=root)], env={**os.environ, **env},
+                       capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (env, r.stdout[-500:], r.stderr[-2000:])
