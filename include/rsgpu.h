@@ -91,8 +91,9 @@ int rsg_create(int device, rsg_ctx **out);
 void rsg_destroy(rsg_ctx *ctx);
 
 /* Measurement hook (no reference counterpart; bench.py): with timing on, the
- * record engines (rsg_decode_records_dev, rsg_heal_records_dev) record HIP
- * events around their kernel launches on the call's stream;
+ * record engines (rsg_decode_records_dev, rsg_heal_records_dev,
+ * rsg_bitrot_verify_dev) record HIP events around their kernel launches on
+ * the call's stream;
  * rsg_last_kernel_ms returns the summed kernel time of the last such call
  * (-1 if none was timed).  Off by default. */
 int rsg_set_kernel_timing(rsg_ctx *ctx, int on);

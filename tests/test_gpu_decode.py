@@ -175,7 +175,8 @@ def test_decode_records_lost_disk_many_workgroups(gpu, oracle, k, m, lost):
 def test_kernel_timing_hook(gpu, oracle, engine_path):
     """rsg_set_kernel_timing / rsg_last_kernel_ms (bench.py's measurement
     hook): off by default (-1), a positive kernel time after a timed GET with
-    a lost disk and after an all-present GET, unchanged results."""
+    a lost disk, after an all-present GET and after a whole-file
+    bitrot_verify, unchanged results."""
     import ctypes
     import torch
     from rustfs_amd import _lib
@@ -196,5 +197,11 @@ def test_kernel_timing_hook(gpu, oracle, engine_path):
             assert status == [0] * n and torch.equal(out, want)
             _lib.check(L.rsg_last_kernel_ms(ctx, ctypes.byref(v)))
             assert v.value > 0, lost
+        # whole-file bitrot_verify is timed the same way
+        from rustfs_amd.bitrot import HashAlgorithm, bitrot_verify_batch
+        rec = 32 + S
+        assert bitrot_verify_batch(files, n * rec, n * S, HashAlgorithm.HighwayHash256S, S) == [0] * (k + m)
+        _lib.check(L.rsg_last_kernel_ms(ctx, ctypes.byref(v)))
+        assert v.value > 0
     finally:
         _lib.check(L.rsg_set_kernel_timing(ctx, 0))
