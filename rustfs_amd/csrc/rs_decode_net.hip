@@ -48,6 +48,22 @@ __device__ __forceinline__ void put8(uint8_t* p, const uint2& v, bool cached) {
     else st16_nt_half(p, v);
 }
 
+// LDS rows through 32-bit address-space-3 pointers (the low 32 bits of a
+// generic LDS address are its LDS offset, as dma::read16 relies on).
+typedef __attribute__((address_space(3))) const uint64_t lds_u2;
+__device__ __forceinline__ const lds_u2* lds_at(const uint8_t* p) {
+    return (const lds_u2*)(uintptr_t)(uint32_t)(uintptr_t)p;
+}
+__device__ __forceinline__ uint2 u2_of(uint64_t v) { return make_uint2((uint32_t)v, (uint32_t)(v >> 32)); }
+// one 8-byte lane column of the group's 4 stripes, row at byte offset off:
+// stripes at +0, +IP, +CH, +IP+CH
+__device__ __forceinline__ void row4(const lds_u2* slot, uint32_t off, uint2 (&x)[4]) {
+    x[0] = u2_of(slot[off / 8]);
+    x[1] = u2_of(slot[(off + dma::IP) / 8]);
+    x[2] = u2_of(slot[(off + dma::CH) / 8]);
+    x[3] = u2_of(slot[(off + dma::IP + dma::CH) / 8]);
+}
+
 template <int NF, int TH>
 struct NetShape : RecRing<NF, 8, TH> {
     static constexpr int NG = 2;  // network waves (4-stripe groups)
@@ -88,14 +104,16 @@ __device__ __forceinline__ void net_wave(const GfApplyParams& p, uint64_t n, uin
     lds_barrier();  // B(0)
 #pragma unroll 1
     for (uint32_t s = 0; s < steps; ++s) {
-        const uint8_t* slot = ring + (s % D) * L::DSLOT + goff;
+        // the step's ring slot as a 32-bit LDS address: the row reads fold
+        // their constant offsets (ds_read2_b64 pairs) instead of one VALU
+        // add per read through a generic pointer
+        const lds_u2* slot = lds_at(ring + (s % D) * L::DSLOT + goff);
         uint32_t P[64];
 #pragma unroll
         for (int c = 0; c < C; ++c) {
-            const uint8_t* row = slot + c * HS * IP;
-            const uint2 a0 = *(const uint2*)row, a1 = *(const uint2*)(row + IP);
-            const uint2 a2 = *(const uint2*)(row + CH), a3 = *(const uint2*)(row + IP + CH);
-            uint32_t w[8] = {a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y};
+            uint2 a[4];
+            row4(slot, c * HS * IP, a);
+            uint32_t w[8] = {a[0].x, a[0].y, a[1].x, a[1].y, a[2].x, a[2].y, a[3].x, a[3].y};
 #if !RSG_NET_ABLATE
             dma::transpose(w, m4, m2, m1);
 #endif
@@ -126,9 +144,8 @@ __device__ __forceinline__ void net_wave(const GfApplyParams& p, uint64_t n, uin
                         *(uint2*)(trow + (s & 1) * L::TSLOT + (r * SPW + mys[j]) * PP + lane * 8u) = v;
                 }
             } else {
-                const uint8_t* row = slot + (C + (r - NST)) * HS * IP;
-                const uint2 o[4] = {*(const uint2*)row, *(const uint2*)(row + IP), *(const uint2*)(row + CH),
-                                    *(const uint2*)(row + IP + CH)};
+                uint2 o[4];
+                row4(slot, (C + (r - NST)) * HS * IP, o);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) bad[j] |= ((o[j].x ^ w[2 * j]) | (o[j].y ^ w[2 * j + 1])) != 0u;
             }
@@ -137,9 +154,8 @@ __device__ __forceinline__ void net_wave(const GfApplyParams& p, uint64_t n, uin
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 if (!((cmask >> c) & 1u)) continue;  // wave-uniform
-                const uint8_t* row = slot + c * HS * IP;
-                const uint2 x[4] = {*(const uint2*)row, *(const uint2*)(row + IP), *(const uint2*)(row + CH),
-                                    *(const uint2*)(row + IP + CH)};
+                uint2 x[4];
+                row4(slot, c * HS * IP, x);
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     if (live[j]) put8(ob[j] + p.copy_off[c] + (uint64_t)s * CH, x[j], cached);
