@@ -100,7 +100,7 @@ __device__ __forceinline__ void net_wave(const GfApplyParams& p, uint64_t n, uin
     // this group's 8-byte lane column of a ring row (file f: + f * HS * IP);
     // the 4 stripes sit at +0, +IP, +CH, +IP+CH
     const uint32_t goff = 2 * g * IP + lane * 8u;
-    bool bad[4] = {false, false, false, false};  // this lane saw a surplus-parity mismatch
+    uint32_t diff[4] = {0u, 0u, 0u, 0u};  // OR of this lane's surplus-parity differences
     lds_barrier();  // B(0)
 #pragma unroll 1
     for (uint32_t s = 0; s < steps; ++s) {
@@ -147,7 +147,7 @@ __device__ __forceinline__ void net_wave(const GfApplyParams& p, uint64_t n, uin
                 uint2 o[4];
                 row4(slot, (C + (r - NST)) * HS * IP, o);
 #pragma unroll
-                for (int j = 0; j < 4; ++j) bad[j] |= ((o[j].x ^ w[2 * j]) | (o[j].y ^ w[2 * j + 1])) != 0u;
+                for (int j = 0; j < 4; ++j) diff[j] = or_diff(or_diff(diff[j], o[j].x, w[2 * j]), o[j].y, w[2 * j + 1]);
             }
         }
         if (!TH && cmask) {  // GET: the present data survivors copied through
@@ -167,7 +167,7 @@ __device__ __forceinline__ void net_wave(const GfApplyParams& p, uint64_t n, uin
     if constexpr (NST < R) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const bool any_bad = __builtin_amdgcn_ballot_w64(bad[j]) != 0;
+            const bool any_bad = __builtin_amdgcn_ballot_w64(diff[j] != 0u) != 0;
             if (live[j] && lane == 0) p.ok_flags[s0 + mys[j]] = any_bad ? 0 : 1;
         }
     }

@@ -78,7 +78,7 @@ __device__ __forceinline__ void net16_wave(const GfApplyParams& p, uint64_t n, u
         x[2] = *(const uint2*)(row + CH);
         x[3] = *(const uint2*)(row + IP + CH);
     };
-    bool bad[4] = {false, false, false, false};  // A: this lane saw a surplus-parity mismatch
+    uint32_t diff[4] = {0u, 0u, 0u, 0u};         // A: OR of this lane's surplus-parity differences
     uint32_t O[32];                              // A: step t-1's rows over survivors 0-7, held across B(t)
     uint2 cmp[NCMP ? NCMP : 1][4];               // A: step t-1's surplus rows, held across B(t)
     // step t: this wave's 8 survivors -> planes -> its half of every row;
@@ -139,7 +139,7 @@ __device__ __forceinline__ void net16_wave(const GfApplyParams& p, uint64_t n, u
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const uint2 o = cmp[r - NST][j];
-                    bad[j] |= ((o.x ^ w[2 * j]) | (o.y ^ w[2 * j + 1])) != 0u;
+                    diff[j] = or_diff(or_diff(diff[j], o.x, w[2 * j]), o.y, w[2 * j + 1]);
                 }
             }
         }
@@ -167,7 +167,7 @@ __device__ __forceinline__ void net16_wave(const GfApplyParams& p, uint64_t n, u
     if constexpr (A && NCMP > 0) {  // each stripe's surplus verdict, written whole
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const bool any_bad = __builtin_amdgcn_ballot_w64(bad[j]) != 0;
+            const bool any_bad = __builtin_amdgcn_ballot_w64(diff[j] != 0u) != 0;
             if (live[j] && lane == 0) p.ok_flags[s0 + j] = any_bad ? 0 : 1;
         }
     }

@@ -34,6 +34,13 @@ __device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
+// acc | (a ^ b) in one v_bitop3_b32 (truth table over (S0, S1, S2) =
+// (a, b, acc), index S0*4 + S1*2 + S2): the surplus-parity compares OR
+// their differences into one word per stripe, tested once at the end.
+__device__ __forceinline__ uint32_t or_diff(uint32_t acc, uint32_t a, uint32_t b) {
+    return __builtin_amdgcn_bitop3_b32(a, b, acc, 0xBE);
+}
+
 // odd: input index parity (a compile-time constant in the unrolled loops)
 __device__ __forceinline__ void gf_fold(bool odd, uint32_t& acc, uint32_t& pend, uint32_t a, uint32_t b, uint32_t c) {
     if (odd) {
