@@ -40,14 +40,24 @@ namespace rsg {
 
 template <int NF, int TH>
 struct Net16Shape : RecRing<NF, 4, TH> {
-    static constexpr int NG = 2;                   // network waves A (rows out) and B (half rows to LDS)
+    static constexpr int NG = 2;                   // network waves A (survivors 0-7) and B (8-15)
     static constexpr int WAVES = RecRing<NF, 4, TH>::HW + NG + RecRing<NF, 4, TH>::TW;
-    static constexpr uint32_t XSLOT = 32 * 64 * 4;  // B's 32 partial planes, lane-major (8 KiB)
+    static constexpr uint32_t XSLOT = 32 * 64 * 4;  // a step's exchanged partial planes, lane-major (<= 8 KiB)
     static constexpr int XB = TH ? 1 : 0;           // extra barrier: heal's target hashers trail by 2 steps
 };
 
 __device__ __forceinline__ void put8_16(uint8_t* p, const uint2& v) { *(uint2*)p = v; }
 
+// Network wave A (survivors 0-7) or B (8-15) of the 4-stripe group.  Each
+// runs its half network for all R rows, keeps its half of the rows it
+// finishes — A the stored rows [0, NST), B the compared rows [NST, R) — and
+// hands its half of the other wave's rows over through a double-buffered LDS
+// area; one interval later each XORs the other's half in, transposes its
+// rows back and stores (A; heal: also into the target-row area) or compares
+// them with the surplus rows it kept from the ring (B, which also writes the
+// stripes' verdicts).  Splitting the finishing work by row kind keeps the
+// two waves' issue about equal (a single finishing wave paired with a hash
+// wave on its SIMD set the pace).
 template <int PID, int NF, int TH, bool A>
 __device__ __forceinline__ void net16_wave(const GfApplyParams& p, uint64_t n, uint32_t steps, uint64_t s0,
                                            const uint8_t* ring, uint8_t* xbuf, uint8_t* trow) {
@@ -60,6 +70,16 @@ __device__ __forceinline__ void net16_wave(const GfApplyParams& p, uint64_t n, u
     constexpr int R = pat.R, NST = pat.n_store, NCMP = R - NST, SPW = L::SPW, HS = L::HS;
     static_assert(pat.nf == NF && (pat.heal ? NST : 0) == TH && R <= 4 && NST <= R && HS == 2, "pattern shape");
     constexpr int C0 = A ? 0 : 8;  // this wave's survivors [C0, C0 + 8)
+    // heal (SF): A finishes the stored rows, B the compared ones; GET: A
+    // finishes every row (B holding half the rows as well as GET's
+    // copy-through spilled at the 256-VGPR cap)
+    constexpr bool SF = TH > 0;
+    constexpr int K0 = A ? 0 : NST, KN = A ? (SF ? NST : R) : (SF ? NCMP : 0);  // rows it finishes
+    constexpr int G0 = A ? NST : 0, GN = A ? (SF ? NCMP : 0) : (SF ? NST : R);  // rows it gives away
+    constexpr bool CMP = K0 + KN > NST;  // it finishes compared rows (keeps the surplus rows, writes verdicts)
+    // xbuf: B -> A (its half of the stored rows) at +0, A -> B (its half of the
+    // compared rows) at +2 XSLOT, each double-buffered by step parity
+    constexpr uint32_t TO_A = 0, TO_B = L::XSLOT;
     if (p.wave_prio & kPrioGf) __builtin_amdgcn_s_setprio(2);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t m4 = vgpr_const(0x0f0f0f0fu), m2 = vgpr_const(0x33333333u), m1 = vgpr_const(0x55555555u);
@@ -78,11 +98,13 @@ __device__ __forceinline__ void net16_wave(const GfApplyParams& p, uint64_t n, u
         x[2] = *(const uint2*)(row + CH);
         x[3] = *(const uint2*)(row + IP + CH);
     };
-    uint32_t diff[4] = {0u, 0u, 0u, 0u};         // A: OR of this lane's surplus-parity differences
-    uint32_t O[32];                              // A: step t-1's rows over survivors 0-7, held across B(t)
-    uint2 cmp[NCMP ? NCMP : 1][4];               // A: step t-1's surplus rows, held across B(t)
+    uint32_t diff[4] = {0u, 0u, 0u, 0u};  // CMP: OR of this lane's surplus-parity differences
+    uint32_t keep[32];                    // step t-1's half of the rows it finishes ([8 K0, 8 (K0 + KN))), held across B(t)
+    uint2 cmp[NCMP ? NCMP : 1][4];        // CMP: step t-1's surplus rows, held across B(t)
+    // the exchange slot (direction to, step t) as lane-major dwords
+    auto xb_at = [&](uint32_t to, uint32_t t) { return (uint32_t*)(xbuf + 2 * to + (t & 1) * L::XSLOT) + lane; };
     // step t: this wave's 8 survivors -> planes -> its half of every row;
-    // copy-through of its data survivors (GET); A keeps the surplus rows
+    // the other wave's rows out to LDS; copy-through of its data survivors (GET)
     auto half = [&](uint32_t t) {
         const uint8_t* slot = ring + (t % D) * L::DSLOT + lane * 8u;
         uint32_t P[64];
@@ -95,16 +117,16 @@ __device__ __forceinline__ void net16_wave(const GfApplyParams& p, uint64_t n, u
 #pragma unroll
             for (int j = 0; j < 8; ++j) P[8 * c + j] = w[j];
         }
-        if constexpr (A) {
-            decnet16::net_lo<PID>(P, O);
+        // the network writes every row straight into keep; the given-away
+        // rows are stored to LDS from there and never read again
+        if constexpr (A) decnet16::net_lo<PID>(P, keep);
+        else decnet16::net_hi<PID>(P, keep);
+        uint32_t* xo = xb_at(A ? TO_B : TO_A, t);
+#pragma unroll
+        for (int i = 0; i < 8 * GN; ++i) xo[64 * i] = keep[8 * G0 + i];
+        if constexpr (CMP) {
 #pragma unroll
             for (int r = 0; r < NCMP; ++r) row4(slot + (16 + r) * HS * IP, cmp[r]);
-        } else {
-            uint32_t Ob[32];
-            decnet16::net_hi<PID>(P, Ob);
-            uint32_t* xb = (uint32_t*)(xbuf + (t & 1) * L::XSLOT) + lane;
-#pragma unroll
-            for (int i = 0; i < 8 * R; ++i) xb[64 * i] = Ob[i];
         }
         if (!TH && cmask) {  // GET: this wave's present data survivors copied through
 #pragma unroll
@@ -118,14 +140,16 @@ __device__ __forceinline__ void net16_wave(const GfApplyParams& p, uint64_t n, u
             }
         }
     };
-    // A, step s (in interval s+1): B's half in, rows back to bytes, stores / compares
+    // step s (in interval s+1): the other wave's half in, rows back to bytes,
+    // stores (A) / compares (B)
     auto finish = [&](uint32_t s) {
-        const uint32_t* xb = (const uint32_t*)(xbuf + (s & 1) * L::XSLOT) + lane;
+        const uint32_t* xi = xb_at(A ? TO_A : TO_B, s);
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
+        for (int k = 0; k < KN; ++k) {
+            const int r = K0 + k;  // the row (compile-time after unrolling)
             uint32_t w[8];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) w[i] = O[8 * r + i] ^ xb[64 * (8 * r + i)];
+            for (int i = 0; i < 8; ++i) w[i] = keep[8 * r + i] ^ xi[64 * (8 * k + i)];
             dma::transpose(w, m4, m2, m1);
             if (r < NST) {
 #pragma unroll
@@ -137,16 +161,21 @@ __device__ __forceinline__ void net16_wave(const GfApplyParams& p, uint64_t n, u
                 }
             } else {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint2 o = cmp[r - NST][j];
-                    diff[j] = or_diff(or_diff(diff[j], o.x, w[2 * j]), o.y, w[2 * j + 1]);
-                }
+                for (int j = 0; j < 4; ++j)
+                    diff[j] = or_diff(or_diff(diff[j], cmp[r - NST][j].x, w[2 * j]), cmp[r - NST][j].y,
+                                      w[2 * j + 1]);
             }
         }
     };
     lds_barrier();  // B(0)
-    if constexpr (A) {
-        // interval t: finish step t-1 (B's half published by B(t)), then step t's half
+    if constexpr (KN == 0) {  // GET's B: halves only
+#pragma unroll 1
+        for (uint32_t t = 0; t < steps; ++t) {
+            half(t);
+            lds_barrier();  // B(t+1)
+        }
+    } else {
+        // interval t: finish step t-1 (the other half published by B(t)), then step t's half
 #pragma unroll 1
         for (uint32_t t = 0; t <= steps; ++t) {
             if (t > 0) finish(t - 1);
@@ -155,16 +184,10 @@ __device__ __forceinline__ void net16_wave(const GfApplyParams& p, uint64_t n, u
                 lds_barrier();  // B(t+1)
             }
         }
-    } else {
-#pragma unroll 1
-        for (uint32_t t = 0; t < steps; ++t) {
-            half(t);
-            lds_barrier();  // B(t+1)
-        }
     }
 #pragma unroll
     for (int b = 0; b < L::XB; ++b) lds_barrier();  // B(steps+1): the last target rows published
-    if constexpr (A && NCMP > 0) {  // each stripe's surplus verdict, written whole
+    if constexpr (CMP) {  // each stripe's surplus verdict, written whole
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const bool any_bad = __builtin_amdgcn_ballot_w64(diff[j] != 0u) != 0;
@@ -178,7 +201,7 @@ __global__ __launch_bounds__((64 * Net16Shape<NF, TH>::WAVES)) void k_decode_rec
                                                                                            const HashParams h) {
     using L = Net16Shape<NF, TH>;
     __shared__ __attribute__((aligned(16))) uint8_t ring[dma::D * L::DSLOT];
-    __shared__ __attribute__((aligned(16))) uint8_t xbuf[2 * L::XSLOT];
+    __shared__ __attribute__((aligned(16))) uint8_t xbuf[4 * L::XSLOT];
     __shared__ __attribute__((aligned(16))) uint8_t trow[TH ? 2 * L::TSLOT : 16];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t steps = p.units;
@@ -198,9 +221,11 @@ __global__ __launch_bounds__((64 * Net16Shape<NF, TH>::WAVES)) void k_decode_rec
     records_hash_wave<NF, 4, L::XB>(h, p.wave_prio, ring, wave, steps, s0);
 }
 
-static_assert(dma::D * 2 * 19 * dma::IP + 2 * Net16Shape<19, 0>::XSLOT + 16 <= 160 * 1024, "RS(16,4) GET fits");
-static_assert(dma::D * 2 * 18 * dma::IP + 2 * Net16Shape<18, 2>::XSLOT + 2 * Net16Shape<18, 2>::TSLOT <= 160 * 1024,
+static_assert(dma::D * 2 * 19 * dma::IP + 4 * Net16Shape<19, 0>::XSLOT + 16 <= 160 * 1024, "RS(16,4) GET fits");
+static_assert(dma::D * 2 * 18 * dma::IP + 4 * Net16Shape<18, 2>::XSLOT + 2 * Net16Shape<18, 2>::TSLOT <= 160 * 1024,
               "RS(16,4) heal fits");
+static_assert(dma::D * 2 * 19 * dma::IP + 4 * Net16Shape<19, 1>::XSLOT + 2 * Net16Shape<19, 1>::TSLOT <= 160 * 1024,
+              "RS(16,4) heal of one shard fits");
 
 using Net16Launch = void (*)(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream);
 
