@@ -11,6 +11,6 @@ for envs in "$@"; do
   python - $OUT/ab$i.json "$envs" <<'PY'
 import json,sys
 d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); g=d['extras']['engines']
-print(sys.argv[2], {k:(v.get('kernel_ms'),v['frac']) for k,v in g.items() if isinstance(v,dict) and 'get_all' not in k and 'bitrot' not in k}, flush=True)
+print(sys.argv[2], {k:(v.get('kernel_ms'),v['frac']) for k,v in g.items() if isinstance(v,dict) and 'bitrot' not in k}, flush=True)
 PY
 done
