@@ -243,16 +243,22 @@ def random_stripes(dev, k, m, S, n, seed):
     return st
 
 
-def pmc_traffic(k, m, S, n, digests):
-    """HBM bytes per launch of this configuration's kernel from the committed
-    PMC passes (profiles/pmc_traffic.json: FETCH_SIZE x 2 + WRITE_SIZE, the
-    microarch guide's gfx950 correction; tools/pmc.sh, tools/pmc_traffic.py),
-    or None when no pass covered it."""
-    prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "tools", "pmc_traffic.json")
+
+
+def pmc_lookup(key):
+    """HBM bytes per call of one measured configuration from the committed
+    PMC passes (tools/pmc_traffic.json, shipped with the tree: FETCH_SIZE x 2
+    + WRITE_SIZE, the microarch guide's gfx950 correction; tools/pmc.sh,
+    tools/pmc_engine.sh, tools/pmc_traffic.py), or None when no pass covered it."""
     try:
-        return json.load(open(prof)).get(f"rs{k}{m}_S{S}_n{n}{'_hash' if digests else ''}", {}).get("bytes_per_launch")
+        return json.load(open(PMC_TRAFFIC)).get(key, {}).get("bytes_per_launch")
     except Exception:
         return None
+
+
+def pmc_traffic(k, m, S, n, digests):
+    return pmc_lookup(f"rs{k}{m}_S{S}_n{n}{'_hash' if digests else ''}")
 
 
 def time_encode(e, stripes, digests, stream, reps, warm=3, warm_seconds=0.3):
@@ -352,7 +358,7 @@ def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto"):
     from rustfs_amd import _lib
     L, ctx = _lib.load(), _lib.context(stripes.device.index or 0).handle
 
-    def timed(name, fn, alg, check, reps=5):
+    def timed(name, fn, alg, check, reps=5, traffic_key=None):
         fn()
         torch.cuda.synchronize()
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -365,7 +371,8 @@ def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto"):
         check(r)
         res[name] = {"call_ms": round(ms, 4), "GiB_s_payload": round(n * k * S / (ms * 1e-3) / GiB, 1),
                      "alg_bytes": alg, "achieved_GB_s": round(alg / (ms * 1e-3) / 1e9, 1),
-                     "frac_call": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                     "frac_call": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "traffic": pmc_lookup(traffic_key) if traffic_key else None}
         # the engine's kernels alone (HIP events around its launches inside
         # the call, rsg_set_kernel_timing), averaged over `reps` more calls
         kms = []
@@ -384,6 +391,28 @@ def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto"):
         else:
             res[name]["frac"] = res[name]["frac_call"]
 
+    def timed_pipelined(name, submit, alg, check, reps=8):
+        """`reps` calls, each submitted before the previous one is waited on
+        (the asynchronous ABI), timed with HIP events on the stream around
+        all of them: the device never idles while the host reads a batch's
+        verdicts, so the per-call time approaches the kernel time."""
+        submit().wait()
+        torch.cuda.synchronize()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record(stream)
+        tk = submit()
+        for _ in range(reps - 1):
+            nxt = submit()
+            r = tk.wait()
+            tk = nxt
+        r = tk.wait()
+        ev[1].record(stream)
+        torch.cuda.synchronize()
+        ms = ev[0].elapsed_time(ev[1]) / reps
+        check(r)
+        res[name] = {"call_ms": round(ms, 4), "calls": reps, "GiB_s_payload": round(n * k * S / (ms * 1e-3) / GiB, 1),
+                     "alg_bytes": alg, "frac_call": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
     _lib.check(L.rsg_set_record_engine(ctx, {"auto": _lib.RSG_RECORD_ENGINE_AUTO,
                                               "one-pass": _lib.RSG_RECORD_ENGINE_ONE_PASS,
                                               "two-pass": _lib.RSG_RECORD_ENGINE_TWO_PASS}[record_engine]))
@@ -393,11 +422,38 @@ def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto"):
         o, status = r
         assert all(x == 0 for x in status) and torch.equal(o[n - 1], want_last)
 
-    timed("get_all_present", lambda: e.decode_records_batch(files, S, n, out=out, stream=stream),
-          n * (k * rec + k * S), ok_get)
+    # GET, in-place form (rsg_decode_records_into_dev, reconstruct_into's
+    # contract, bridge.rs:274-307): present data served from the verified
+    # records, only the lost shards written into their slots — all present:
+    # the k data records read once; two data disks lost: t-2 records read, two
+    # shards written
+    slots = torch.empty((n, k * S), dtype=torch.uint8, device=stripes.device)
+
+    def ok_into(lost):
+        def check(r):
+            sl, src, status = r
+            assert all(x == 0 for x in status)
+            for i in range(k):
+                assert (not src[i].any()) if i in lost else src[i].all(), i
+            for i in lost:
+                assert torch.equal(sl.view(n, k, S)[n - 1, i], want_last.view(k, S)[i])
+        return check
+
     lost = [None if i in (0, 3) else files[i] for i in range(t)]
-    timed("get_2_data_lost", lambda: e.decode_records_batch(lost, S, n, out=out, stream=stream),
-          n * ((t - 2) * rec + k * S), ok_get)
+    timed("get_all_present", lambda: e.decode_records_into_batch(files, S, n, targets=slots, stream=stream),
+          n * k * rec, ok_into(()), traffic_key=f"get_into0_rs{k}{m}_S{S}_n{n}")
+    timed("get_2_data_lost", lambda: e.decode_records_into_batch(lost, S, n, targets=slots, stream=stream),
+          n * ((t - 2) * rec + 2 * S), ok_into((0, 3)), traffic_key=f"get_into2_rs{k}{m}_S{S}_n{n}")
+    # the same GETs submitted back to back (rsg_decode_records_submit): each
+    # batch's status handling overlaps the next batch's kernels
+    timed_pipelined("get_2_data_lost_async",
+                    lambda: e.decode_records_submit(lost, S, n, targets=slots, inplace=True, stream=stream),
+                    n * ((t - 2) * rec + 2 * S), ok_into((0, 3)))
+    # gather form (rsg_decode_records_dev: every data shard copied to one block buffer)
+    timed("get_all_present_gather", lambda: e.decode_records_batch(files, S, n, out=out, stream=stream),
+          n * (k * rec + k * S), ok_get, traffic_key=f"get_gather0_rs{k}{m}_S{S}_n{n}")
+    timed("get_2_data_lost_gather", lambda: e.decode_records_batch(lost, S, n, out=out, stream=stream),
+          n * ((t - 2) * rec + k * S), ok_get, traffic_key=f"get_gather2_rs{k}{m}_S{S}_n{n}")
     tg = [torch.empty(n * rec, dtype=torch.uint8, device=stripes.device) if i in (1, k) else None for i in range(t)]
     src = [None if i in (1, k) else files[i] for i in range(t)]
 
@@ -407,12 +463,14 @@ def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto"):
     def ok_verify(status):
         assert status == [0] * t
 
-    timed("heal_1data_1parity", lambda: e.heal_records_batch(src, tg, S, n, work=out, stream=stream),
-          n * ((t - 2) * rec + 2 * rec), ok_heal)
+    timed("heal_1data_1parity", lambda: e.heal_records_batch(src, tg, S, n, stream=stream),
+          n * ((t - 2) * rec + 2 * rec), ok_heal, traffic_key=f"heal_1d1p_rs{k}{m}_S{S}_n{n}")
+    timed_pipelined("heal_1data_1parity_async", lambda: e.heal_records_submit(src, tg, S, n, stream=stream),
+                    n * ((t - 2) * rec + 2 * rec), ok_heal)
     timed("bitrot_verify_all_files",
           lambda: bitrot_verify_batch(files, n * rec, n * S, HashAlgorithm.HighwayHash256S, S, stream=stream),
           t * n * rec, ok_verify)
-    del files, lost, tg, src, out
+    del files, lost, tg, src, out, slots
     torch.cuda.empty_cache()
     return res
 

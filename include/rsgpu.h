@@ -17,9 +17,10 @@
  * (own stream and device buffer), so up to 8 concurrent callers overlap and
  * further ones wait for a free lane (the reference calls encode from many
  * tokio workers concurrently, encode.rs:511-526).  Device-batch calls are
- * asynchronous on the caller's stream; the record engines (decode / heal /
- * bitrot_verify) share the context's scratch and run one at a time.
- * Host-batch tickets may be polled or waited on from several threads.
+ * asynchronous on the caller's stream; every record-engine call (decode / heal /
+ * bitrot_verify) takes its own scratch from the context's pool, so concurrent
+ * calls overlap.  Tickets (host-batch PUT, asynchronous GET / heal) may be
+ * polled or waited on from several threads.
  *
  * Errors: functions return an rsg_status; rsg_strerror() gives the message
  * fragment the reference uses for the same condition (erasure.rs:87-121,
@@ -35,7 +36,7 @@
 extern "C" {
 #endif
 
-#define RSG_ABI_VERSION 4
+#define RSG_ABI_VERSION 5
 #define RSG_MAX_TOTAL_SHARDS 256 /* galois_8::Field::ORDER, erasure.rs:72 */
 #define RSG_DIGEST_BYTES 32      /* HighwayHash-256 */
 
@@ -184,6 +185,45 @@ int rsg_decode_records_dev(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t 
                            const uint8_t *const *d_files, int algo, int verify_surplus,
                            uint8_t *d_out, int *h_status, void *stream);
 
+/* GET-side engine, in-place form (ABI 5): RustfsCodecDecodeEngine::reconstruct_into
+ * (bridge.rs:274-307) fills only the None slots of its shards slice and skips a
+ * stripe whose data shards are all present (data_shards_complete ->
+ * skip_data_complete, bridge.rs:52-54); write_data_blocks then writes straight
+ * from the per-shard buffers (decode.rs:1390).  Same sources, verification and
+ * statuses as rsg_decode_records_dev, but a data shard whose record verifies is
+ * served from that record (its body at d_files[i] + s*(32+shard_len) + 32) and
+ * nothing is copied; only the shards no verified record serves — file absent or
+ * record rotten — are rebuilt, into d_targets[i] + s*target_stride.
+ * d_targets: k device slots, one per data shard, each at least
+ * (n-1)*target_stride + shard_len bytes (target_stride >= shard_len;
+ * target_stride = k*shard_len with d_targets[i] = base + i*shard_len gives the
+ * contiguous block layout); a slot range overlapping a source record file is
+ * RSG_ERR_INVALID_ARG.  With every data file present the call only verifies
+ * the k data records of each stripe (parity is read for a stripe only if one of
+ * its data records is rotten).  h_src (host, optional, k*n bytes, [shard][stripe]):
+ * 1 where data shard i of stripe s is served from its record, 0 where it was
+ * written to its slot (unspecified for a failed stripe).  Synchronous. */
+int rsg_decode_records_into_dev(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t n,
+                                const uint8_t *const *d_files, int algo, int verify_surplus,
+                                uint8_t *const *d_targets, size_t target_stride, uint8_t *h_src,
+                                int *h_status, void *stream);
+
+/* Asynchronous GET (ABI 5): either form — d_out (gather) or d_targets +
+ * target_stride (in place), exactly one non-NULL — queued on `stream` with a
+ * ticket returned at once, so a caller decoding many batches (decode.rs's
+ * pipeline, decode.rs:1702-1968) overlaps one batch's status handling with the
+ * next batch's kernels.  rsg_poll / rsg_wait complete it (the same tickets as
+ * the host-batch PUT); h_status and h_src are filled when the ticket completes,
+ * and every buffer must stay alive and unmodified (sources) / unread (outputs)
+ * until then.  Each call uses its own scratch: calls from several threads run
+ * concurrently.  Completion normally needs no further device work; a batch with
+ * a rotten record is redone for the affected stripes inside the wait/poll that
+ * completes it. */
+int rsg_decode_records_submit(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t n,
+                              const uint8_t *const *d_files, int algo, int verify_surplus,
+                              uint8_t *d_out, uint8_t *const *d_targets, size_t target_stride,
+                              uint8_t *h_src, int *h_status, void *stream, uint64_t *ticket);
+
 /* Heal, batched (Erasure::heal, heal.rs:112-206, which calls
  * decode_data_and_parity, erasure.rs:917, per block).  Sources as in
  * rsg_decode_records_dev (d_files[i] == NULL: no reader; every record is
@@ -202,6 +242,13 @@ int rsg_decode_records_dev(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t 
 int rsg_heal_records_dev(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t n,
                          const uint8_t *const *d_files, uint8_t *const *d_targets, int algo,
                          uint8_t *d_work, int *h_status, void *stream);
+
+/* Asynchronous heal (ABI 5): rsg_heal_records_dev queued with a ticket, as
+ * rsg_decode_records_submit (heal.rs's per-block loop, heal.rs:112-206, batched
+ * and overlapped). */
+int rsg_heal_records_submit(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t n,
+                            const uint8_t *const *d_files, uint8_t *const *d_targets, int algo,
+                            int *h_status, void *stream, uint64_t *ticket);
 
 /* Whole-shard-file bitrot verification (bitrot_verify, bitrot.rs:616-655) of
  * n_files device-resident shard files of one part (file f: file_lens[f]

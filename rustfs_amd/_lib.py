@@ -62,7 +62,8 @@ EXPORTED = (
     "rsg_hash_batch_dev", "rsg_sync", "rsg_encode_batch_host", "rsg_pin", "rsg_unpin",
     "rsg_decode_records_dev", "rsg_heal_records_dev", "rsg_bitrot_verify_dev",
     "rsg_encode_batch_host_submit", "rsg_poll", "rsg_wait", "rsg_set_kernel_timing", "rsg_last_kernel_ms",
-    "rsg_set_record_engine",
+    "rsg_set_record_engine", "rsg_decode_records_into_dev", "rsg_decode_records_submit",
+    "rsg_heal_records_submit",
 )
 
 
@@ -118,6 +119,10 @@ def load():
         L.rsg_wait.argtypes = [P, ctypes.c_uint64]
         L.rsg_decode_records_dev.argtypes = [P, I, I, S, S, P, I, I, P, P, P]
         L.rsg_heal_records_dev.argtypes = [P, I, I, S, S, P, P, I, P, P, P]
+        L.rsg_decode_records_into_dev.argtypes = [P, I, I, S, S, P, I, I, P, S, P, P, P]
+        L.rsg_decode_records_submit.argtypes = [P, I, I, S, S, P, I, I, P, P, S, P, P, P,
+                                                ctypes.POINTER(ctypes.c_uint64)]
+        L.rsg_heal_records_submit.argtypes = [P, I, I, S, S, P, P, I, P, P, ctypes.POINTER(ctypes.c_uint64)]
         L.rsg_bitrot_verify_dev.argtypes = [P, I, S, P, P, S, S, S, P, P]
         L.rsg_pin.argtypes = [P, S]
         L.rsg_unpin.argtypes = [P]

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <list>
 #include <map>
 #include <memory>
@@ -478,12 +479,106 @@ struct HostLane {
 
 constexpr int kHostLanes = 8;
 
+// Scratch of one record-engine call (GET / heal / bitrot_verify): the device
+// verify flags and surplus verdicts, their page-locked mirror (the verdict
+// D2H is a few tens of KB, where a pageable copy's staging costs more than
+// the copy) and the timing marks of rsg_set_kernel_timing.  Calls take one
+// from the context's pool, so concurrent calls never share scratch.
+struct RecScratch {
+    uint8_t* d = nullptr;
+    size_t dcap = 0;
+    uint8_t* h = nullptr;
+    size_t hcap = 0;
+    bool timing = false;
+    std::vector<hipEvent_t> tev;
+    size_t tev_used = 0;
+
+    RecScratch() = default;
+    RecScratch(const RecScratch&) = delete;
+    RecScratch& operator=(const RecScratch&) = delete;
+    ~RecScratch() {  // the context's device is current (rsg_destroy / job release)
+        if (d) (void)hipFree(d);
+        if (h) (void)hipHostFree(h);
+        for (hipEvent_t e : tev) (void)hipEventDestroy(e);
+    }
+    int ensure(size_t dbytes, size_t hbytes) {
+        if (dbytes > dcap) {
+            if (d) (void)hipFree(d);
+            d = nullptr;
+            dcap = 0;
+            const size_t want = std::max(dbytes, (size_t)64 << 10);
+            hipError_t e = hipMalloc((void**)&d, want);
+            if (e != hipSuccess) return hip_status(e);
+            dcap = want;
+        }
+        if (hbytes > hcap) {
+            if (h) (void)hipHostFree(h);
+            h = nullptr;
+            hcap = 0;
+            const size_t want = std::max(hbytes, (size_t)64 << 10);
+            hipError_t e = hipHostMalloc((void**)&h, want, hipHostMallocDefault);
+            if (e != hipSuccess) return hip_status(e);
+            hcap = want;
+        }
+        return RSG_OK;
+    }
+    // HIP event pairs around the kernel launches on the call's stream
+    void tmark(hipStream_t s) {
+        if (!timing) return;
+        if (tev_used == tev.size()) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return;
+            tev.push_back(e);
+        }
+        (void)hipEventRecord(tev[tev_used++], s);
+    }
+    void tunmark() {  // drop the last mark (a launch that did not happen)
+        if (timing && tev_used) --tev_used;
+    }
+    // summed kernel time once the stream has passed the last mark, or -1
+    float tsum() {
+        float sum = 0.f;
+        for (size_t i = 0; i + 1 < tev_used; i += 2) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, tev[i], tev[i + 1]) == hipSuccess) sum += ms;
+        }
+        const float r = (timing && tev_used >= 2) ? sum : -1.f;
+        tev_used = 0;
+        return r;
+    }
+};
+
 struct rsg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    std::mutex mu;  // serialises the device-batch record engines' scratch use
-    uint8_t* d_scratch = nullptr;
-    size_t scratch_cap = 0;
+
+    // record-engine scratch pool (RecScratch): taken per call, returned when
+    // the call's ticket finishes
+    std::mutex rec_mu;
+    std::vector<std::unique_ptr<RecScratch>> rec_free;
+    std::atomic<bool> timing{false};          // rsg_set_kernel_timing
+    std::atomic<int> record_engine{RSG_RECORD_ENGINE_AUTO};  // rsg_set_record_engine
+    std::atomic<float> last_kernel_ms{-1.f};  // the last finished timed record call
+
+    std::unique_ptr<RecScratch> take_scratch() {
+        std::unique_ptr<RecScratch> sc;
+        {
+            std::lock_guard<std::mutex> g(rec_mu);
+            if (!rec_free.empty()) {
+                sc = std::move(rec_free.back());
+                rec_free.pop_back();
+            }
+        }
+        if (!sc) sc.reset(new RecScratch());
+        sc->timing = timing.load();
+        sc->tev_used = 0;
+        return sc;
+    }
+    void give_scratch(std::unique_ptr<RecScratch> sc) {
+        if (!sc) return;
+        std::lock_guard<std::mutex> g(rec_mu);
+        if (rec_free.size() < 16) rec_free.push_back(std::move(sc));  // else freed here
+    }
 
     HostLane lanes[kHostLanes];
     std::atomic<unsigned> next_lane{0};
@@ -502,9 +597,18 @@ struct rsg_ctx {
     uint64_t next_ticket = 1;
     // A job's completion events, destroyed with the last reference: a ticket
     // waited on by several threads keeps its events alive until every waiter
-    // has returned.
+    // has returned.  Record-engine jobs (GET / heal) also carry a host
+    // finishing step, run once by the first waiter or poller that sees the
+    // events complete (it reads the verdicts the job copied back and redoes
+    // the rare stripes whose verified pattern differs from the assumed one);
+    // every waiter gets its result.  The step's argument is the events'
+    // status: a failed job only releases its scratch.
     struct Job {
         std::vector<hipEvent_t> done;
+        std::function<int(int)> finish;
+        std::mutex fin_mu;
+        bool finished = false;
+        int result = RSG_OK;
         Job() = default;
         Job(const Job&) = delete;
         Job& operator=(const Job&) = delete;
@@ -513,69 +617,6 @@ struct rsg_ctx {
         }
     };
     std::map<uint64_t, std::shared_ptr<Job>> jobs;
-
-    // page-locked mirror of the flag scratch: the verdict D2H of the record
-    // engines is a few tens of KB, where a pageable copy's staging costs more
-    // than the copy (ctx->mu held)
-    uint8_t* h_flags = nullptr;
-    size_t h_flags_cap = 0;
-
-    int ensure_host_flags(size_t bytes) {
-        if (bytes <= h_flags_cap) return RSG_OK;
-        if (h_flags) (void)hipHostFree(h_flags);
-        h_flags = nullptr;
-        h_flags_cap = 0;
-        const size_t want = std::max(bytes, (size_t)64 << 10);
-        hipError_t e = hipHostMalloc((void**)&h_flags, want, hipHostMallocDefault);
-        if (e != hipSuccess) return hip_status(e);
-        h_flags_cap = want;
-        return RSG_OK;
-    }
-
-    // Measurement hook (rsg_set_kernel_timing, bench.py): HIP event pairs
-    // around the record engines' kernel launches on the call's stream, summed
-    // after the call's last synchronisation (ctx->mu held).
-    bool timing = false;
-    int record_engine = RSG_RECORD_ENGINE_AUTO;  // rsg_set_record_engine (ctx->mu held)
-    std::vector<hipEvent_t> tev;
-    size_t tev_used = 0;
-    float last_kernel_ms = -1.f;
-
-    void tmark(hipStream_t s) {
-        if (!timing) return;
-        if (tev_used == tev.size()) {
-            hipEvent_t e;
-            if (hipEventCreate(&e) != hipSuccess) return;
-            tev.push_back(e);
-        }
-        (void)hipEventRecord(tev[tev_used++], s);
-    }
-    void tunmark() {  // drop the last mark (a launch that did not happen)
-        if (timing && tev_used) --tev_used;
-    }
-    // after the stream has been synchronised
-    void tcollect() {
-        if (!timing) return;
-        float sum = 0.f;
-        for (size_t i = 0; i + 1 < tev_used; i += 2) {
-            float ms = 0.f;
-            if (hipEventElapsedTime(&ms, tev[i], tev[i + 1]) == hipSuccess) sum += ms;
-        }
-        last_kernel_ms = tev_used >= 2 ? sum : -1.f;
-        tev_used = 0;
-    }
-
-    int ensure_scratch(size_t bytes) {
-        if (bytes <= scratch_cap) return RSG_OK;
-        if (d_scratch) (void)hipFree(d_scratch);
-        d_scratch = nullptr;
-        scratch_cap = 0;
-        size_t cap = std::max(bytes, (size_t)1 << 20);
-        hipError_t e = hipMalloc((void**)&d_scratch, cap);
-        if (e != hipSuccess) return hip_status(e);
-        scratch_cap = cap;
-        return RSG_OK;
-    }
 
     // pipe_mu held.  Growing the staging buffers waits for every sub-batch in
     // flight (they may still be reading the old ones).
@@ -722,8 +763,14 @@ void rsg_destroy(rsg_ctx* ctx) {
         (void)hipStreamSynchronize(ctx->stream);
         (void)hipStreamDestroy(ctx->stream);
     }
-    if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
-    if (ctx->h_flags) (void)hipHostFree(ctx->h_flags);
+    // tickets never waited on: their work drains before anything is freed
+    // (a record job's finishing step then releases its scratch)
+    std::vector<uint64_t> pending;
+    {
+        std::lock_guard<std::mutex> g(ctx->pipe_mu);
+        for (auto& j : ctx->jobs) pending.push_back(j.first);
+    }
+    for (uint64_t t : pending) (void)rsg_wait(ctx, t);
     for (HostLane& l : ctx->lanes) {
         if (l.stream) {
             (void)hipStreamSynchronize(l.stream);
@@ -739,7 +786,7 @@ void rsg_destroy(rsg_ctx* ctx) {
         if (ctx->d_stage[i]) (void)hipFree(ctx->d_stage[i]);
     }
     ctx->jobs.clear();  // events destroyed with the last reference
-    for (hipEvent_t e : ctx->tev) (void)hipEventDestroy(e);
+    ctx->rec_free.clear();
     delete ctx;
 }
 
@@ -877,6 +924,15 @@ int finish_ticket(rsg_ctx* ctx, uint64_t ticket, bool wait, int* done) {
         }
         if (q != hipSuccess && !res) res = hip_status(q);
     }
+    {  // a record job's host finishing step, exactly once
+        std::lock_guard<std::mutex> g(job->fin_mu);
+        if (!job->finished) {
+            job->result = job->finish ? job->finish(res) : res;
+            job->finish = nullptr;  // releases the job's scratch
+            job->finished = true;
+        }
+        res = job->result;
+    }
     {
         std::lock_guard<std::mutex> g(ctx->pipe_mu);
         auto it = ctx->jobs.find(ticket);
@@ -1010,7 +1066,7 @@ int rsg_hash_batch_dev(rsg_ctx* ctx, int algo, const uint8_t* d_data, size_t len
     return hash_messages(algo, d_data, len, n, 1, 0, stride, d_out, pick_stream(ctx, stream));
 }
 
-// GET-side engine: verify every [digest][block] record, then copy or rebuild
+// GET-side engine: verify every [digest][block] record, then serve or rebuild
 // the data shards of each stripe, runs of stripes with one erasure pattern at
 // a time (normally one run: whole shard files present or absent).
 }  // extern "C"
@@ -1155,67 +1211,78 @@ int launch_verify_and_digest(const std::vector<int>& idx, const uint8_t* const* 
     return RSG_OK;
 }
 
-// Device flags -> host through the context's page-locked buffer, stream
+// Device bytes -> host through the call's page-locked mirror, stream
 // synchronised on return.
-int flags_to_host(rsg_ctx* ctx, const uint8_t* d_src, size_t bytes, uint8_t* dst, hipStream_t s) {
+int flags_to_host(RecScratch& sc, const uint8_t* d_src, size_t bytes, uint8_t* dst, hipStream_t s) {
     int st;
-    if ((st = ctx->ensure_host_flags(bytes))) return st;
-    if ((st = hip_status(hipMemcpyAsync(ctx->h_flags, d_src, bytes, hipMemcpyDeviceToHost, s)))) return st;
+    if ((st = sc.ensure(0, bytes))) return st;
+    if ((st = hip_status(hipMemcpyAsync(sc.h, d_src, bytes, hipMemcpyDeviceToHost, s)))) return st;
     if ((st = hip_status(hipStreamSynchronize(s)))) return st;
-    std::memcpy(dst, ctx->h_flags, bytes);
+    std::memcpy(dst, sc.h, bytes);
     return RSG_OK;
 }
 
-// GET-side verify-before-use: the data records are verified and gathered into
-// d_out in one pass; parity records are read only for stripes that need them
-// (a data record missing or rotten), or for all stripes with all_parity (heal).
-// flags (host) returns the verified map [shard][stripe]; an unread parity
-// record counts as absent.  Uses ctx->d_scratch[0, t*n).
-int verify_gather(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64_t n, const uint8_t* const* d_files,
-                  const uint64_t* key, uint8_t* d_out, bool all_parity, std::vector<uint8_t>& flags, hipStream_t s) {
-    const int t = k + m;
-    uint8_t* d_flags = ctx->d_scratch;
-    int st;
-    if ((st = hip_status(hipMemsetAsync(d_flags, 0, (size_t)t * n, s)))) return st;
-    std::vector<int> data_idx, par_idx, all_idx;
-    for (int i = 0; i < t; ++i)
-        if (d_files[i]) {
-            (i < k ? data_idx : par_idx).push_back(i);
-            all_idx.push_back(i);
-        }
-    flags.assign((size_t)t * n, 0);
-    if (all_parity || (int)data_idx.size() < k) {
-        // every stripe needs its parity (heal, or a lost data disk): all
-        // present records of all stripes in one launch, data gathered
-        ctx->tmark(s);
-        if ((st = launch_verify_group(all_idx, d_files, d_flags, k, shard_len, n, 0, n, key, d_out, s))) return st;
-        ctx->tmark(s);
-        return flags_to_host(ctx, d_flags, (size_t)t * n, flags.data(), s);
+uint64_t rel(const uint8_t* p, const uint8_t* base) { return (uint64_t)(uintptr_t)p - (uint64_t)(uintptr_t)base; }
+
+// Where a GET puts data shard i of stripe s: the gather form's contiguous
+// output (n x k*S, every data shard: rsg_decode_records_dev), or the in-place
+// form's per-shard target buffers (rsg_decode_records_into_dev: like
+// reconstruct_into, only the shards no verified record serves are written).
+struct GetOut {
+    uint8_t* d_out = nullptr;
+    std::vector<uint8_t*> tg;  // in-place form: k targets
+    uint64_t tstride = 0, S = 0, ks = 0;
+    bool into() const { return !tg.empty(); }
+    uint8_t* at(int i, uint64_t s) const { return into() ? tg[i] + s * tstride : d_out + s * ks + (uint64_t)i * S; }
+    uint64_t stride() const { return into() ? tstride : ks; }
+};
+
+// One record-engine call (GET or heal) between its submit and its finish.
+// submit (get_begin / heal_begin) enqueues the optimistic pass — the one the
+// call normally needs alone — and the copy of its verdicts into the call's
+// page-locked scratch; the ticket's event follows that copy.  finish
+// (get_finish / heal_finish), on the first wait or poll that sees the event
+// complete, reads the verdicts, redoes the rare runs of stripes whose
+// verified pattern differs from the assumed one and fills the caller's
+// status array.  The scratch goes back to the context's pool with the job.
+struct RecJob {
+    rsg_ctx* ctx = nullptr;
+    bool heal = false;
+    int k = 0, m = 0, t = 0;
+    uint64_t S = 0, n = 0, rec = 0;
+    const uint64_t* key = nullptr;
+    bool verify_surplus = false;
+    std::vector<const uint8_t*> files;  // t entries (null: unavailable)
+    std::vector<uint8_t*> targets;      // heal: t entries (null: no writer)
+    GetOut out;                         // GET
+    int* h_status = nullptr;
+    uint8_t* h_src = nullptr;  // GET in-place form, optional: [k][n], 1 = served from its record
+    hipStream_t s = nullptr;
+    std::unique_ptr<RecScratch> sc;
+    hipEvent_t fin = nullptr;  // the finishing step's own work (redo runs), when it has any
+    std::shared_ptr<Codec> cd;
+    enum Phase { GENERAL, FAST, DATA_VERIFIED } phase = GENERAL;
+    bool one_pass = false, any_verify = false;
+    std::vector<uint8_t> present0;
+
+    uint8_t* d_flags() const { return sc->d; }
+    uint8_t* d_ok() const { return sc->d + (size_t)t * n; }
+    ~RecJob() {
+        if (fin) (void)hipEventDestroy(fin);
+        if (sc) ctx->give_scratch(std::move(sc));
     }
-    ctx->tmark(s);
-    if ((st = launch_verify_group(data_idx, d_files, d_flags, k, shard_len, n, 0, n, key, d_out, s))) return st;
-    ctx->tmark(s);
-    if ((st = flags_to_host(ctx, d_flags, (size_t)k * n, flags.data(), s))) return st;
-    uint64_t lo = n, hi = 0;
-    if (all_parity) {
-        lo = 0;
-        hi = n;
-    } else {
-        for (uint64_t x = 0; x < n; ++x) {
-            bool whole = true;
-            for (int i = 0; i < k && whole; ++i) whole = flags[(size_t)i * n + x] != 0;
-            if (!whole) {
-                lo = std::min(lo, x);
-                hi = x + 1;
-            }
-        }
+    // wait for the work this finishing step queued (not for whatever the
+    // caller queued on the stream after the job)
+    int drain() {
+        int st;
+        if (!fin && (st = hip_status(hipEventCreateWithFlags(&fin, hipEventDisableTiming)))) return st;
+        if ((st = hip_status(hipEventRecord(fin, s)))) return st;
+        return hip_status(hipEventSynchronize(fin));
     }
-    if (lo >= hi || par_idx.empty()) return RSG_OK;
-    ctx->tmark(s);
-    if ((st = launch_verify_group(par_idx, d_files, d_flags, k, shard_len, n, lo, hi, key, nullptr, s))) return st;
-    ctx->tmark(s);
-    return flags_to_host(ctx, d_flags + (size_t)k * n, (size_t)m * n, flags.data() + (size_t)k * n, s);
-}
+    void collect_time() {
+        if (sc->timing) ctx->last_kernel_ms.store(sc->tsum());
+    }
+};
 
 // One-pass GET/heal (k_decode_records_dma) for a batch of n stripes.  A
 // workgroup walks its 8 stripes front to back (~0.6 ms for 1 MiB RS(8,4)
@@ -1225,344 +1292,715 @@ int verify_gather(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64_t n, co
 // record-engine setting (rsg_set_record_engine: tests and A/B runs) forces
 // either path.
 bool get_dma_enabled(const rsg_ctx* ctx, uint64_t n) {
-    if (ctx->record_engine == RSG_RECORD_ENGINE_ONE_PASS) return true;
-    if (ctx->record_engine == RSG_RECORD_ENGINE_TWO_PASS) return false;
+    const int e = ctx->record_engine.load();
+    if (e == RSG_RECORD_ENGINE_ONE_PASS) return true;
+    if (e == RSG_RECORD_ENGINE_TWO_PASS) return false;
     return n >= 1024;
 }
 
+// Every present record of every stripe verified in one launch (gathering the
+// present data into d_out when given); flags returns the verified map
+// [shard][stripe].  Synchronous.
+int verify_all(RecJob& j, uint8_t* d_out, std::vector<uint8_t>& flags) {
+    int st;
+    if ((st = hip_status(hipMemsetAsync(j.d_flags(), 0, (size_t)j.t * j.n, j.s)))) return st;
+    std::vector<int> all_idx;
+    for (int i = 0; i < j.t; ++i)
+        if (j.files[i]) all_idx.push_back(i);
+    j.sc->tmark(j.s);
+    if ((st = launch_verify_group(all_idx, j.files.data(), j.d_flags(), j.k, j.S, j.n, 0, j.n, j.key, d_out, j.s))) return st;
+    j.sc->tmark(j.s);
+    flags.assign((size_t)j.t * j.n, 0);
+    return flags_to_host(*j.sc, j.d_flags(), flags.size(), flags.data(), j.s);
+}
+
+// GET verify-before-use, first half: the k data records of every stripe
+// verified (and gathered into d_out when given) in one launch, their flags
+// copied back asynchronously into the scratch mirror [0, k*n); the parity
+// rows are cleared on the device.
+int verify_data_begin(RecJob& j, uint8_t* d_out) {
+    int st;
+    if ((st = hip_status(hipMemsetAsync(j.d_flags(), 0, (size_t)j.t * j.n, j.s)))) return st;
+    std::vector<int> data_idx;
+    for (int i = 0; i < j.k; ++i)
+        if (j.files[i]) data_idx.push_back(i);
+    j.sc->tmark(j.s);
+    if ((st = launch_verify_group(data_idx, j.files.data(), j.d_flags(), j.k, j.S, j.n, 0, j.n, j.key, d_out, j.s)))
+        return st;
+    j.sc->tmark(j.s);
+    return hip_status(hipMemcpyAsync(j.sc->h, j.d_flags(), (size_t)j.k * j.n, hipMemcpyDeviceToHost, j.s));
+}
+
+// Second half, once the data flags have landed: the parity records are
+// verified for the stripes that need them (a data record rotten), and flags
+// returns the whole verified map (an unread parity record counts as absent).
+int verify_parity_rest(RecJob& j, std::vector<uint8_t>& flags) {
+    const int k = j.k, t = j.t;
+    const uint64_t n = j.n;
+    flags.assign((size_t)t * n, 0);
+    std::memcpy(flags.data(), j.sc->h, (size_t)k * n);
+    uint64_t lo = n, hi = 0;
+    for (uint64_t x = 0; x < n; ++x) {
+        bool whole = true;
+        for (int i = 0; i < k && whole; ++i) whole = flags[(size_t)i * n + x] != 0;
+        if (!whole) {
+            lo = std::min(lo, x);
+            hi = x + 1;
+        }
+    }
+    std::vector<int> par_idx;
+    for (int i = k; i < t; ++i)
+        if (j.files[i]) par_idx.push_back(i);
+    if (lo >= hi || par_idx.empty()) return RSG_OK;
+    int st;
+    j.sc->tmark(j.s);
+    if ((st = launch_verify_group(par_idx, j.files.data(), j.d_flags(), k, j.S, n, lo, hi, j.key, nullptr, j.s)))
+        return st;
+    j.sc->tmark(j.s);
+    return flags_to_host(*j.sc, j.d_flags() + (size_t)k * n, (size_t)j.m * n, flags.data() + (size_t)k * n, j.s);
+}
+
+// Rebuild the missing data of stripes [s0, s1) that share one valid-shard
+// pattern from the first k valid shards, read in place from the records, and
+// (verify_surplus) compare every other valid parity with its re-derived value
+// (erasure.rs:935-973).  With `gather` (gather form only), the present data
+// shards are copied to the output by the same pass (copy-through).
+int get_rebuild_run(RecJob& j, uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present, bool gather) {
+    const int k = j.k, t = j.t;
+    const uint64_t rec = j.rec, S = j.S, cnt = s1 - s0;
+    int valid = 0, missing_data = 0, e;
+    for (int i = 0; i < t; ++i) valid += present[i];
+    for (int i = 0; i < k; ++i) missing_data += present[i] ? 0 : 1;
+    const int run_status = valid < k ? RSG_ERR_TOO_FEW_SHARDS : RSG_OK;
+    for (uint64_t x = s0; x < s1; ++x) j.h_status[x] = run_status;
+    if (run_status != RSG_OK) return RSG_OK;
+    if (!missing_data) {
+        if (!gather) return RSG_OK;  // verified data already gathered / served in place
+        for (int i = 0; i < k; ++i)
+            if ((e = hip_status(hipMemcpy2DAsync(j.out.at(i, s0), j.out.stride(), j.files[i] + s0 * rec + 32, rec, S,
+                                                 cnt, hipMemcpyDeviceToDevice, j.s))))
+                return e;
+        return RSG_OK;
+    }
+    auto plan = j.cd->plan(present.data());
+    if (!plan) return RSG_ERR_TOO_FEW_SHARDS;
+    // survivors read in place from the records; base = first survivor, out =
+    // the first missing data shard's slot (every offset relative to them)
+    const uint8_t* base = j.files[plan->survivors[0]] + s0 * rec + 32;
+    int first_missing = 0;
+    while (present[first_missing]) ++first_missing;
+    uint8_t* out = j.out.at(first_missing, s0);
+    RowSet rs;
+    rs.C = k;
+    for (int sv : plan->survivors) rs.in_off.push_back(rel(j.files[sv] + s0 * rec + 32, base));
+    if (gather) {
+        rs.copy.assign(k, 0);
+        rs.copy_off.assign(k, 0);
+        for (int c = 0; c < k; ++c)
+            if (plan->survivors[c] < k) {
+                rs.copy[c] = 1;
+                rs.copy_off[c] = rel(j.out.at(plan->survivors[c], s0), out);
+            }
+    }
+    for (int i = 0; i < k; ++i) {
+        if (present[i]) continue;
+        rs.coef.resize((size_t)(rs.R + 1) * k);
+        plan_row(*j.cd, *plan, i, &rs.coef[(size_t)rs.R * k]);
+        rs.out_off.push_back(rel(j.out.at(i, s0), out));
+        ++rs.R;
+    }
+    // surplus parity must agree with the rebuilt data (erasure.rs:935-973)
+    RowSet vs;
+    vs.C = k;
+    vs.in_off = rs.in_off;
+    if (j.verify_surplus && valid > k) {
+        for (int p = k; p < t; ++p) {
+            if (!present[p] || is_survivor(*plan, p)) continue;  // a survivor re-derives to itself
+            vs.coef.resize((size_t)(vs.R + 1) * k);
+            plan_row(*j.cd, *plan, p, &vs.coef[(size_t)vs.R * k]);
+            vs.out_off.push_back(rel(j.files[p] + s0 * rec + 32, base));
+            ++vs.R;
+        }
+    }
+    if (vs.R) j.any_verify = true;
+    if (vs.R && rs.R + vs.R <= rsg::kMaxR && k <= rsg::kMaxC) {
+        // rebuild + check in one pass over the survivors
+        RowSet both = rs;
+        both.coef.insert(both.coef.end(), vs.coef.begin(), vs.coef.end());
+        for (uint64_t o : vs.out_off) both.out_off.push_back(rel(base + o, out));  // compare targets relative to `out`
+        both.R = rs.R + vs.R;
+        return apply_store_compare(both, rs.R, base, out, rec, j.out.stride(), rec, S, cnt, j.d_ok() + s0, j.s);
+    }
+    if ((e = apply_rows(rs, base, out, rec, j.out.stride(), S, cnt, rsg::GF_MODE_STORE, nullptr, j.s))) return e;
+    if (!vs.R) return RSG_OK;
+    return apply_rows(vs, base, const_cast<uint8_t*>(base), rec, rec, S, cnt, rsg::GF_MODE_COMPARE, j.d_ok() + s0,
+                      j.s);
+}
+
 // Launch k_decode_records_dma over all stripes for the erasure pattern
-// `present`: present files in ascending order, the first k are the
-// survivors (DecodePlan order); rows = the missing data shards, then (with
-// verify_surplus) the present non-survivor parity, compared in place.
-int launch_get_one_pass(Codec& cd, const std::vector<uint8_t>& present, const std::vector<int>& files,
-                        const uint8_t* const* d_files, uint8_t* d_flags, uint8_t* d_ok, int k, uint64_t shard_len,
-                        uint64_t n, const uint64_t* key, bool verify_surplus, uint8_t* d_out, bool& any_verify,
-                        hipStream_t s) {
-    const int t = (int)present.size();
-    auto plan = cd.plan(present.data());
+// present0: present files in ascending order, the first k are the survivors
+// (DecodePlan order); rows = the missing data shards (stored to the GET's
+// output), then (with verify_surplus) the present non-survivor parity,
+// compared in place.  The gather form also copies the present data through.
+int launch_get_one_pass(RecJob& j, const std::vector<int>& files) {
+    const int k = j.k;
+    auto plan = j.cd->plan(j.present0.data());
     if (!plan) return RSG_ERR_TOO_FEW_SHARDS;
     for (int c = 0; c < k; ++c)
         if (plan->survivors[c] != files[c]) return RSG_ERR_INVALID_ARG;  // survivors = first k present
     std::vector<uint8_t> coef;
     rsg::GfApplyParams p;
     std::memset(&p, 0, sizeof(p));
+    int first_missing = 0;
+    while (j.present0[first_missing]) ++first_missing;
+    p.out_base = j.out.at(first_missing, 0);
     int R = 0;
     for (int i = 0; i < k; ++i) {
-        if (present[i]) continue;
+        if (j.present0[i]) continue;
         coef.resize((size_t)(R + 1) * k);
-        plan_row(cd, *plan, i, &coef[(size_t)R * k]);
-        p.out_off[R++] = (uint64_t)i * shard_len;
+        plan_row(*j.cd, *plan, i, &coef[(size_t)R * k]);
+        p.out_off[R++] = rel(j.out.at(i, 0), p.out_base);
     }
     const int n_store = R;
-    if (verify_surplus) {
+    if (j.verify_surplus) {
         for (int f = k; f < (int)files.size(); ++f) {  // present non-survivors: parity, ascending
             if (R >= rsg::kMaxR) return RSG_ERR_UNSUPPORTED;
             coef.resize((size_t)(R + 1) * k);
-            plan_row(cd, *plan, files[f], &coef[(size_t)R * k]);
+            plan_row(*j.cd, *plan, files[f], &coef[(size_t)R * k]);
             ++R;
         }
     }
     if (R > 4 || R == 0) return RSG_ERR_UNSUPPORTED;
-    if (R > n_store) any_verify = true;
+    if (R > n_store) j.any_verify = true;
     for (int r = 0; r < R; ++r)
         for (int c = 0; c < k; ++c) coef_tables(coef[(size_t)r * k + c], p.tab[r][c]);
     p.C = (uint32_t)k;
     p.R = (uint32_t)R;
     p.n_store = (uint32_t)n_store;
     p.mode = rsg::GF_MODE_STORE_COMPARE;
-    p.out_base = d_out;
-    p.out_stripe_stride = (uint64_t)k * shard_len;
-    p.ok_flags = d_ok;
-    for (int c = 0; c < k; ++c)
-        if (files[c] < k) {
-            p.copy_mask |= 1u << c;
-            p.copy_off[c] = (uint64_t)files[c] * shard_len;
-        }
+    p.out_stripe_stride = j.out.stride();
+    p.ok_flags = j.d_ok();
+    if (!j.out.into())
+        for (int c = 0; c < k; ++c)
+            if (files[c] < k) {
+                p.copy_mask |= 1u << c;
+                p.copy_off[c] = rel(j.out.at(files[c], 0), p.out_base);
+            }
     rsg::HashParams h;
     std::memset(&h, 0, sizeof(h));
-    h.len = shard_len;
-    h.stripe_stride = 32 + shard_len;
-    std::memcpy(h.key, key, sizeof(h.key));
+    h.len = j.S;
+    h.stripe_stride = j.rec;
+    std::memcpy(h.key, j.key, sizeof(h.key));
     h.nbases = (uint32_t)files.size();
     h.digest_off = -32;
     for (size_t f = 0; f < files.size(); ++f) {
-        h.base[f] = d_files[files[f]] + 32;
-        h.flag_base[f] = d_flags + (size_t)files[f] * n;
+        h.base[f] = j.files[files[f]] + 32;
+        h.flag_base[f] = j.d_flags() + (size_t)files[f] * j.n;
     }
-    (void)t;
-    return hip_status(rsg::launch_decode_records_dma(p, h, k, (int)present.size() - k, (int)files.size(), shard_len,
-                                                     n, coef.data(), s));
+    return hip_status(rsg::launch_decode_records_dma(p, h, k, j.m, (int)files.size(), j.S, j.n, coef.data(), j.s));
+}
+
+// GET submit: the pass the call normally needs alone, then the verdict copy.
+//  - a data file missing (a lost disk, the common degraded case): every
+//    stripe misses the same data shards, so ONE optimistic pass over the
+//    present records rebuilds the missing data (gather form: and copies the
+//    present data through), checks the surplus parity and verifies every
+//    present record, as if all verify — k_decode_records_dma / _net where the
+//    geometry has a one-pass kernel, else a GF pass then a verify launch;
+//  - every data file present: one launch verifies the k data records (gather
+//    form: copying them to the output); the in-place form writes nothing;
+//  - anything else (no codec, too many rows for one pass): the general path,
+//    all of it in the finishing step.
+int get_begin(RecJob& j) {
+    const int k = j.k, m = j.m, t = j.t;
+    const uint64_t n = j.n;
+    int st;
+    if ((st = j.sc->ensure((size_t)(t + 1) * n, (size_t)(t + 1) * n))) return st;
+    if (m > 0 && !(j.cd = get_codec(k, m))) return RSG_ERR_INVALID_ARG;
+    j.present0.assign(t, 0);
+    int nfiles = 0, lost_data = 0;
+    std::vector<int> all_idx;
+    for (int i = 0; i < t; ++i) {
+        j.present0[i] = j.files[i] ? 1 : 0;
+        nfiles += j.present0[i];
+        if (j.files[i]) all_idx.push_back(i);
+        if (i < k && !j.files[i]) ++lost_data;
+    }
+    const int surplus = std::max(0, nfiles - k);  // present shards beyond the k survivors
+    const bool fast = m > 0 && lost_data > 0 && nfiles >= k && k <= rsg::kMaxC &&
+                      lost_data + (j.verify_surplus ? surplus : 0) <= rsg::kMaxR && lost_disk_fast_enabled();
+    if (fast) {
+        j.phase = RecJob::FAST;
+        bool one_pass = get_dma_enabled(j.ctx, n) && rsg::decode_dma_supported(k, m, nfiles, j.S) && j.rec % 16 == 0;
+        for (int i : all_idx) one_pass = one_pass && (uintptr_t)(j.files[i] + 32) % 16 == 0;
+        if (j.out.into()) {  // the kernels' 8-byte row stores
+            one_pass = one_pass && j.out.tstride % 8 == 0;
+            for (int i = 0; i < k; ++i) one_pass = one_pass && (j.present0[i] || (uintptr_t)j.out.tg[i] % 8 == 0);
+        }
+        j.one_pass = one_pass;
+        if (one_pass) {
+            // verify every present record, rebuild (and gather) and check
+            // the surplus parity in ONE pass; the kernel writes every present
+            // file's flags and, with surplus rows, every stripe's verdict
+            // whole (no memsets before it)
+            j.sc->tmark(j.s);
+            if ((st = launch_get_one_pass(j, all_idx))) return st;
+            j.sc->tmark(j.s);
+            if (!j.any_verify && (st = hip_status(hipMemsetAsync(j.d_ok(), 1, n, j.s)))) return st;
+            for (uint64_t x = 0; x < n; ++x) j.h_status[x] = RSG_OK;
+        } else {
+            if ((st = hip_status(hipMemsetAsync(j.d_ok(), 1, n, j.s)))) return st;
+            j.sc->tmark(j.s);
+            if ((st = get_rebuild_run(j, 0, n, j.present0, !j.out.into()))) return st;
+            j.sc->tmark(j.s);
+            if ((st = hip_status(hipMemsetAsync(j.d_flags(), 0, (size_t)t * n, j.s)))) return st;
+            j.sc->tmark(j.s);
+            if ((st = launch_verify_group(all_idx, j.files.data(), j.d_flags(), k, j.S, n, 0, n, j.key, nullptr, j.s)))
+                return st;
+            j.sc->tmark(j.s);
+        }
+        // the verified map and the surplus verdict (adjacent in scratch) in one copy
+        return hip_status(hipMemcpyAsync(j.sc->h, j.d_flags(), (size_t)(t + 1) * n, hipMemcpyDeviceToHost, j.s));
+    }
+    if (lost_data == 0) {
+        j.phase = RecJob::DATA_VERIFIED;
+        if ((st = hip_status(hipMemsetAsync(j.d_ok(), 1, n, j.s)))) return st;
+        return verify_data_begin(j, j.out.into() ? nullptr : j.out.d_out);
+    }
+    j.phase = RecJob::GENERAL;
+    return RSG_OK;
+}
+
+int get_finish(RecJob& j) {
+    const int k = j.k, t = j.t;
+    const uint64_t n = j.n;
+    const bool gather = !j.out.into();
+    std::vector<uint8_t> flags;
+    const uint8_t* fmap = nullptr;  // the final verified map [shard][stripe]
+    bool queued = false;             // work queued here: drain before returning
+    int st;
+    if (j.phase == RecJob::FAST) {
+        uint8_t* hf = j.sc->h;
+        if (j.one_pass)  // absent files' rows were never written on the device
+            for (int i = 0; i < t; ++i)
+                if (!j.files[i]) std::memset(hf + (size_t)i * n, 0, n);
+        bool redone = false;
+        if (!flags_match_pattern(hf, j.present0, n)) {
+            flags.assign(hf, hf + (size_t)t * n);
+            st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) {
+                if (present == j.present0) return (int)RSG_OK;  // the optimistic pass was right
+                redone = true;
+                int e = hip_status(hipMemsetAsync(j.d_ok() + s0, 1, s1 - s0, j.s));
+                return e ? e : get_rebuild_run(j, s0, s1, present, gather);
+            });
+            if (st) return st;
+        }
+        if (!redone) {
+            if (j.any_verify)
+                for (uint64_t x = 0; x < n; ++x)
+                    if (j.h_status[x] == RSG_OK && !hf[(size_t)t * n + x]) j.h_status[x] = RSG_ERR_INCONSISTENT_SOURCES;
+            if (j.h_src)
+                for (int i = 0; i < k; ++i) std::memcpy(j.h_src + (size_t)i * n, hf + (size_t)i * n, n);
+            j.collect_time();
+            return RSG_OK;  // nothing queued after the ticket's event
+        }
+        fmap = flags.data();
+        queued = true;
+    } else {
+        if (j.phase == RecJob::DATA_VERIFIED) {
+            if (!std::memchr(j.sc->h, 0, (size_t)k * n)) {  // every data record verified: nothing to rebuild
+                for (uint64_t x = 0; x < n; ++x) j.h_status[x] = RSG_OK;
+                if (j.h_src) std::memset(j.h_src, 1, (size_t)k * n);
+                j.collect_time();
+                return RSG_OK;
+            }
+            if ((st = verify_parity_rest(j, flags))) return st;
+        } else {
+            if ((st = hip_status(hipMemsetAsync(j.d_ok(), 1, n, j.s)))) return st;
+            if ((st = verify_all(j, gather ? j.out.d_out : nullptr, flags))) return st;
+        }
+        st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) {
+            return get_rebuild_run(j, s0, s1, present, false);
+        });
+        if (st) return st;
+        fmap = flags.data();
+        queued = true;
+    }
+    if (j.any_verify) {
+        std::vector<uint8_t> ok(n, 1);
+        if ((st = flags_to_host(*j.sc, j.d_ok(), n, ok.data(), j.s))) return st;
+        for (uint64_t x = 0; x < n; ++x)
+            if (j.h_status[x] == RSG_OK && !ok[x]) j.h_status[x] = RSG_ERR_INCONSISTENT_SOURCES;
+    } else if (queued && (st = j.drain())) {
+        return st;
+    }
+    if (j.h_src)
+        for (int i = 0; i < k; ++i) std::memcpy(j.h_src + (size_t)i * n, fmap + (size_t)i * n, n);
+    j.collect_time();
+    return RSG_OK;
 }
 
 // Launch the one-pass heal (k_decode_records_dma with target hashing) for
-// the pattern `present`: survivors = the first k present files; rows = every
+// the pattern present0: survivors = the first k present files; rows = every
 // target (absent from the sources), then the present non-survivor parity,
 // compared in place (heal.rs:180-196).
-int launch_heal_one_pass(Codec& cd, const std::vector<uint8_t>& present, const std::vector<int>& files,
-                         const std::vector<int>& targets, const uint8_t* const* d_files, uint8_t* const* d_targets,
-                         uint8_t* d_flags, uint8_t* d_ok, int k, uint64_t shard_len, uint64_t n, const uint64_t* key,
-                         bool& any_verify, hipStream_t s) {
-    auto plan = cd.plan(present.data());
+int launch_heal_one_pass(RecJob& j, const std::vector<int>& files, const std::vector<int>& targets) {
+    const int k = j.k;
+    auto plan = j.cd->plan(j.present0.data());
     if (!plan) return RSG_ERR_TOO_FEW_SHARDS;
     for (int c = 0; c < k; ++c)
         if (plan->survivors[c] != files[c]) return RSG_ERR_INVALID_ARG;
-    const uint64_t rec = 32 + shard_len;
     rsg::GfApplyParams p;
     std::memset(&p, 0, sizeof(p));
     std::vector<uint8_t> coef;
     int R = 0;
-    p.out_base = d_targets[targets[0]] + 32;
+    p.out_base = j.targets[targets[0]] + 32;
     for (int i : targets) {
         coef.resize((size_t)(R + 1) * k);
-        plan_row(cd, *plan, i, &coef[(size_t)R * k]);
-        p.out_off[R++] = (uint64_t)(uintptr_t)(d_targets[i] + 32) - (uint64_t)(uintptr_t)p.out_base;
+        plan_row(*j.cd, *plan, i, &coef[(size_t)R * k]);
+        p.out_off[R++] = rel(j.targets[i] + 32, p.out_base);
     }
     const int n_store = R;
     for (int f = k; f < (int)files.size(); ++f) {  // present non-survivors: parity, ascending
         if (R >= 4) return RSG_ERR_UNSUPPORTED;
         coef.resize((size_t)(R + 1) * k);
-        plan_row(cd, *plan, files[f], &coef[(size_t)R * k]);
+        plan_row(*j.cd, *plan, files[f], &coef[(size_t)R * k]);
         ++R;
     }
-    if (R > n_store) any_verify = true;
+    if (R > n_store) j.any_verify = true;
     for (int r = 0; r < R; ++r)
         for (int c = 0; c < k; ++c) coef_tables(coef[(size_t)r * k + c], p.tab[r][c]);
     p.C = (uint32_t)k;
     p.R = (uint32_t)R;
     p.n_store = (uint32_t)n_store;
     p.mode = rsg::GF_MODE_STORE_COMPARE;
-    p.out_stripe_stride = rec;
-    p.ok_flags = d_ok;
+    p.out_stripe_stride = j.rec;
+    p.ok_flags = j.d_ok();
     rsg::HashParams h;
     std::memset(&h, 0, sizeof(h));
-    h.len = shard_len;
-    h.stripe_stride = rec;
-    std::memcpy(h.key, key, sizeof(h.key));
+    h.len = j.S;
+    h.stripe_stride = j.rec;
+    std::memcpy(h.key, j.key, sizeof(h.key));
     h.nbases = (uint32_t)files.size();
     h.digest_off = -32;
     for (size_t f = 0; f < files.size(); ++f) {
-        h.base[f] = d_files[files[f]] + 32;
-        h.flag_base[f] = d_flags + (size_t)files[f] * n;
+        h.base[f] = j.files[files[f]] + 32;
+        h.flag_base[f] = j.d_flags() + (size_t)files[f] * j.n;
     }
-    const hipError_t e = rsg::launch_heal_records_dma(p, h, k, (int)present.size() - k, (int)files.size(),
-                                                      (int)targets.size(), shard_len, n, coef.data(), s);
+    const hipError_t e = rsg::launch_heal_records_dma(p, h, k, j.m, (int)files.size(), (int)targets.size(), j.S,
+                                                      j.n, coef.data(), j.s);
     return e == hipErrorNotSupported ? RSG_ERR_UNSUPPORTED : hip_status(e);  // unsupported: nothing launched
 }
 
-// GET engine body (ctx->mu held): verify records, copy/rebuild the k data
-// shards of every stripe into d_out (n x k*S), optional surplus-parity check.
-// Uses ctx->d_scratch[0, (t+1)*n).  `flags` returns the verified-shard map.
-int decode_records_locked(rsg_ctx* ctx, int k, int m, uint64_t shard_len, uint64_t n, const uint8_t* const* d_files,
-                          const uint64_t* key, bool verify_surplus, uint8_t* d_out, int* h_status, hipStream_t s) {
-    const int t = k + m;
-    const uint64_t rec = 32 + shard_len;  // BitrotWriter record: [hash][block]
-    const uint64_t ks = (uint64_t)k * shard_len;
-    int st;
-    if ((st = ctx->ensure_scratch((size_t)(t + 1) * n))) return st;
-    uint8_t* d_ok = ctx->d_scratch + (size_t)t * n;  // surplus-parity verdict per stripe
-    auto cd = m > 0 ? get_codec(k, m) : nullptr;
-    if (m > 0 && !cd) return RSG_ERR_INVALID_ARG;
-    bool any_verify = false;
-    // Rebuild the missing data of stripes [s0, s1) that share one valid-shard
-    // pattern from the first k valid shards, read in place from the records,
-    // and (verify_surplus) compare every other valid parity with its
-    // re-derived value (erasure.rs:935-973).  With `gather`, the present data
-    // shards are copied into d_out by the same pass (copy-through).
-    auto rebuild_run = [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present, bool gather) -> int {
-        const uint64_t cnt = s1 - s0;
-        int valid = 0, missing_data = 0, e;
-        for (int i = 0; i < t; ++i) valid += present[i];
-        for (int i = 0; i < k; ++i) missing_data += present[i] ? 0 : 1;
-        const int run_status = valid < k ? RSG_ERR_TOO_FEW_SHARDS : RSG_OK;
-        for (uint64_t x = s0; x < s1; ++x) h_status[x] = run_status;
-        if (run_status != RSG_OK) return RSG_OK;
-        uint8_t* out = d_out + s0 * ks;
-        if (!missing_data) {
-            if (!gather) return RSG_OK;  // verified data already gathered here
-            for (int i = 0; i < k; ++i)
-                if ((e = hip_status(hipMemcpy2DAsync(out + (uint64_t)i * shard_len, ks, d_files[i] + s0 * rec + 32, rec,
-                                                     shard_len, cnt, hipMemcpyDeviceToDevice, s))))
-                    return e;
-            return RSG_OK;
-        }
-        auto plan = cd->plan(present.data());
-        if (!plan) return RSG_ERR_TOO_FEW_SHARDS;
-        // survivors read in place from the records; base = first survivor
-        const uint8_t* base = d_files[plan->survivors[0]] + s0 * rec + 32;
-        RowSet rs;
-        rs.C = k;
-        for (int sv : plan->survivors)
-            rs.in_off.push_back((uint64_t)(uintptr_t)(d_files[sv] + s0 * rec + 32) - (uint64_t)(uintptr_t)base);
-        if (gather) {
-            rs.copy.assign(k, 0);
-            rs.copy_off.assign(k, 0);
-            for (int c = 0; c < k; ++c)
-                if (plan->survivors[c] < k) {
-                    rs.copy[c] = 1;
-                    rs.copy_off[c] = (uint64_t)plan->survivors[c] * shard_len;
-                }
-        }
-        for (int i = 0; i < k; ++i) {
-            if (present[i]) continue;
-            rs.coef.resize((size_t)(rs.R + 1) * k);
-            plan_row(*cd, *plan, i, &rs.coef[(size_t)rs.R * k]);
-            rs.out_off.push_back((uint64_t)i * shard_len);
-            ++rs.R;
-        }
-        // surplus parity must agree with the rebuilt data (erasure.rs:935-973)
-        RowSet vs;
-        vs.C = k;
-        vs.in_off = rs.in_off;
-        if (verify_surplus && valid > k) {
-            for (int p = k; p < t; ++p) {
-                if (!present[p] || is_survivor(*plan, p)) continue;  // a survivor re-derives to itself
-                vs.coef.resize((size_t)(vs.R + 1) * k);
-                plan_row(*cd, *plan, p, &vs.coef[(size_t)vs.R * k]);
-                vs.out_off.push_back((uint64_t)(uintptr_t)(d_files[p] + s0 * rec + 32) - (uint64_t)(uintptr_t)base);
-                ++vs.R;
-            }
-        }
-        if (vs.R) any_verify = true;
-        if (vs.R && rs.R + vs.R <= rsg::kMaxR && k <= rsg::kMaxC) {
-            // rebuild + check in one pass over the survivors
-            RowSet both = rs;
-            both.coef.insert(both.coef.end(), vs.coef.begin(), vs.coef.end());
-            for (uint64_t o : vs.out_off)  // compare targets relative to `out`
-                both.out_off.push_back(o + (uint64_t)(uintptr_t)base - (uint64_t)(uintptr_t)out);
-            both.R = rs.R + vs.R;
-            return apply_store_compare(both, rs.R, base, out, rec, ks, rec, shard_len, cnt, d_ok + s0, s);
-        }
-        if ((e = apply_rows(rs, base, out, rec, ks, shard_len, cnt, rsg::GF_MODE_STORE, nullptr, s))) return e;
-        if (!vs.R) return RSG_OK;
-        return apply_rows(vs, base, const_cast<uint8_t*>(base), rec, rec, shard_len, cnt, rsg::GF_MODE_COMPARE,
-                          d_ok + s0, s);
-    };
-
-    std::vector<uint8_t> present0(t), flags;
-    int nfiles = 0, lost_data = 0;
+// Per run of stripes with one verified pattern, ONE pass over the survivors
+// (first k verified shards) writes every target's record body — data rebuilt
+// or, if verified, reproduced (identity row), parity re-encoded — and
+// compares every verified source parity that is not a survivor with its
+// re-encoded value: "inconsistent heal source shards" (heal.rs:180-196; a
+// survivor parity re-encodes to itself).
+int heal_run(RecJob& j, uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) {
+    const int k = j.k, t = j.t;
+    const uint64_t rec = j.rec;
+    int valid = 0;
+    for (int i = 0; i < t; ++i) valid += present[i];
+    for (uint64_t x = s0; x < s1; ++x) j.h_status[x] = valid < k ? RSG_ERR_TOO_FEW_SHARDS : RSG_OK;
+    if (valid < k) return RSG_OK;
+    auto plan = j.cd->plan(present.data());
+    if (!plan) return RSG_ERR_TOO_FEW_SHARDS;
+    const uint8_t* base = j.files[plan->survivors[0]] + s0 * rec + 32;
+    auto off = [&](const uint8_t* p) { return rel(p + s0 * rec + 32, base); };
+    RowSet ps, vs;  // target bodies (store), non-survivor verified parity (compare)
+    ps.C = vs.C = k;
+    for (int sv : plan->survivors) ps.in_off.push_back(off(j.files[sv]));
+    vs.in_off = ps.in_off;
     for (int i = 0; i < t; ++i) {
-        present0[i] = d_files[i] ? 1 : 0;
-        nfiles += present0[i];
-        if (i < k && !d_files[i]) ++lost_data;
-    }
-    const int surplus = std::max(0, nfiles - k);  // present shards beyond the k survivors
-    const bool fast = m > 0 && lost_data > 0 && nfiles >= k && k <= rsg::kMaxC &&
-                      lost_data + (verify_surplus ? surplus : 0) <= rsg::kMaxR && lost_disk_fast_enabled();
-    if (fast) {
-        // Lost disk(s): every stripe misses the same data shards, so one
-        // optimistic sweep over the present records rebuilds the missing data,
-        // gathers the present data (copy-through) and checks surplus parity,
-        // as if every present record verifies; then every present record is
-        // verified (read-only).  Stripes where a record fails are redone from
-        // their actual valid shards.  Survivors are read twice (rebuild, then
-        // verify) instead of three times by the general path.
-        uint8_t* d_flags = ctx->d_scratch;
-        std::vector<int> all_idx;
-        for (int i = 0; i < t; ++i)
-            if (d_files[i]) all_idx.push_back(i);
-        bool one_pass = get_dma_enabled(ctx, n) && rsg::decode_dma_supported(k, m, nfiles, shard_len) &&
-                        rec % 16 == 0;
-        for (int i : all_idx) one_pass = one_pass && (uintptr_t)(d_files[i] + 32) % 16 == 0;
-        if (one_pass) {
-            // RS(8,4): verify every present record, rebuild, gather and check
-            // the surplus parity in ONE pass (k_decode_records_dma); the kernel
-            // writes every present file's flags and, with surplus rows, every
-            // stripe's verdict whole (no memsets before it)
-            ctx->tmark(s);
-            if ((st = launch_get_one_pass(*cd, present0, all_idx, d_files, d_flags, d_ok, k, shard_len, n, key,
-                                          verify_surplus, d_out, any_verify, s)))
-                return st;
-            ctx->tmark(s);
-            if (!any_verify && (st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
-            for (uint64_t x = 0; x < n; ++x) h_status[x] = RSG_OK;
-        } else {
-            if ((st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
-            ctx->tmark(s);
-            if ((st = rebuild_run(0, n, present0, true))) return st;
-            ctx->tmark(s);
-            if ((st = hip_status(hipMemsetAsync(d_flags, 0, (size_t)t * n, s)))) return st;
-            ctx->tmark(s);
-            if ((st = launch_verify_group(all_idx, d_files, d_flags, k, shard_len, n, 0, n, key, nullptr, s)))
-                return st;
-            ctx->tmark(s);
+        if (j.targets[i]) {
+            ps.coef.resize((size_t)(ps.R + 1) * k);
+            plan_row(*j.cd, *plan, i, &ps.coef[(size_t)ps.R * k]);
+            ps.out_off.push_back(off(j.targets[i]));
+            ++ps.R;
         }
-        // the verified map and the surplus verdict (adjacent in scratch) in one
-        // copy and one synchronisation; a second one only if a run is redone
-        if ((st = ctx->ensure_host_flags((size_t)(t + 1) * n))) return st;
-        if ((st = hip_status(hipMemcpyAsync(ctx->h_flags, d_flags, (size_t)(t + 1) * n, hipMemcpyDeviceToHost, s))))
+        if (i >= k && present[i] && !is_survivor(*plan, i)) {
+            vs.coef.resize((size_t)(vs.R + 1) * k);
+            plan_row(*j.cd, *plan, i, &vs.coef[(size_t)vs.R * k]);
+            vs.out_off.push_back(off(j.files[i]));
+            ++vs.R;
+        }
+    }
+    if (vs.R) j.any_verify = true;
+    uint8_t* ob = const_cast<uint8_t*>(base);
+    if (ps.R + vs.R <= rsg::kMaxR && k <= rsg::kMaxC) {
+        RowSet both = ps;
+        both.coef.insert(both.coef.end(), vs.coef.begin(), vs.coef.end());
+        both.out_off.insert(both.out_off.end(), vs.out_off.begin(), vs.out_off.end());
+        both.R = ps.R + vs.R;
+        return apply_store_compare(both, ps.R, base, ob, rec, rec, rec, j.S, s1 - s0, j.d_ok() + s0, j.s);
+    }
+    int e = apply_rows(ps, base, ob, rec, rec, j.S, s1 - s0, rsg::GF_MODE_STORE, nullptr, j.s);
+    if (e || !vs.R) return e;
+    return apply_rows(vs, base, ob, rec, rec, j.S, s1 - s0, rsg::GF_MODE_COMPARE, j.d_ok() + s0, j.s);
+}
+
+// the target records of stripes [s0, s1) get their HH256S headers
+int heal_hash_targets(RecJob& j, uint64_t s0, uint64_t s1) {
+    std::vector<uint8_t*> tg(j.t, nullptr);
+    for (int i = 0; i < j.t; ++i)
+        if (j.targets[i]) tg[i] = j.targets[i] + s0 * j.rec;
+    return hash_records_inplace(tg.data(), j.t, j.S, s1 - s0, j.key, j.s);
+}
+
+// Heal submit.  Optimistic (replaced disks, sound sources — the common heal):
+// one pass writes every target record (body + digest), verifies every source
+// record and compares the surplus parity (RS(8,4)/(16,4) networks and the
+// k <= 8 table kernel), or a GF pass then one hash launch that verifies the
+// sources and writes the targets' digests; then the verified map and the
+// parity verdict go back in one copy.  Anything else: the general path, all
+// of it in the finishing step.
+int heal_begin(RecJob& j) {
+    const int k = j.k, m = j.m, t = j.t;
+    const uint64_t n = j.n;
+    int st;
+    if ((st = j.sc->ensure((size_t)(t + 1) * n, (size_t)(t + 1) * n))) return st;
+    if (!(j.cd = get_codec(k, m))) return RSG_ERR_INVALID_ARG;
+    j.present0.assign(t, 0);
+    int valid0 = 0;
+    std::vector<int> all_idx, tg_idx;
+    for (int i = 0; i < t; ++i) {
+        valid0 += (j.present0[i] = j.files[i] ? 1 : 0);
+        if (j.files[i]) all_idx.push_back(i);
+        if (j.targets[i]) tg_idx.push_back(i);
+    }
+    if (valid0 < k || !lost_disk_fast_enabled()) {
+        j.phase = RecJob::GENERAL;
+        return RSG_OK;
+    }
+    j.phase = RecJob::FAST;
+    bool one_pass = get_dma_enabled(j.ctx, n) &&
+                    rsg::heal_one_pass_shape(k, m, (int)all_idx.size(), (int)tg_idx.size(), j.S) && j.rec % 16 == 0;
+    for (int i : all_idx) one_pass = one_pass && (uintptr_t)(j.files[i] + 32) % 16 == 0;
+    for (int i : tg_idx) one_pass = one_pass && !j.files[i] && (uintptr_t)(j.targets[i] + 32) % 8 == 0;
+    if (one_pass) {
+        j.sc->tmark(j.s);
+        st = launch_heal_one_pass(j, all_idx, tg_idx);
+        if (st == RSG_ERR_UNSUPPORTED) {  // RS(16,4) pattern without a network: the two-pass path
+            j.sc->tunmark();
+            one_pass = false;
+            j.any_verify = false;
+        } else if (st) {
             return st;
-        if ((st = hip_status(hipStreamSynchronize(s)))) return st;
-        if (one_pass)  // absent files' rows were never written on the device
+        } else {
+            j.sc->tmark(j.s);
+            if (!j.any_verify && (st = hip_status(hipMemsetAsync(j.d_ok(), 1, n, j.s)))) return st;
+            for (uint64_t x = 0; x < n; ++x) j.h_status[x] = RSG_OK;
+        }
+    }
+    j.one_pass = one_pass;
+    if (!one_pass) {
+        if ((st = hip_status(hipMemsetAsync(j.d_ok(), 1, n, j.s)))) return st;
+        j.sc->tmark(j.s);
+        if ((st = heal_run(j, 0, n, j.present0))) return st;
+        j.sc->tmark(j.s);
+        if ((st = hip_status(hipMemsetAsync(j.d_flags(), 0, (size_t)t * n, j.s)))) return st;
+        j.sc->tmark(j.s);
+        if ((st = launch_verify_and_digest(all_idx, j.files.data(), j.d_flags(), j.targets.data(), t, j.S, n, j.key,
+                                           j.s)))
+            return st;
+        j.sc->tmark(j.s);
+    }
+    return hip_status(hipMemcpyAsync(j.sc->h, j.d_flags(), (size_t)(t + 1) * n, hipMemcpyDeviceToHost, j.s));
+}
+
+int heal_finish(RecJob& j) {
+    const int t = j.t;
+    const uint64_t n = j.n, rec = j.rec;
+    bool queued = false;
+    int st;
+    std::vector<uint8_t> flags, ok(n, 1);
+    if (j.phase == RecJob::FAST) {
+        uint8_t* hf = j.sc->h;
+        if (j.one_pass)  // absent files' rows were never written on the device
             for (int i = 0; i < t; ++i)
-                if (!d_files[i]) std::memset(ctx->h_flags + (size_t)i * n, 0, n);
+                if (!j.files[i]) std::memset(hf + (size_t)i * n, 0, n);
+        std::memcpy(ok.data(), hf + (size_t)t * n, n);
         bool redone = false;
-        if (!flags_match_pattern(ctx->h_flags, present0, n)) {
-            flags.assign(ctx->h_flags, ctx->h_flags + (size_t)t * n);
-            st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) -> int {
-                if (present == present0) return RSG_OK;  // the optimistic pass was right
+        if (!flags_match_pattern(hf, j.present0, n)) {
+            flags.assign(hf, hf + (size_t)t * n);
+            st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) {
+                if (present == j.present0) return (int)RSG_OK;
                 redone = true;
-                int e = hip_status(hipMemsetAsync(d_ok + s0, 1, s1 - s0, s));
-                return e ? e : rebuild_run(s0, s1, present, true);
+                int e = hip_status(hipMemsetAsync(j.d_ok() + s0, 1, s1 - s0, j.s));
+                if (!e) e = heal_run(j, s0, s1, present);
+                return e ? e : heal_hash_targets(j, s0, s1);
             });
             if (st) return st;
         }
-        if (!redone) {
-            if (any_verify)
-                for (uint64_t x = 0; x < n; ++x)
-                    if (h_status[x] == RSG_OK && !ctx->h_flags[(size_t)t * n + x])
-                        h_status[x] = RSG_ERR_INCONSISTENT_SOURCES;
-            return RSG_OK;  // the stream was synchronised after the last launch
+        if (redone) {
+            queued = true;
+            if (j.any_verify && (st = flags_to_host(*j.sc, j.d_ok(), n, ok.data(), j.s))) return st;
         }
     } else {
-        // verify the data records and gather them into d_out; parity where needed
-        if ((st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
-        if ((st = verify_gather(ctx, k, m, shard_len, n, d_files, key, d_out, false, flags, s))) return st;
-        st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) {
-            return rebuild_run(s0, s1, present, false);
-        });
-        if (st) return st;
+        // verify every source record first (read quorum: k verified shards
+        // per stripe), then the per-pattern GF passes, then the digests
+        if ((st = hip_status(hipMemsetAsync(j.d_ok(), 1, n, j.s)))) return st;
+        if ((st = verify_all(j, nullptr, flags))) return st;
+        if ((st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& p) {
+                 return heal_run(j, s0, s1, p);
+             })))
+            return st;
+        if ((st = heal_hash_targets(j, 0, n))) return st;
+        queued = true;
+        if (j.any_verify && (st = flags_to_host(*j.sc, j.d_ok(), n, ok.data(), j.s))) return st;
     }
-    if (any_verify) {
-        if ((st = ctx->ensure_host_flags(n))) return st;
-        if ((st = hip_status(hipMemcpyAsync(ctx->h_flags, d_ok, n, hipMemcpyDeviceToHost, s)))) return st;
-        if ((st = hip_status(hipStreamSynchronize(s)))) return st;
+    if (j.any_verify)
         for (uint64_t x = 0; x < n; ++x)
-            if (h_status[x] == RSG_OK && !ctx->h_flags[x]) h_status[x] = RSG_ERR_INCONSISTENT_SOURCES;
+            if (j.h_status[x] == RSG_OK && !ok[x]) j.h_status[x] = RSG_ERR_INCONSISTENT_SOURCES;
+    // A failed stripe's target records hold unverified bytes: their digest
+    // headers are zeroed so they can never pass bitrot verification even if a
+    // caller ignores h_status (the reference writes nothing for a failed heal).
+    for (uint64_t s0 = 0; s0 < n;) {
+        if (j.h_status[s0] == RSG_OK) {
+            ++s0;
+            continue;
+        }
+        uint64_t s1 = s0 + 1;
+        while (s1 < n && j.h_status[s1] != RSG_OK) ++s1;
+        for (int i = 0; i < t; ++i)
+            if (j.targets[i] && (st = hip_status(hipMemset2DAsync(j.targets[i] + s0 * rec, rec, 0, 32, s1 - s0, j.s))))
+                return st;
+        queued = true;
+        s0 = s1;
     }
-    return hip_status(hipStreamSynchronize(s));
+    if (queued && (st = j.drain())) return st;
+    j.collect_time();
+    return RSG_OK;
+}
+
+// Register a record job: its event follows the submit's work on the stream;
+// the first wait / poll that sees it runs the finishing step.  On a submit
+// error nothing of the job stays in flight and no ticket is issued.
+int submit_record_job(rsg_ctx* ctx, std::shared_ptr<RecJob> rj, int (*begin)(RecJob&), int (*finish)(RecJob&),
+                      uint64_t* ticket) {
+    auto job = std::make_shared<rsg_ctx::Job>();
+    int st = begin(*rj);
+    hipEvent_t e = nullptr;
+    if (!st) st = hip_status(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (e) job->done.push_back(e);
+    if (!st) st = hip_status(hipEventRecord(e, rj->s));
+    if (st) {
+        (void)hipStreamSynchronize(rj->s);  // the job's queued work reads its scratch
+        return st;                          // rj (and its scratch) released here
+    }
+    job->finish = [rj, finish](int ev) -> int {
+        int r = ev ? ev : finish(*rj);
+        if (r) (void)hipStreamSynchronize(rj->s);  // nothing of the job outlives its scratch
+        rj->sc->tev_used = 0;
+        return r;
+    };
+    std::lock_guard<std::mutex> g(ctx->pipe_mu);
+    *ticket = ctx->next_ticket++;
+    ctx->jobs.emplace(*ticket, std::move(job));
+    return RSG_OK;
+}
+
+// A ticket with nothing to wait for (empty batch).
+uint64_t done_ticket(rsg_ctx* ctx) {
+    std::lock_guard<std::mutex> g(ctx->pipe_mu);
+    const uint64_t t = ctx->next_ticket++;
+    ctx->jobs.emplace(t, std::make_shared<rsg_ctx::Job>());
+    return t;
+}
+
+// Byte ranges [a, a+la) and [b, b+lb) intersect.
+bool spans_overlap(const uint8_t* a, uint64_t la, const uint8_t* b, uint64_t lb) {
+    return (uintptr_t)a < (uintptr_t)b + lb && (uintptr_t)b < (uintptr_t)a + la;
 }
 
 }  // namespace
 
 extern "C" {
 
-int rsg_decode_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n, const uint8_t* const* d_files,
-                           int algo, int verify_surplus, uint8_t* d_out, int* h_status, void* stream) {
+int rsg_decode_records_submit(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n, const uint8_t* const* d_files,
+                              int algo, int verify_surplus, uint8_t* d_out, uint8_t* const* d_targets,
+                              size_t target_stride, uint8_t* h_src, int* h_status, void* stream, uint64_t* ticket) {
     int st = enter(ctx);
     if (st) return st;
+    if (!ticket) return RSG_ERR_INVALID_ARG;
+    *ticket = 0;
     if ((st = check_geometry(k, m))) return st;
-    if (!d_files || (n && (!d_out || !h_status))) return RSG_ERR_INVALID_ARG;
+    if (!d_files || (d_out && d_targets)) return RSG_ERR_INVALID_ARG;  // one output form
+    if (n && (!h_status || (!d_out && !d_targets))) return RSG_ERR_INVALID_ARG;
     const uint64_t* key = hash_key(algo);
     if (!key) return RSG_ERR_INVALID_ARG;
+    const uint64_t rec = 32 + (uint64_t)shard_len;
+    if (d_targets) {
+        // in-place form: a slot per data shard (reconstruct_into's shards
+        // slice); a slot range overlapping a source record file would be
+        // written while it is read
+        if (target_stride < shard_len) return RSG_ERR_INVALID_ARG;
+        const uint64_t span = n ? (uint64_t)(n - 1) * target_stride + shard_len : 0;
+        for (int i = 0; i < k; ++i) {
+            if (!d_targets[i]) return RSG_ERR_INVALID_ARG;
+            for (int f = 0; f < k + m && span; ++f)
+                if (d_files[f] && spans_overlap(d_targets[i], span, d_files[f], (uint64_t)n * rec))
+                    return RSG_ERR_INVALID_ARG;
+        }
+    }
     if (n == 0 || shard_len == 0) {
         for (size_t s = 0; s < n; ++s) h_status[s] = RSG_OK;
+        if (h_src) std::memset(h_src, 1, (size_t)k * n);
+        *ticket = done_ticket(ctx);
         return RSG_OK;
     }
-    hipStream_t s = pick_stream(ctx, stream);
-    std::lock_guard<std::mutex> g(ctx->mu);
-    ctx->tev_used = 0;
-    st = decode_records_locked(ctx, k, m, shard_len, n, d_files, key, verify_surplus != 0, d_out, h_status, s);
-    if (!st) ctx->tcollect();  // every path returns with the stream synchronised
-    return st;
+    auto rj = std::make_shared<RecJob>();
+    rj->ctx = ctx;
+    rj->k = k;
+    rj->m = m;
+    rj->t = k + m;
+    rj->S = shard_len;
+    rj->n = n;
+    rj->rec = rec;
+    rj->key = key;
+    rj->verify_surplus = verify_surplus != 0;
+    rj->files.assign(d_files, d_files + k + m);
+    rj->out.S = shard_len;
+    rj->out.ks = (uint64_t)k * shard_len;
+    if (d_targets) {
+        rj->out.tg.assign(d_targets, d_targets + k);
+        rj->out.tstride = target_stride;
+    } else {
+        rj->out.d_out = d_out;
+    }
+    rj->h_status = h_status;
+    rj->h_src = h_src;
+    rj->s = pick_stream(ctx, stream);
+    rj->sc = ctx->take_scratch();
+    return submit_record_job(ctx, std::move(rj), get_begin, get_finish, ticket);
+}
+
+int rsg_decode_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n, const uint8_t* const* d_files,
+                           int algo, int verify_surplus, uint8_t* d_out, int* h_status, void* stream) {
+    if (!d_out && n) return RSG_ERR_INVALID_ARG;
+    uint64_t t = 0;
+    int st = rsg_decode_records_submit(ctx, k, m, shard_len, n, d_files, algo, verify_surplus, d_out, nullptr, 0,
+                                       nullptr, h_status, stream, &t);
+    return st ? st : rsg_wait(ctx, t);
+}
+
+int rsg_decode_records_into_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
+                                const uint8_t* const* d_files, int algo, int verify_surplus,
+                                uint8_t* const* d_targets, size_t target_stride, uint8_t* h_src, int* h_status,
+                                void* stream) {
+    uint64_t t = 0;
+    int st = rsg_decode_records_submit(ctx, k, m, shard_len, n, d_files, algo, verify_surplus, nullptr, d_targets,
+                                       target_stride, h_src, h_status, stream, &t);
+    return st ? st : rsg_wait(ctx, t);
 }
 
 int rsg_set_kernel_timing(rsg_ctx* ctx, int on) {
     int st = enter(ctx);
     if (st) return st;
-    std::lock_guard<std::mutex> g(ctx->mu);
-    ctx->timing = on != 0;
-    ctx->tev_used = 0;
-    ctx->last_kernel_ms = -1.f;
+    ctx->timing.store(on != 0);
+    ctx->last_kernel_ms.store(-1.f);
     return RSG_OK;
 }
 
@@ -1570,8 +2008,7 @@ int rsg_set_record_engine(rsg_ctx* ctx, int engine) {
     int st = enter(ctx);
     if (st) return st;
     if (engine < RSG_RECORD_ENGINE_AUTO || engine > RSG_RECORD_ENGINE_TWO_PASS) return RSG_ERR_INVALID_ARG;
-    std::lock_guard<std::mutex> g(ctx->mu);
-    ctx->record_engine = engine;
+    ctx->record_engine.store(engine);
     return RSG_OK;
 }
 
@@ -1579,16 +2016,17 @@ int rsg_last_kernel_ms(rsg_ctx* ctx, float* ms) {
     int st = enter(ctx);
     if (st) return st;
     if (!ms) return RSG_ERR_INVALID_ARG;
-    std::lock_guard<std::mutex> g(ctx->mu);
-    *ms = ctx->last_kernel_ms;
+    *ms = ctx->last_kernel_ms.load();
     return RSG_OK;
 }
 
 // Heal (Erasure::heal, heal.rs:112-206) over n stripes of bitrot records.
-int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n, const uint8_t* const* d_files,
-                         uint8_t* const* d_targets, int algo, uint8_t* d_work, int* h_status, void* stream) {
+int rsg_heal_records_submit(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n, const uint8_t* const* d_files,
+                            uint8_t* const* d_targets, int algo, int* h_status, void* stream, uint64_t* ticket) {
     int st = enter(ctx);
     if (st) return st;
+    if (!ticket) return RSG_ERR_INVALID_ARG;
+    *ticket = 0;
     if ((st = check_geometry(k, m))) return st;
     if (m == 0) return RSG_ERR_ZERO_PARITY_SHARDS;
     if (!d_files || !d_targets || (n && !h_status)) return RSG_ERR_INVALID_ARG;
@@ -1596,202 +2034,47 @@ int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
     if (!key) return RSG_ERR_INVALID_ARG;
     if (n == 0 || shard_len == 0) {
         for (size_t x = 0; x < n; ++x) h_status[x] = RSG_OK;
+        *ticket = done_ticket(ctx);
         return RSG_OK;
     }
     const int t = k + m;
-    const uint64_t rec = 32 + shard_len, ks = (uint64_t)k * shard_len;
+    const uint64_t rec = 32 + shard_len;
     // Targets are written in the same pass that reads the sources: a target
     // range overlapping any source (or another target) would be silent
     // corruption (e.g. rewriting a rotten shard file in place), so it is
     // rejected up front.
-    {
-        const uint64_t span = n * rec;
-        auto overlap = [span](const uint8_t* a, const uint8_t* b) {
-            return (uintptr_t)a < (uintptr_t)b + span && (uintptr_t)b < (uintptr_t)a + span;
-        };
-        for (int i = 0; i < t; ++i) {
-            if (!d_targets[i]) continue;
-            for (int j = 0; j < t; ++j)
-                if ((d_files[j] && overlap(d_targets[i], d_files[j])) ||
-                    (j != i && d_targets[j] && overlap(d_targets[i], d_targets[j])))
-                    return RSG_ERR_INVALID_ARG;
-        }
+    const uint64_t span = n * rec;
+    for (int i = 0; i < t; ++i) {
+        if (!d_targets[i]) continue;
+        for (int j = 0; j < t; ++j)
+            if ((d_files[j] && spans_overlap(d_targets[i], span, d_files[j], span)) ||
+                (j != i && d_targets[j] && spans_overlap(d_targets[i], span, d_targets[j], span)))
+                return RSG_ERR_INVALID_ARG;
     }
-    hipStream_t s = pick_stream(ctx, stream);
-    std::lock_guard<std::mutex> g(ctx->mu);
-    if ((st = ctx->ensure_scratch((size_t)(t + 1) * n))) return st;
-    auto cd = get_codec(k, m);
-    if (!cd) return RSG_ERR_INVALID_ARG;
-    uint8_t* d_flags = ctx->d_scratch;
-    uint8_t* d_ok = ctx->d_scratch + (size_t)t * n;
-    ctx->tev_used = 0;
-    bool any_verify = false;
-    // Per run of stripes with one verified pattern, ONE pass over the
-    // survivors (first k verified shards) writes every target's record body —
-    // data rebuilt or, if verified, reproduced (identity row), parity
-    // re-encoded — and compares every verified source parity that is not a
-    // survivor with its re-encoded value: "inconsistent heal source shards"
-    // (heal.rs:180-196; a survivor parity re-encodes to itself).
-    auto heal_run = [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) -> int {
-        int valid = 0;
-        for (int i = 0; i < t; ++i) valid += present[i];
-        for (uint64_t x = s0; x < s1; ++x) h_status[x] = valid < k ? RSG_ERR_TOO_FEW_SHARDS : RSG_OK;
-        if (valid < k) return RSG_OK;
-        auto plan = cd->plan(present.data());
-        if (!plan) return RSG_ERR_TOO_FEW_SHARDS;
-        const uint8_t* base = d_files[plan->survivors[0]] + s0 * rec + 32;
-        auto rel = [&](const uint8_t* p) { return (uint64_t)(uintptr_t)(p + s0 * rec + 32) - (uint64_t)(uintptr_t)base; };
-        RowSet ps, vs;  // target bodies (store), non-survivor verified parity (compare)
-        ps.C = vs.C = k;
-        for (int sv : plan->survivors) ps.in_off.push_back(rel(d_files[sv]));
-        vs.in_off = ps.in_off;
-        for (int i = 0; i < t; ++i) {
-            if (d_targets[i]) {
-                ps.coef.resize((size_t)(ps.R + 1) * k);
-                plan_row(*cd, *plan, i, &ps.coef[(size_t)ps.R * k]);
-                ps.out_off.push_back(rel(d_targets[i]));
-                ++ps.R;
-            }
-            if (i >= k && present[i] && !is_survivor(*plan, i)) {
-                vs.coef.resize((size_t)(vs.R + 1) * k);
-                plan_row(*cd, *plan, i, &vs.coef[(size_t)vs.R * k]);
-                vs.out_off.push_back(rel(d_files[i]));
-                ++vs.R;
-            }
-        }
-        if (vs.R) any_verify = true;
-        uint8_t* ob = const_cast<uint8_t*>(base);
-        if (ps.R + vs.R <= rsg::kMaxR && k <= rsg::kMaxC) {
-            RowSet both = ps;
-            both.coef.insert(both.coef.end(), vs.coef.begin(), vs.coef.end());
-            both.out_off.insert(both.out_off.end(), vs.out_off.begin(), vs.out_off.end());
-            both.R = ps.R + vs.R;
-            return apply_store_compare(both, ps.R, base, ob, rec, rec, rec, shard_len, s1 - s0, d_ok + s0, s);
-        }
-        int e = apply_rows(ps, base, ob, rec, rec, shard_len, s1 - s0, rsg::GF_MODE_STORE, nullptr, s);
-        if (e || !vs.R) return e;
-        return apply_rows(vs, base, ob, rec, rec, shard_len, s1 - s0, rsg::GF_MODE_COMPARE, d_ok + s0, s);
-    };
-    // the target records of stripes [s0, s1) get their HH256S headers
-    auto hash_targets = [&](uint64_t s0, uint64_t s1) -> int {
-        std::vector<uint8_t*> tg(t, nullptr);
-        for (int i = 0; i < t; ++i)
-            if (d_targets[i]) tg[i] = d_targets[i] + s0 * rec;
-        return hash_records_inplace(tg.data(), t, shard_len, s1 - s0, key, s);
-    };
-    std::vector<uint8_t> present0(t), flags;
-    int valid0 = 0;
-    for (int i = 0; i < t; ++i) valid0 += (present0[i] = d_files[i] ? 1 : 0);
-    bool done = false;
-    if (valid0 >= k && lost_disk_fast_enabled()) {
-        // Optimistic (replaced disks, sound sources — the common heal): the GF
-        // pass first, as if every present record verifies; then ONE hash launch
-        // verifies every present record and writes every target's digest; one
-        // copy + synchronisation brings back the verified map and the parity
-        // verdict.  Runs whose verified pattern differs are redone (targets
-        // rewritten and rehashed) from their actual valid shards.
-        std::vector<int> all_idx, tg_idx;
-        for (int i = 0; i < t; ++i) {
-            if (d_files[i]) all_idx.push_back(i);
-            if (d_targets[i]) tg_idx.push_back(i);
-        }
-        bool one_pass = get_dma_enabled(ctx, n) &&
-                        rsg::heal_one_pass_shape(k, m, (int)all_idx.size(), (int)tg_idx.size(), shard_len) &&
-                        rec % 16 == 0;
-        for (int i : all_idx) one_pass = one_pass && (uintptr_t)(d_files[i] + 32) % 16 == 0;
-        for (int i : tg_idx) one_pass = one_pass && !d_files[i] && (uintptr_t)(d_targets[i] + 32) % 8 == 0;
-        if (one_pass) {
-            // RS(8,4): verify every source record, write every target record
-            // (body + digest) and compare the surplus parity in ONE pass
-            // (the kernel writes every source's flags and, with surplus rows,
-            // every stripe's verdict whole: no memsets before it)
-            ctx->tmark(s);
-            st = launch_heal_one_pass(*cd, present0, all_idx, tg_idx, d_files, d_targets, d_flags, d_ok, k, shard_len,
-                                      n, key, any_verify, s);
-            if (st == RSG_ERR_UNSUPPORTED) {  // RS(16,4) pattern without a network: the two-pass path
-                ctx->tunmark();
-                one_pass = false;
-                any_verify = false;
-            } else if (st) {
-                return st;
-            } else {
-                ctx->tmark(s);
-                if (!any_verify && (st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
-                for (uint64_t x = 0; x < n; ++x) h_status[x] = RSG_OK;
-            }
-        }
-        if (!one_pass) {
-            if ((st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
-            ctx->tmark(s);
-            if ((st = heal_run(0, n, present0))) return st;
-            ctx->tmark(s);
-            if ((st = hip_status(hipMemsetAsync(d_flags, 0, (size_t)t * n, s)))) return st;
-            ctx->tmark(s);
-            if ((st = launch_verify_and_digest(all_idx, d_files, d_flags, d_targets, t, shard_len, n, key, s)))
-                return st;
-            ctx->tmark(s);
-        }
-        if ((st = ctx->ensure_host_flags((size_t)(t + 1) * n))) return st;
-        if ((st = hip_status(hipMemcpyAsync(ctx->h_flags, d_flags, (size_t)(t + 1) * n, hipMemcpyDeviceToHost, s))))
-            return st;
-        if ((st = hip_status(hipStreamSynchronize(s)))) return st;
-        if (one_pass)  // absent files' rows were never written on the device
-            for (int i = 0; i < t; ++i)
-                if (!d_files[i]) std::memset(ctx->h_flags + (size_t)i * n, 0, n);
-        std::vector<uint8_t> ok(ctx->h_flags + (size_t)t * n, ctx->h_flags + (size_t)(t + 1) * n);
-        bool redone = false;
-        if (!flags_match_pattern(ctx->h_flags, present0, n)) {
-            flags.assign(ctx->h_flags, ctx->h_flags + (size_t)t * n);
-            st = for_each_pattern_run(t, n, flags, [&](uint64_t s0, uint64_t s1, const std::vector<uint8_t>& present) -> int {
-                if (present == present0) return RSG_OK;
-                redone = true;
-                int e = hip_status(hipMemsetAsync(d_ok + s0, 1, s1 - s0, s));
-                if (!e) e = heal_run(s0, s1, present);
-                return e ? e : hash_targets(s0, s1);
-            });
-            if (st) return st;
-        }
-        if (redone && any_verify && (st = flags_to_host(ctx, d_ok, n, ok.data(), s))) return st;
-        if (any_verify)
-            for (uint64_t x = 0; x < n; ++x)
-                if (h_status[x] == RSG_OK && !ok[x]) h_status[x] = RSG_ERR_INCONSISTENT_SOURCES;
-        done = true;
-    }
-    if (!done) {
-        // verify every source record in place first (read quorum: k verified
-        // shards per stripe), then the per-pattern GF passes, then the digests
-        if ((st = hip_status(hipMemsetAsync(d_ok, 1, n, s)))) return st;
-        if ((st = verify_gather(ctx, k, m, shard_len, n, d_files, key, nullptr, true, flags, s))) return st;
-        if ((st = for_each_pattern_run(t, n, flags, heal_run))) return st;
-        if ((st = hash_targets(0, n))) return st;
-        if (any_verify) {
-            std::vector<uint8_t> ok(n, 1);
-            if ((st = flags_to_host(ctx, d_ok, n, ok.data(), s))) return st;
-            for (uint64_t x = 0; x < n; ++x)
-                if (h_status[x] == RSG_OK && !ok[x]) h_status[x] = RSG_ERR_INCONSISTENT_SOURCES;
-        }
-    }
-    (void)d_work;
-    (void)ks;
-    // A failed stripe's target records hold unverified bytes: their digest
-    // headers are zeroed so they can never pass bitrot verification even if a
-    // caller ignores h_status (the reference writes nothing for a failed heal).
-    for (uint64_t s0 = 0; s0 < n;) {
-        if (h_status[s0] == RSG_OK) {
-            ++s0;
-            continue;
-        }
-        uint64_t s1 = s0 + 1;
-        while (s1 < n && h_status[s1] != RSG_OK) ++s1;
-        for (int i = 0; i < t; ++i)
-            if (d_targets[i] &&
-                (st = hip_status(hipMemset2DAsync(d_targets[i] + s0 * rec, rec, 0, 32, s1 - s0, s))))
-                return st;
-        s0 = s1;
-    }
-    if ((st = hip_status(hipStreamSynchronize(s)))) return st;
-    ctx->tcollect();
-    return RSG_OK;
+    auto rj = std::make_shared<RecJob>();
+    rj->ctx = ctx;
+    rj->heal = true;
+    rj->k = k;
+    rj->m = m;
+    rj->t = t;
+    rj->S = shard_len;
+    rj->n = n;
+    rj->rec = rec;
+    rj->key = key;
+    rj->files.assign(d_files, d_files + t);
+    rj->targets.assign(d_targets, d_targets + t);
+    rj->h_status = h_status;
+    rj->s = pick_stream(ctx, stream);
+    rj->sc = ctx->take_scratch();
+    return submit_record_job(ctx, std::move(rj), heal_begin, heal_finish, ticket);
+}
+
+int rsg_heal_records_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n, const uint8_t* const* d_files,
+                         uint8_t* const* d_targets, int algo, uint8_t* d_work, int* h_status, void* stream) {
+    (void)d_work;  // unused since ABI 3
+    uint64_t t = 0;
+    int st = rsg_heal_records_submit(ctx, k, m, shard_len, n, d_files, d_targets, algo, h_status, stream, &t);
+    return st ? st : rsg_wait(ctx, t);
 }
 
 // Whole-shard-file verification (bitrot_verify, bitrot.rs:616-655) of n files.
@@ -1800,6 +2083,7 @@ int rsg_bitrot_verify_dev(rsg_ctx* ctx, int algo, size_t n_files, const uint8_t*
                           int* h_status, void* stream) {
     int st = enter(ctx);
     if (st) return st;
+    if (ctx->timing.load()) ctx->last_kernel_ms.store(-1.f);  // a call that returns early was not timed
     if (n_files && (!d_files || !file_lens || !h_status)) return RSG_ERR_INVALID_ARG;
     const bool streaming = algo == RSG_HASH_HIGHWAY256S || algo == RSG_HASH_HIGHWAY256S_LEGACY;
     if (!streaming && algo != RSG_HASH_NONE) return RSG_ERR_UNSUPPORTED;
@@ -1812,45 +2096,52 @@ int rsg_bitrot_verify_dev(rsg_ctx* ctx, int algo, size_t n_files, const uint8_t*
         for (size_t f = 0; f < n_files; ++f) h_status[f] = RSG_ERR_FILE_SIZE_MISMATCH;
         return RSG_OK;
     }
+    for (size_t f = 0; f < n_files; ++f)
+        if (!d_files[f] && file_lens[f]) return RSG_ERR_INVALID_ARG;
     const uint64_t* key = streaming ? hash_key(algo) : nullptr;
     const uint64_t full = part_size ? part_size / shard_size : 0, tail = part_size - full * shard_size;
     const uint64_t recs = full + (tail ? 1 : 0);  // records in a complete file
     const uint64_t rec = hs + shard_size;
     hipStream_t s = pick_stream(ctx, stream);
-    std::lock_guard<std::mutex> g(ctx->mu);
-    ctx->tev_used = 0;
-    if (streaming && recs && (st = ctx->ensure_scratch((size_t)recs * n_files))) return st;
+    struct Lease {  // the call's scratch, back to the pool on every return
+        rsg_ctx* ctx;
+        std::unique_ptr<RecScratch> sc;
+        ~Lease() { ctx->give_scratch(std::move(sc)); }
+    } lease{ctx, ctx->take_scratch()};
+    RecScratch& sc = *lease.sc;
+    if (streaming && recs && (st = sc.ensure((size_t)recs * n_files, (size_t)recs * n_files))) return st;
     // records wholly inside each file are verified on the GPU (flags per
     // record, [file][record]); full records of up to kMaxHashBases files per
-    // launch, then the short last records likewise
+    // launch, then the short last records likewise; a short file's complete
+    // records alone in a launch of its own
     std::vector<uint64_t> avail(n_files, 0);
     std::vector<size_t> bulk_full, bulk_tail;
     for (size_t f = 0; f < n_files; ++f) {
-        if (!d_files[f] && file_lens[f]) return RSG_ERR_INVALID_ARG;
         const uint64_t len = std::min<uint64_t>(file_lens[f], want_size);
         uint64_t a = std::min<uint64_t>(len / rec, full);
         if (a == full && tail && len - full * rec >= hs + tail) a = recs;
         avail[f] = a;
         if (!streaming || !a) continue;
-        if ((st = hip_status(hipMemsetAsync(ctx->d_scratch + (size_t)f * recs, 1, a, s)))) return st;
+        if ((st = hip_status(hipMemsetAsync(sc.d + (size_t)f * recs, 1, a, s)))) return st;
         if (a >= full && full) bulk_full.push_back(f);
         if (a > full) bulk_tail.push_back(f);
-        if (a < full) {  // a short file: its complete records alone
-            rsg::HashParams h;
-            std::memset(&h, 0, sizeof(h));
-            std::memcpy(h.key, key, sizeof(h.key));
-            h.len = shard_size;
-            h.n = a;
-            h.stripe_stride = rec;
-            h.nbases = 1;
-            h.per_base = a;
-            h.digest_off = -(int64_t)hs;
-            h.base[0] = d_files[f] + hs;
-            h.flag_base[0] = ctx->d_scratch + (size_t)f * recs;
-            if ((st = hip_status(rsg::launch_hh256(h, s)))) return st;
-        }
     }
-    ctx->tmark(s);  // the kernel-timing hook brackets the multi-file verify launches
+    sc.tmark(s);  // the kernel-timing hook brackets every verify launch of the call
+    for (size_t f = 0; f < n_files; ++f) {
+        if (!streaming || !avail[f] || avail[f] >= full) continue;
+        rsg::HashParams h;  // a short file: its complete records alone
+        std::memset(&h, 0, sizeof(h));
+        std::memcpy(h.key, key, sizeof(h.key));
+        h.len = shard_size;
+        h.n = avail[f];
+        h.stripe_stride = rec;
+        h.nbases = 1;
+        h.per_base = avail[f];
+        h.digest_off = -(int64_t)hs;
+        h.base[0] = d_files[f] + hs;
+        h.flag_base[0] = sc.d + (size_t)f * recs;
+        if ((st = hip_status(rsg::launch_hh256(h, s)))) return st;
+    }
     for (int pass = 0; pass < 2; ++pass) {
         const std::vector<size_t>& list = pass == 0 ? bulk_full : bulk_tail;
         for (size_t g0 = 0; g0 < list.size(); g0 += rsg::kMaxHashBases) {
@@ -1867,15 +2158,15 @@ int rsg_bitrot_verify_dev(rsg_ctx* ctx, int algo, size_t n_files, const uint8_t*
             for (size_t x = g0; x < g1; ++x) {
                 const size_t f = list[x];
                 h.base[x - g0] = d_files[f] + (pass == 0 ? 0 : full * rec) + hs;
-                h.flag_base[x - g0] = ctx->d_scratch + (size_t)f * recs + (pass == 0 ? 0 : full);
+                h.flag_base[x - g0] = sc.d + (size_t)f * recs + (pass == 0 ? 0 : full);
             }
             if ((st = hip_status(rsg::launch_hh256(h, s)))) return st;
         }
     }
-    ctx->tmark(s);
+    sc.tmark(s);
     std::vector<uint8_t> flags(streaming ? (size_t)recs * n_files : 0);
     if (!flags.empty()) {
-        if ((st = flags_to_host(ctx, ctx->d_scratch, flags.size(), flags.data(), s))) return st;
+        if ((st = flags_to_host(sc, sc.d, flags.size(), flags.data(), s))) return st;
     } else if ((st = hip_status(hipStreamSynchronize(s)))) {
         return st;
     }
@@ -1891,7 +2182,7 @@ int rsg_bitrot_verify_dev(rsg_ctx* ctx, int algo, size_t n_files, const uint8_t*
         if (res == RSG_OK && file_lens[f] > want_size) res = RSG_ERR_TRAILING_DATA;
         h_status[f] = res;
     }
-    ctx->tcollect();  // the stream was synchronised above
+    if (sc.timing) ctx->last_kernel_ms.store(sc.tsum());  // the stream was synchronised above
     return RSG_OK;
 }
 

@@ -350,11 +350,8 @@ class Erasure:
             d = digests.ctypes.data
         return n, t, S, d
 
-    def decode_records_batch(self, files: Sequence, shard_len: int, n: int, verify_surplus: bool = True,
-                             algo: int = _lib.RSG_HASH_HIGHWAY256S, out=None, stream=None):
-        """GET engine (rsg_decode_records_dev): `files[i]` is a cuda uint8 tensor
-        holding shard i's n BitrotWriter records ([32-byte digest][shard_len]) or
-        None.  Returns (data (n, k*shard_len) tensor, per-stripe status list)."""
+    def _record_files(self, files: Sequence, shard_len: int, n: int):
+        """Validate the GET's record files; returns (device, ctypes pointer array)."""
         import torch
         t = self.total_shard_count()
         if len(files) != t:
@@ -368,26 +365,125 @@ class Erasure:
                 dev = f.device
         if dev is None:
             raise RsgError(_lib.RSG_ERR_TOO_FEW_SHARDS, "no shard available")
+        return dev, (ctypes.c_void_p * t)(*[f.data_ptr() if f is not None else None for f in files])
+
+    def _slots(self, targets, shard_len: int, n: int, dev, target_stride: Optional[int]):
+        """The in-place GET's k data-shard slots: None -> a new (n, k*S) block
+        tensor (slot i = columns [i*S, (i+1)*S)); a 2-D (n, k*S) tensor, the
+        same layout; or k tensors with `target_stride` bytes between stripes
+        (default S).  Returns (keep, ctypes pointer array, stride)."""
+        import torch
+        k = self.data_shards
+        if targets is None:
+            targets = torch.empty((n, k * shard_len), dtype=torch.uint8, device=dev)
+        if isinstance(targets, torch.Tensor):
+            if targets.dtype != torch.uint8 or not targets.is_cuda or not targets.is_contiguous() \
+                    or targets.numel() < n * k * shard_len:
+                raise TypeError("targets must be a contiguous cuda uint8 tensor (n, k*shard_len)")
+            base = targets.data_ptr()
+            return targets, (ctypes.c_void_p * k)(*[base + i * shard_len for i in range(k)]), k * shard_len
+        if len(targets) != k:
+            raise RsgError(_lib.RSG_ERR_INVALID_SHARD_COUNT, f"invalid slot count: got {len(targets)}, expected {k}")
+        stride = shard_len if target_stride is None else target_stride
+        for tg in targets:
+            if tg is None or tg.dtype != torch.uint8 or not tg.is_cuda or not tg.is_contiguous() \
+                    or (n and tg.numel() < (n - 1) * stride + shard_len):
+                raise TypeError("each slot must be a contiguous cuda uint8 tensor of n strided shards")
+        return targets, (ctypes.c_void_p * k)(*[tg.data_ptr() for tg in targets]), stride
+
+    @staticmethod
+    def _stream_handle(stream, dev):
+        import torch
+        if stream is None:
+            return torch.cuda.current_stream(dev).cuda_stream
+        return stream if isinstance(stream, int) else stream.cuda_stream
+
+    def decode_records_batch(self, files: Sequence, shard_len: int, n: int, verify_surplus: bool = True,
+                             algo: int = _lib.RSG_HASH_HIGHWAY256S, out=None, stream=None):
+        """GET engine, gather form (rsg_decode_records_dev): `files[i]` is a cuda
+        uint8 tensor holding shard i's n BitrotWriter records ([32-byte
+        digest][shard_len]) or None.  Returns (data (n, k*shard_len) tensor,
+        per-stripe status list)."""
+        import torch
+        dev, ptrs = self._record_files(files, shard_len, n)
         if out is None:
             out = torch.empty((n, self.data_shards * shard_len), dtype=torch.uint8, device=dev)
-        ptrs = (ctypes.c_void_p * t)(*[f.data_ptr() if f is not None else None for f in files])
         status = (ctypes.c_int * max(n, 1))()
-        s = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
         check(_lib.load().rsg_decode_records_dev(
             _lib.context(dev.index or 0).handle, self.data_shards, self.parity_shards, shard_len, n, ptrs, algo,
-            1 if verify_surplus else 0, out.data_ptr(), status, s), "RustFS codec reconstruct failed")
+            1 if verify_surplus else 0, out.data_ptr(), status, self._stream_handle(stream, dev)),
+            "RustFS codec reconstruct failed")
         return out, _lib.status_list(status, n)
 
-    def heal_records_batch(self, files: Sequence, targets: Sequence, shard_len: int, n: int,
-                           algo: int = _lib.RSG_HASH_HIGHWAY256S, work=None, stream=None):
-        """Batched heal (rsg_heal_records_dev; Erasure::heal, heal.rs:112-206).
-        `work` is accepted for compatibility and unused (ABI 3).
+    def decode_records_into_batch(self, files: Sequence, shard_len: int, n: int, targets=None,
+                                  target_stride: Optional[int] = None, verify_surplus: bool = True,
+                                  algo: int = _lib.RSG_HASH_HIGHWAY256S, stream=None):
+        """GET engine, in-place form (rsg_decode_records_into_dev): the
+        reference's reconstruct_into contract (bridge.rs:274-307) — a data
+        shard whose record verifies is served from that record and never
+        copied; only the shards no verified record serves (file absent or
+        record rotten) are rebuilt, into their slot (`targets`, see _slots).
+        Returns (slots, src, status): src is a (k, n) bool array, True where
+        data shard i of stripe s is the body of files[i]'s record s, False
+        where it was written to slot i."""
+        dev, ptrs = self._record_files(files, shard_len, n)
+        slots, tptr, stride = self._slots(targets, shard_len, n, dev, target_stride)
+        k = self.data_shards
+        src = np.ones((k, max(n, 1)), dtype=np.uint8)
+        status = (ctypes.c_int * max(n, 1))()
+        check(_lib.load().rsg_decode_records_into_dev(
+            _lib.context(dev.index or 0).handle, k, self.parity_shards, shard_len, n, ptrs, algo,
+            1 if verify_surplus else 0, tptr, stride, src.ctypes.data, status, self._stream_handle(stream, dev)),
+            "RustFS codec reconstruct failed")
+        return slots, src[:, :n].astype(bool), _lib.status_list(status, n)
 
-        `files[i]`: cuda uint8 tensor with shard i's n BitrotWriter records, or
-        None (no reader).  `targets[i]`: cuda uint8 tensor of n*(32+shard_len)
-        bytes that receives the rebuilt records of shard i, or None (no
-        writer).  Returns the per-stripe status list (RSG_OK,
-        RSG_ERR_TOO_FEW_SHARDS = read quorum, RSG_ERR_INCONSISTENT_SOURCES)."""
+    def decode_records_submit(self, files: Sequence, shard_len: int, n: int, out=None, targets=None,
+                              target_stride: Optional[int] = None, inplace: bool = False,
+                              verify_surplus: bool = True, algo: int = _lib.RSG_HASH_HIGHWAY256S,
+                              stream=None) -> "RecordTicket":
+        """Asynchronous GET (rsg_decode_records_submit): returns at once; the
+        ticket's wait() gives what the synchronous form returns — (data,
+        status) for the gather form, (slots, src, status) with inplace=True."""
+        import torch
+        dev, ptrs = self._record_files(files, shard_len, n)
+        k = self.data_shards
+        status = (ctypes.c_int * max(n, 1))()
+        src = np.ones((k, max(n, 1)), dtype=np.uint8) if inplace else None
+        if inplace:
+            slots, tptr, stride = self._slots(targets, shard_len, n, dev, target_stride)
+            d_out, keep = None, slots
+        else:
+            if out is None:
+                out = torch.empty((n, k * shard_len), dtype=torch.uint8, device=dev)
+            d_out, tptr, stride, keep = out.data_ptr(), None, 0, out
+        tk = ctypes.c_uint64(0)
+        ctx = _lib.context(dev.index or 0)
+        check(_lib.load().rsg_decode_records_submit(
+            ctx.handle, k, self.parity_shards, shard_len, n, ptrs, algo, 1 if verify_surplus else 0, d_out, tptr,
+            stride, src.ctypes.data if inplace else None, status, self._stream_handle(stream, dev),
+            ctypes.byref(tk)), "RustFS codec reconstruct failed")
+
+        def result():
+            st = _lib.status_list(status, n)
+            return (keep, src[:, :n].astype(bool), st) if inplace else (keep, st)
+        return RecordTicket(ctx, tk.value, (files, keep, ptrs, tptr, status, src), result,
+                            "RustFS codec reconstruct failed")
+
+    def heal_records_submit(self, files: Sequence, targets: Sequence, shard_len: int, n: int,
+                            algo: int = _lib.RSG_HASH_HIGHWAY256S, stream=None) -> "RecordTicket":
+        """Asynchronous heal (rsg_heal_records_submit); wait() returns the
+        per-stripe status list of heal_records_batch."""
+        dev, src, dst = self._heal_args(files, targets, shard_len, n)
+        status = (ctypes.c_int * max(n, 1))()
+        tk = ctypes.c_uint64(0)
+        ctx = _lib.context(dev.index or 0)
+        check(_lib.load().rsg_heal_records_submit(
+            ctx.handle, self.data_shards, self.parity_shards, shard_len, n, src, dst, algo, status,
+            self._stream_handle(stream, dev), ctypes.byref(tk)), "erasure heal")
+        return RecordTicket(ctx, tk.value, (files, targets, src, dst, status),
+                            lambda: _lib.status_list(status, n), "erasure heal")
+
+    def _heal_args(self, files, targets, shard_len, n):
         import torch
         t = self.total_shard_count()
         if len(files) != t or len(targets) != t:
@@ -404,11 +500,24 @@ class Erasure:
             raise RsgError(_lib.RSG_ERR_INVALID_ARG, "invalid argument")
         src = (ctypes.c_void_p * t)(*[f.data_ptr() if f is not None else None for f in files])
         dst = (ctypes.c_void_p * t)(*[f.data_ptr() if f is not None else None for f in targets])
+        return dev, src, dst
+
+    def heal_records_batch(self, files: Sequence, targets: Sequence, shard_len: int, n: int,
+                           algo: int = _lib.RSG_HASH_HIGHWAY256S, work=None, stream=None):
+        """Batched heal (rsg_heal_records_dev; Erasure::heal, heal.rs:112-206).
+        `work` is accepted for compatibility and unused (ABI 3).
+
+        `files[i]`: cuda uint8 tensor with shard i's n BitrotWriter records, or
+        None (no reader).  `targets[i]`: cuda uint8 tensor of n*(32+shard_len)
+        bytes that receives the rebuilt records of shard i, or None (no
+        writer).  Returns the per-stripe status list (RSG_OK,
+        RSG_ERR_TOO_FEW_SHARDS = read quorum, RSG_ERR_INCONSISTENT_SOURCES)."""
+        dev, src, dst = self._heal_args(files, targets, shard_len, n)
         status = (ctypes.c_int * max(n, 1))()
-        s = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
         check(_lib.load().rsg_heal_records_dev(
             _lib.context(dev.index or 0).handle, self.data_shards, self.parity_shards, shard_len, n, src, dst,
-            algo, work.data_ptr() if work is not None else None, status, s), "erasure heal")
+            algo, work.data_ptr() if work is not None else None, status, self._stream_handle(stream, dev)),
+            "erasure heal")
         return _lib.status_list(status, n)
 
     def reconstruct_batch(self, stripes, present: Sequence[bool], mode: int = _lib.RSG_RECONSTRUCT_MISSING,
@@ -463,6 +572,55 @@ class HostBatchTicket:
         try:
             if not self._done:
                 self.wait()
+        except Exception:
+            pass
+
+
+class RecordTicket:
+    """A submitted GET or heal (rsg_decode_records_submit /
+    rsg_heal_records_submit).  Holds the call's buffers and status arrays
+    until it completes; wait() returns what the synchronous call returns."""
+
+    def __init__(self, ctx, ticket: int, keep, result, what: str):
+        self._ctx = ctx
+        self.ticket = ticket
+        self._keep = keep
+        self._result = result
+        self._what = what
+        self._done = False
+        self._value = None
+        self._error = None
+
+    def _complete(self, st: int) -> None:
+        self._done = True
+        try:
+            check(st, self._what)
+            self._value = self._result()
+        except RsgError as err:
+            self._error = err
+        self._keep = None
+
+    def poll(self) -> bool:
+        if not self._done:
+            done = ctypes.c_int(0)
+            st = _lib.load().rsg_poll(self._ctx.handle, self.ticket, ctypes.byref(done))
+            if not done.value:
+                check(st, self._what)
+                return False
+            self._complete(st)
+        return True
+
+    def wait(self):
+        if not self._done:
+            self._complete(_lib.load().rsg_wait(self._ctx.handle, self.ticket))
+        if self._error is not None:
+            raise self._error
+        return self._value
+
+    def __del__(self):  # never leave a job reading or writing freed buffers
+        try:
+            if not self._done:
+                self._complete(_lib.load().rsg_wait(self._ctx.handle, self.ticket))
         except Exception:
             pass
 

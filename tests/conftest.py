@@ -54,5 +54,36 @@ def gpu(rsgpu_lib):
     return _lib.context(0)
 
 
+SLOT_FILL = 0xA5  # what the in-place GET's slots hold before the call
+
+
+def decode_get(e, files, S, n, form, **kw):
+    """One GET through either form of the engine, as (data (n, k*S), status).
+    "gather": rsg_decode_records_dev.  "into": rsg_decode_records_into_dev
+    (reconstruct_into's contract), with the data assembled the way
+    write_data_blocks reads it (decode.rs:1390): shard i of stripe s from
+    files[i]'s record where src says it was served from there, else from slot
+    i — and checked that the call left every served shard's slot untouched and
+    never claimed to serve an absent file."""
+    import torch
+    if form == "gather":
+        return e.decode_records_batch(files, S, n, **kw)
+    k = e.data_shards
+    slots = torch.full((n, k * S), SLOT_FILL, dtype=torch.uint8, device="cuda")
+    slots_, src, status = e.decode_records_into_batch(files, S, n, targets=slots, **kw)
+    assert slots_ is slots and src.shape == (k, n)
+    out = slots.clone().view(n, k, S)
+    for i in range(k):
+        if files[i] is None:
+            assert not src[i].any(), f"absent shard {i} reported as served from its record"
+            continue
+        served = torch.from_numpy(src[i].copy()).cuda()
+        if bool(served.any()):
+            assert bool((slots.view(n, k, S)[:, i][served] == SLOT_FILL).all()), f"slot {i} written though served"
+            body = files[i][: n * (32 + S)].view(n, 32 + S)[:, 32:]
+            out[:, i][served] = body[served]
+    return out.view(n, k * S), status
+
+
 def compat_data(n: int) -> bytes:
     return bytes((i * 7 + 13) % 256 for i in range(n))

@@ -33,7 +33,7 @@ def test_exported_symbols_have_c_linkage():
 
 
 def test_abi_version(rsgpu_lib):
-    assert rsgpu_lib.rsg_abi_version() == 4
+    assert rsgpu_lib.rsg_abi_version() == 5
 
 
 @pytest.mark.parametrize("k,m", [(1, 1), (2, 2), (3, 1), (4, 2), (6, 3), (8, 4), (12, 4), (16, 4), (10, 10),

@@ -19,7 +19,11 @@ import re
 import numpy as np
 import pytest
 
+from conftest import decode_get
+
 pytestmark = pytest.mark.gpu
+
+FORMS = ["gather", "into"]  # rsg_decode_records_dev / rsg_decode_records_into_dev
 
 K, M, T = 8, 4, 12
 S, N = 1024, 19
@@ -82,22 +86,23 @@ def _rehashed(torch, oracle, f, stripe, pos):
 LOSSES = [(a,) for a in range(T)] + list(itertools.combinations(range(T), 2))
 
 
+@pytest.mark.parametrize("form", FORMS)
 @pytest.mark.parametrize("lost", [x for x in LOSSES if min(x) < K], ids=str)
-def test_get_every_pattern(gpu, oracle, records, one_pass, lost):
+def test_get_every_pattern(gpu, oracle, records, one_pass, lost, form):
     import torch
     from rustfs_amd import Erasure, _lib
     shards, recs, files = records
     e = Erasure(K, M, K * S)
     want = torch.from_numpy(shards[:, :K].reshape(N, K * S).copy()).cuda()
     f = [None if i in lost else files[i] for i in range(T)]
-    out, status = e.decode_records_batch(f, S, N)
+    out, status = decode_get(e, f, S, N, form)
     assert status == [0] * N and torch.equal(out, want)
     sur = _surplus(lost)
     if sur:
         stripe = sum(lost) % N
         f2 = list(f)
         f2[sur[-1]] = _rehashed(torch, oracle, files[sur[-1]], stripe, 3 * sum(lost) % S)
-        out, status = e.decode_records_batch(f2, S, N)
+        out, status = decode_get(e, f2, S, N, form)
         assert [i for i, x in enumerate(status) if x] == [stripe]
         assert status[stripe] == _lib.RSG_ERR_INCONSISTENT_SOURCES
         ok = torch.ones(N, dtype=torch.bool, device="cuda")
@@ -155,6 +160,11 @@ def records16(gpu, oracle):
 
 @pytest.mark.parametrize("heal,lost", LISTED16, ids=lambda x: str(x))
 def test_rs16_every_listed_pattern(gpu, oracle, records16, one_pass, heal, lost):
+    for form in FORMS if not heal else [None]:
+        _rs16_pattern(oracle, records16, heal, lost, form)
+
+
+def _rs16_pattern(oracle, records16, heal, lost, form):
     import torch
     from rustfs_amd import Erasure, _lib
     shards, recs, files = records16
@@ -164,13 +174,13 @@ def test_rs16_every_listed_pattern(gpu, oracle, records16, one_pass, heal, lost)
     if not heal:
         want = torch.from_numpy(shards[:, :K16].reshape(N16, K16 * S).copy()).cuda()
         f = [None if i in lost else files[i] for i in range(T16)]
-        out, status = e.decode_records_batch(f, S, N16)
+        out, status = decode_get(e, f, S, N16, form)
         assert status == [0] * N16 and torch.equal(out, want)
         if sur:
             stripe = sum(lost) % N16
             f2 = list(f)
             f2[sur[-1]] = _rehashed(torch, oracle, files[sur[-1]], stripe, 3 * sum(lost) % S)
-            out, status = e.decode_records_batch(f2, S, N16)
+            out, status = decode_get(e, f2, S, N16, form)
             assert [i for i, x in enumerate(status) if x] == [stripe]
             assert status[stripe] == _lib.RSG_ERR_INCONSISTENT_SOURCES
             ok = torch.ones(N16, dtype=torch.bool, device="cuda")
@@ -258,3 +268,72 @@ def test_network_knobs_in_own_process(gpu, oracle, env):
     r = subprocess.run([sys.executable, "-c", _TABLE_SNIPPET.format(root=root)], env={**os.environ, **env},
                        capture_output=True, text=True, timeout=150)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (env, r.stdout[-500:], r.stderr[-2000:])
+
+
+# ------------------------------------------------- long shards (the ring wraps)
+SL = 4096  # 8 steps of 512 B: the 3-slot ring, the A/B exchange and the trailing target hashers wrap
+
+
+def _long_records(oracle, k, n, seed):
+    import torch
+    t = k + 4
+    rng = np.random.default_rng(seed)
+    shards = np.zeros((n, t, SL), dtype=np.uint8)
+    recs = np.zeros((t, n, 32 + SL), dtype=np.uint8)
+    for s in range(n):
+        shards[s, :k] = rng.integers(0, 256, (k, SL), dtype=np.uint8)
+        oracle.encode(k, 4, shards[s])
+        for i in range(t):
+            recs[i, s, :32] = np.frombuffer(oracle.hh256s(shards[s, i].tobytes()), dtype=np.uint8)
+            recs[i, s, 32:] = shards[s, i]
+    return shards, recs, [torch.from_numpy(recs[i].reshape(-1).copy()).cuda() for i in range(t)]
+
+
+# one pattern of each distinct kernel shape (present files, targets, stored and compared rows)
+LONG = [(8, 19, 0, (0,)), (8, 19, 0, (0, 3)), (8, 19, 0, (2, 9)), (8, 19, 0, (6, 11)),
+        (8, 19, 1, (8,)), (8, 19, 1, (5,)), (8, 19, 1, (1, 8)), (8, 19, 1, (0, 5)), (8, 19, 1, (9, 11)),
+        (16, 11, 0, (3,)), (16, 11, 0, (2, 11)), (16, 11, 0, (4, 17)),
+        (16, 11, 1, (17,)), (16, 11, 1, (1, 16)), (16, 11, 1, (0, 5)), (16, 11, 1, (7,))]
+
+
+@pytest.mark.parametrize("k,n,heal,lost", LONG, ids=str)
+def test_long_shards_every_shape(gpu, oracle, one_pass, k, n, heal, lost):
+    """the per-pattern tests use 2 steps per shard, fewer than the
+    3-slot ring; here one pattern of each kernel shape runs 8 steps, GET in
+    both forms and heal, bit-exact against the oracle, with an inconsistent
+    surplus caught for its stripe alone."""
+    import torch
+    from rustfs_amd import Erasure, _lib
+    t = k + 4
+    shards, recs, files = _long_records(oracle, k, n, seed=k * 100 + sum(lost))
+    e = Erasure(k, 4, k * SL)
+    rec = 32 + SL
+    present = [i for i in range(t) if i not in lost]
+    sur = present[k:]
+    if not heal:
+        want = torch.from_numpy(shards[:, :k].reshape(n, k * SL).copy()).cuda()
+        f = [None if i in lost else files[i] for i in range(t)]
+        for form in FORMS:
+            out, status = decode_get(e, f, SL, n, form)
+            assert status == [0] * n and torch.equal(out, want), form
+        if sur:
+            stripe = n - 1
+            f2 = list(f)
+            bad = files[sur[-1]].clone()
+            body = bad[stripe * rec + 32:(stripe + 1) * rec].cpu().numpy().copy()
+            body[SL - 5] ^= 0x04  # in the last step
+            bad[stripe * rec + 32:(stripe + 1) * rec] = torch.from_numpy(body).cuda()
+            bad[stripe * rec:stripe * rec + 32] = torch.from_numpy(
+                np.frombuffer(oracle.hh256s(body.tobytes()), dtype=np.uint8).copy()).cuda()
+            f2[sur[-1]] = bad
+            for form in FORMS:
+                out, status = decode_get(e, f2, SL, n, form)
+                assert [i for i, x in enumerate(status) if x] == [stripe], form
+                assert status[stripe] == _lib.RSG_ERR_INCONSISTENT_SOURCES
+                assert torch.equal(out[:stripe], want[:stripe])
+        return
+    src = [None if i in lost else files[i] for i in range(t)]
+    tgt = [torch.zeros(n * rec, dtype=torch.uint8, device="cuda") if i in lost else None for i in range(t)]
+    assert e.heal_records_batch(src, tgt, SL, n) == [0] * n
+    for i in lost:
+        assert np.array_equal(tgt[i].cpu().numpy().reshape(n, rec), recs[i]), f"shard {i}"

@@ -1,6 +1,8 @@
 """One engine call repeated (for rocprofv3 --kernel-trace --stats): GET with
 two data disks lost, or heal, RS(8,4) 1 MiB stripes, n = 4096 records.
-Usage: python tools/engine_prof.py get2|get2_01|get1|get0|heal [reps]"""
+get* = the gather form (rsg_decode_records_dev), into* = the in-place form
+(rsg_decode_records_into_dev).
+Usage: python tools/engine_prof.py get2|get2_01|get1|get0|into2|into1|into0|heal [reps]"""
 import os
 import sys
 
@@ -42,6 +44,9 @@ def main():
         if what == "heal":
             tg = [torch.empty(n * rec, dtype=torch.uint8, device="cuda") if i in (1, k) else None for i in range(t)]
             e.heal_records_batch([None if i in (1, k) else files[i] for i in range(t)], tg, S, n)
+        elif what.startswith("into"):
+            lost = {"into2": (0, 3), "into1": (0,)}.get(what, ())
+            e.decode_records_into_batch([None if i in lost else files[i] for i in range(t)], S, n, targets=out)
         else:
             lost = {"get2": (0, 3), "get2_01": (0, 1), "get1": (0,)}.get(what, ())
             e.decode_records_batch([None if i in lost else files[i] for i in range(t)], S, n, out=out)

@@ -4,7 +4,7 @@ FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the
 bytes of a wide coalesced streaming read, so it is doubled.
 
 Usage: python tools/pmc_traffic.py gpurun_out/TAG KEY "kernel substring"
-Writes/updates profiles/pmc_traffic.json[KEY]."""
+Writes/updates tools/pmc_traffic.json[KEY] (shipped to the GPU box with the tree, read by bench.py)."""
 import collections
 import csv
 import glob
@@ -23,7 +23,7 @@ for f in sorted(glob.glob(os.path.join(root, "p*", "run_counter_collection.csv")
         vals[c].append(v)
 fetch = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"]) * 1024 * 2
 write = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"]) * 1024
-out_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
+out_path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "pmc_traffic.json")
 data = json.load(open(out_path)) if os.path.exists(out_path) else {}
 data[key] = {"bytes_per_launch": int(fetch + write), "fetch_bytes_corrected": int(fetch), "write_bytes": int(write),
              "kernel": filt, "source": root, "dispatches": len(vals["FETCH_SIZE"]),
