@@ -112,6 +112,13 @@ typedef enum rsg_record_engine {
 } rsg_record_engine;
 int rsg_set_record_engine(rsg_ctx *ctx, int engine);
 
+/* Fault injection, tests only (no reference counterpart; ABI 5): sub-batch
+ * `index` of every later rsg_encode_batch_host_submit on this context fails
+ * to enqueue with RSG_ERR_DEVICE (-1, the default: never).  Lets the tests
+ * check that a failing submit drains the sub-batches it had queued.  Nothing
+ * else (no environment variable) can trigger it. */
+int rsg_test_fail_subbatch(rsg_ctx *ctx, int index);
+
 /* Encoding matrix ((k+m) x k, row-major) as reed_solomon_erasure::ReedSolomon::new
  * builds it (erasure.rs:448-470 cached_modern_reed_solomon).  Host only. */
 int rsg_matrix(int k, int m, uint8_t *out);

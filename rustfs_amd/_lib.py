@@ -63,7 +63,7 @@ EXPORTED = (
     "rsg_decode_records_dev", "rsg_heal_records_dev", "rsg_bitrot_verify_dev",
     "rsg_encode_batch_host_submit", "rsg_poll", "rsg_wait", "rsg_set_kernel_timing", "rsg_last_kernel_ms",
     "rsg_set_record_engine", "rsg_decode_records_into_dev", "rsg_decode_records_submit",
-    "rsg_heal_records_submit",
+    "rsg_heal_records_submit", "rsg_test_fail_subbatch",
 )
 
 
@@ -129,6 +129,7 @@ def load():
         L.rsg_set_kernel_timing.argtypes = [P, I]
         L.rsg_last_kernel_ms.argtypes = [P, ctypes.POINTER(ctypes.c_float)]
         L.rsg_set_record_engine.argtypes = [P, I]
+        L.rsg_test_fail_subbatch.argtypes = [P, I]
         _lib = L
         return L
 

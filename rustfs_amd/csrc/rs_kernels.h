@@ -41,9 +41,6 @@ struct Tuning {
     int get_prio = 2;             // RSG_DMA_PRIO=<0..3>: wave priorities of the one-pass GET/heal
     bool decode_net = true;       // RSG_DECODE_NET=0: run-time-table GF waves for every one-pass pattern
     bool get_cached = true;       // RSG_GET_CACHED=0: non-temporal output stores in the network GET/heal kernel
-    // fault injection (tests only): RSG_TEST_FAIL_SUBBATCH=<i> makes sub-batch
-    // i of every rsg_encode_batch_host_submit fail to enqueue (-1: never)
-    int test_fail_subbatch = -1;
 };
 const Tuning& tuning();
 

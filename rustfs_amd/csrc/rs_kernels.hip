@@ -336,15 +336,22 @@ constexpr int fused_spw() {
     return fused_spw_for(T);
 }
 
-// ABLATE (measurement builds only, tools/kbench/fused_variants.hip): bit 0
-// skips the GF arithmetic, bit 1 the hash updates, bit 3 records each wave's
-// HW_ID in its stripe's first digest words, bit 4 raises the hasher waves'
-// issue priority (s_setprio 1), bit 5 the encoder waves'; production uses 0.
-template <int C, int R, int SPW, int ABLATE = 0>
+// ABLATE_ (measurement builds only: tools/kbench/fused_variants.hip defines
+// RSG_MEASUREMENT_BUILD before including this file): bit 0 skips the GF
+// arithmetic, bit 1 the hash updates, bit 3 records each wave's HW_ID in its
+// stripe's first digest words, bit 4 raises the hasher waves' issue priority
+// (s_setprio 1), bit 5 the encoder waves'.  In the shipped library every
+// ablation bit compiles to 0.
+#ifndef RSG_MEASUREMENT_BUILD
+#define RSG_MEASUREMENT_BUILD 0
+#endif
+template <int C, int R, int SPW, int ABLATE_ = 0>
 __global__ __launch_bounds__(64 * (SPW + (SPW * (C + R) + 15) / 16))
 __attribute__((amdgpu_waves_per_eu(R == 1 ? 4 : C <= 8 ? 7 : C <= 12 ? 5 : 4)))
 void k_encode_hash_fused(const GfApplyParams p,
                                                                                               const HashParams h) {
+    static_assert(ABLATE_ == 0 || RSG_MEASUREMENT_BUILD, "ablation variants exist in measurement builds only");
+    constexpr int ABLATE = RSG_MEASUREMENT_BUILD ? ABLATE_ : 0;
     // LDS: [C][R] coefficient tables (32 B each: T0 T0' T1 T1' | T2), then
     // SPW x (C+R) chunk rows.  Tables are read from LDS (broadcast) at their
     // use: held in registers across the chunk loop they cost 64+ VGPRs.
@@ -1094,7 +1101,6 @@ const Tuning& tuning() {
         v.get_prio = num("RSG_DMA_PRIO", 2, 0, 3);
         v.decode_net = flag("RSG_DECODE_NET", true);
         v.get_cached = flag("RSG_GET_CACHED", true);
-        v.test_fail_subbatch = num("RSG_TEST_FAIL_SUBBATCH", -1, 0, 1 << 30);
         return v;
     }();
     return t;

@@ -559,6 +559,7 @@ struct rsg_ctx {
     std::atomic<bool> timing{false};          // rsg_set_kernel_timing
     std::atomic<int> record_engine{RSG_RECORD_ENGINE_AUTO};  // rsg_set_record_engine
     std::atomic<float> last_kernel_ms{-1.f};  // the last finished timed record call
+    std::atomic<int> fail_subbatch{-1};       // rsg_test_fail_subbatch: fault injection, tests only
 
     std::unique_ptr<RecScratch> take_scratch() {
         std::unique_ptr<RecScratch> sc;
@@ -839,7 +840,7 @@ int rsg_encode_batch_host_submit(rsg_ctx* ctx, int k, int m, size_t shard_len, s
         if ((st = ctx->ensure_pipeline((size_t)(chunk * dstride + dig_bytes)))) return st;
         const size_t dpitch_data = (shard_pitch == dpitch) ? (size_t)(k * dpitch) : 0;
         bool used[rsg_ctx::kPipeSlots] = {};
-        const int fail_at = rsg::tuning().test_fail_subbatch;
+        const int fail_at = ctx->fail_subbatch.load();  // rsg_test_fail_subbatch (tests only)
         int sub = 0;
         for (uint64_t s0 = 0; s0 < n && !st; s0 += chunk, ++sub) {
             const int b = (int)(ctx->next_slot++ % rsg_ctx::kPipeSlots);
@@ -2001,6 +2002,12 @@ int rsg_set_kernel_timing(rsg_ctx* ctx, int on) {
     if (st) return st;
     ctx->timing.store(on != 0);
     ctx->last_kernel_ms.store(-1.f);
+    return RSG_OK;
+}
+
+int rsg_test_fail_subbatch(rsg_ctx* ctx, int index) {
+    if (!ctx || index < -1) return RSG_ERR_INVALID_ARG;
+    ctx->fail_subbatch.store(index);
     return RSG_OK;
 }
 

@@ -179,7 +179,7 @@ def test_ticket_waited_from_many_threads(gpu, oracle):
 
 def test_submit_failure_drains_queued_subbatches(tmp_path):
     """rsg_encode_batch_host_submit failing on a later sub-batch (fault
-    injected with RSG_TEST_FAIL_SUBBATCH, in a child process) returns the
+    injected with the test-only rsg_test_fail_subbatch, in a child process) returns the
     error only after the sub-batches it had queued have landed: their parity
     and digests are in the caller's buffers when the call returns, nothing is
     left in flight, and no ticket is issued."""
@@ -195,6 +195,7 @@ import numpy as np, torch
 from oracle import oracle as O
 from rustfs_amd import _lib
 L = _lib.load(); ctx = _lib.context(0).handle
+assert L.rsg_test_fail_subbatch(ctx, 1) == _lib.RSG_OK
 k, m, S = 8, 4, 131072
 n = 3 * ((96 << 20) // ((k + m) * S))  # three ~96 MiB sub-batches
 st = torch.zeros((n, k + m, S), dtype=torch.uint8).pin_memory().numpy()
@@ -214,8 +215,8 @@ t2 = ctypes.c_uint64(0)
 assert L.rsg_encode_batch_host_submit(ctx, k, m, S, 4, st.ctypes.data, S, (k + m) * S, None, 0,
                                       ctypes.byref(t2)) == _lib.RSG_OK  # one sub-batch: index 1 never comes
 assert L.rsg_wait(ctx, t2.value) == _lib.RSG_OK
+assert L.rsg_test_fail_subbatch(ctx, -1) == _lib.RSG_OK
 print("child ok")
 ''')
-    env = dict(os.environ, RSG_TEST_FAIL_SUBBATCH="1")
-    p = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=150)
+    p = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=150)
     assert p.returncode == 0 and "child ok" in p.stdout, p.stderr[-3000:]

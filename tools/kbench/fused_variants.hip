@@ -2,6 +2,7 @@
 // kernel on RS(8,4), 1 MiB stripes, n = 4096, interleaved timing in one
 // process: full kernel, no GF arithmetic, no hashing, neither, and the
 // unfused pair (encode kernel + quad hash kernel).  Not part of the product.
+#define RSG_MEASUREMENT_BUILD 1  // the ablation variants of k_encode_hash_fused
 #include "../../rustfs_amd/csrc/rs_kernels.hip"
 
 #include <stdio.h>
