@@ -23,6 +23,15 @@ what exercises the codec path:
 * VERIFY: deep-scan every shard file (bitrot_verify, bitrot.rs:616-655) with
   one rsg_bitrot_verify_dev call.
 
+Commit: a PUT writes every shard file under a temporary name and renames the
+written ones into place only once the write quorum holds, then writes each
+disk's meta.json (tagged with the PUT's version id); a disk whose writer was
+dropped loses its previous version's part and meta (heal rebuilds them), and a
+PUT that fails leaves the previous version untouched — the reference stages
+through a temporary directory and renames on commit (rename_data).  GET and
+heal pick the metadata version held by the most disks and read only the shard
+files of disks holding it (the reference's quorum choice of FileInfo).
+
 Shard placement is identity (shard i on disk i); the reference's key-hash
 distribution, xl.meta, quorum and locking are out of scope.
 """
@@ -31,6 +40,7 @@ from __future__ import annotations
 import json
 import os
 import threading
+import uuid
 from typing import Iterator, List, Optional
 
 import numpy as np
@@ -98,13 +108,21 @@ class LocalErasureSet:
                 for b in range(nfull):
                     for i in range(t):
                         records[i] += [dig[b, i], st[b, i]]
-            self._write_records(name, records, data[nfull * bs:] if tail else None)
+            version = uuid.uuid4().hex
+            try:
+                self._write_records(name, records, data[nfull * bs:] if tail else None, version)
+            except BaseException:
+                self._discard(name, version)
+                raise
         finally:
             if staged:
                 self._stage_lock.release()
-        return self._write_meta(name, int(data.size))
+        return self._commit(name, int(data.size), version)
 
-    def _write_records(self, name: str, records: List[list], tail) -> None:
+    def _tmp(self, i: int, name: str, version: str) -> str:
+        return self._path(i, name) + ".tmp-" + version
+
+    def _write_records(self, name: str, records: List[list], tail, version: str) -> None:
         e, t = self.erasure, self.k + self.m
         if tail is not None:
             shards = e.encode_data(tail)
@@ -112,7 +130,7 @@ class LocalErasureSet:
                 records[i] += [self.algo.hash_encode(shards[i]), shards[i]]
         for i in range(t):
             os.makedirs(os.path.dirname(self._path(i, name)), exist_ok=True)
-            fd = os.open(self._path(i, name), os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+            fd = os.open(self._tmp(i, name, version), os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
             try:
                 for c0 in range(0, len(records[i]), 512):  # IOV_MAX is 1024 on Linux
                     chunk = records[i][c0:c0 + 512]
@@ -137,12 +155,13 @@ class LocalErasureSet:
         dropped shards are not committed and heal rebuilds them."""
         e, t = self.erasure, self.k + self.m
         fds: List[Optional[int]] = []
+        version = uuid.uuid4().hex
         staged = self._stage_lock.acquire(blocking=False)  # else another PUT holds the stage
         try:
             for i in range(t):
                 try:  # a disk that cannot take the part has no writer (DiskNotFound)
                     os.makedirs(os.path.dirname(self._path(i, name)), exist_ok=True)
-                    fds.append(os.open(self._path(i, name), os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644))
+                    fds.append(os.open(self._tmp(i, name, version), os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644))
                 except OSError:
                     fds.append(None)
             info = put_stream(e, reader, size, fds, self.algo, batch_blocks, inflight_batches,
@@ -151,6 +170,9 @@ class LocalErasureSet:
             if staged:
                 self._put_stage = stage
             self.last_put = info
+        except BaseException:
+            self._discard(name, version)  # below quorum (or any failure): the previous version stays
+            raise
         finally:
             if staged:
                 self._stage_lock.release()
@@ -160,45 +182,72 @@ class LocalErasureSet:
                         os.close(fd)
                     except OSError:
                         pass
-        # the dropped writers' disks are left out of the commit (their
-        # partial part files removed), as the reference drops them before
-        # renaming the object into place
-        failed = set(info["failed_shards"])
-        for i in failed:
+        # the dropped writers' disks are left out of the commit, as the
+        # reference drops them before renaming the object into place
+        return self._commit(name, size, version, skip=set(info["failed_shards"]))
+
+    def _discard(self, name: str, version: str) -> None:
+        for i in range(self.k + self.m):
             try:
-                os.unlink(self._path(i, name))
+                os.unlink(self._tmp(i, name, version))
             except OSError:
                 pass
-        return self._write_meta(name, size, skip=failed)
 
-    def _write_meta(self, name: str, size: int, skip=()) -> dict:
+    def _commit(self, name: str, size: int, version: str, skip=()) -> dict:
+        """Rename the written shard files into place and write each disk's
+        meta.json; a skipped (dropped) disk keeps nothing of the previous
+        version, so no GET or heal reads a stale part or size from it."""
         e = self.erasure
         meta = {"size": int(size), "data_blocks": self.k, "parity_blocks": self.m, "block_size": e.block_size,
-                "shard_size": e.shard_size(), "algorithm": self.algo.name}
+                "shard_size": e.shard_size(), "algorithm": self.algo.name, "version": version}
         for i in range(self.k + self.m):
             if i in skip:
+                for p in (self._tmp(i, name, version), self._path(i, name),
+                          os.path.join(self.dirs[i], name, "meta.json")):
+                    try:
+                        os.unlink(p)
+                    except OSError:
+                        pass
                 continue
-            with open(os.path.join(self.dirs[i], name, "meta.json"), "w") as f:
-                json.dump(meta, f)
+            os.replace(self._tmp(i, name, version), self._path(i, name))
+            self._write_meta_file(i, name, meta)
         return meta
+
+    def _write_meta_file(self, i: int, name: str, meta: dict) -> None:
+        path = os.path.join(self.dirs[i], name, "meta.json")
+        with open(path + ".tmp", "w") as f:
+            json.dump(meta, f)
+        os.replace(path + ".tmp", path)
 
     # ------------------------------------------------------------------ GET
     def _meta(self, name: str) -> dict:
+        """The metadata version held by the most disks (ties: the lowest disk
+        index holding one), with "disks": the disks that hold it."""
+        votes: dict = {}
         for i in range(self.k + self.m):
             try:
                 with open(os.path.join(self.dirs[i], name, "meta.json")) as f:
-                    return json.load(f)
-            except OSError:
+                    meta = json.load(f)
+            except (OSError, ValueError):
                 continue
-        raise FileNotFoundError(name)
+            key = json.dumps(meta, sort_keys=True)
+            votes.setdefault(key, (meta, []))[1].append(i)
+        if not votes:
+            raise FileNotFoundError(name)
+        meta, disks = max(votes.values(), key=lambda v: (len(v[1]), -v[1][0]))
+        return dict(meta, disks=disks)
 
-    def _open_shards(self, name: str, size: int) -> List[Optional[int]]:
-        """Shard file descriptors; a missing or wrong-length file is None
-        (the reader for that disk is unavailable)."""
+    def _open_shards(self, name: str, size: int, disks=None) -> List[Optional[int]]:
+        """Shard file descriptors; a missing or wrong-length file, or a disk
+        not holding the chosen metadata version, is None (the reader for that
+        disk is unavailable)."""
         e = self.erasure
         want = bitrot_shard_file_size(e.shard_file_size(size), e.shard_size(), self.algo)
         fds: List[Optional[int]] = []
         for i in range(self.k + self.m):
+            if disks is not None and i not in disks:
+                fds.append(None)
+                continue
             try:
                 fd = os.open(self._path(i, name), os.O_RDONLY)
             except OSError:
@@ -219,8 +268,9 @@ class LocalErasureSet:
         reusable GET stage stays locked while the stream is open: close() an
         abandoned stream (or consume it) so other GETs can reuse the stage;
         get_object_range does."""
-        size = self._meta(name)["size"]
-        fds = self._open_shards(name, size)
+        meta = self._meta(name)
+        size = meta["size"]
+        fds = self._open_shards(name, size, meta["disks"])
         try:
             yield from get_stream(self.erasure, fds, size, offset, length, self.algo, batch_blocks, self._get_stage)
         finally:
@@ -246,7 +296,7 @@ class LocalErasureSet:
         raws: List[Optional[bytes]] = []
         for i in range(t):
             raw = None
-            if i not in targets:
+            if i not in targets and i in meta["disks"]:
                 try:
                     with open(self._path(i, name), "rb") as f:
                         raw = f.read()
@@ -289,12 +339,14 @@ class LocalErasureSet:
                     raise _lib.InvalidDataError(_lib.RSG_ERR_INCONSISTENT_SOURCES, f"heal {name}")
             for i in targets:
                 out[i] += self.algo.hash_encode(bytes(shards[i])) + bytes(shards[i])
+        meta = {key: v for key, v in meta.items() if key != "disks"}
         for i in targets:
             os.makedirs(os.path.dirname(self._path(i, name)), exist_ok=True)
-            with open(self._path(i, name), "wb") as f:
+            tmp = self._path(i, name) + ".heal-tmp"
+            with open(tmp, "wb") as f:
                 f.write(bytes(out[i]))
-            with open(os.path.join(self.dirs[i], name, "meta.json"), "w") as f:
-                json.dump(meta, f)
+            os.replace(tmp, self._path(i, name))
+            self._write_meta_file(i, name, meta)
 
     # --------------------------------------------------------------- VERIFY
     def verify_object(self, name: str) -> List[int]:

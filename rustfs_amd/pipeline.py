@@ -309,11 +309,11 @@ def get_stream(erasure: Erasure, fds: List[Optional[int]], total_length: int, of
 
 class GetStage:
     """Reusable buffers of the GET pipeline: two page-locked record stages
-    per shard file, the device record files and decode output, the
-    page-locked output and the read pool.  Page-locking megabytes costs more
-    than a whole 1 MiB-object GET (the loopback set's per-object calls), so a
-    LocalErasureSet keeps one; a call that finds it busy (another thread's
-    GET) allocates its own."""
+    per shard file, the device record files, the in-place decode's k device
+    slots and their page-locked mirrors, and the read pool.  Page-locking
+    megabytes costs more than a whole 1 MiB-object GET (the loopback set's
+    per-object calls), so a LocalErasureSet keeps one; a call that finds it
+    busy (another thread's GET) allocates its own."""
 
     def __init__(self):
         self.lock = threading.Lock()
@@ -328,8 +328,8 @@ class GetStage:
         if self.key != key or self.cnt < cnt_max:
             self.stage = [[_pinned(cnt_max * rec) for _ in range(t)] for _ in range(2)]
             self.files_dev = [torch.empty(cnt_max * rec, dtype=torch.uint8, device=dev) for _ in range(t)]
-            self.out = torch.empty((cnt_max, k * S), dtype=torch.uint8, device=dev)
-            self.host_out = _pinned((cnt_max, bs))
+            self.slots = [torch.empty(cnt_max * S, dtype=torch.uint8, device=dev) for _ in range(k)]
+            self.host_slots = [_pinned(cnt_max * S) for _ in range(k)]
             self.key, self.cnt = key, cnt_max
         if self.pool is None:
             self.pool = ThreadPoolExecutor(max_workers=min(t, 8))
@@ -363,12 +363,18 @@ def _get_full(erasure, fds, start, full_end, offset, length, algo, batch_blocks,
 
 
 def _get_batches(erasure, fds, start, full_end, offset, length, algo, cnt_max, gs):
+    """The in-place GET (reconstruct_into's contract, bridge.rs:274-307; the
+    blocks written straight from the per-shard buffers, decode.rs:1390): the
+    records are verified on the device, only the shards no verified record
+    serves are rebuilt and copied back, and every other byte of the range is
+    served from the page-locked record stage it was read into — so the link
+    carries the records in and the rebuilt shards out, nothing else."""
     import torch
     k, t = erasure.data_shards, erasure.total_shard_count()
     bs, S = erasure.block_size, erasure.shard_size()
     rec = 32 + S
     dev = torch.device("cuda", erasure._device or 0)
-    stage, files_dev, out, host_out, pool = gs.stage, gs.files_dev, gs.out, gs.host_out, gs.pool
+    stage, files_dev, slots, host_slots, pool = gs.stage, gs.files_dev, gs.slots, gs.host_slots, gs.pool
     batches = [(b0, min(cnt_max, full_end + 1 - b0)) for b0 in range(start, full_end + 1, cnt_max)]
     got: dict = {}
 
@@ -398,20 +404,33 @@ def _get_batches(erasure, fds, start, full_end, offset, length, algo, cnt_max, g
                                                     non_blocking=True)
             if sum(ok) < k:
                 raise _lib.RsgError(_lib.RSG_ERR_TOO_FEW_SHARDS, "read quorum lost")
-            # batch j+1 goes into the other stage, free since batch j-1's decode
-            # returned (decode_records_batch drains the stream for its status)
+            # batch j+1 goes into the other stage, free since batch j-1's
+            # blocks were yielded (each yield is a copy)
             if j + 1 < len(batches):
                 th = threading.Thread(target=fetch, args=(j + 1,))
                 th.start()
-            data, status = erasure.decode_records_batch(
-                [files_dev[i][: cnt * rec] if ok[i] else None for i in range(t)], S, cnt,
-                algo=algo.value, out=out[:cnt], stream=s)
+            _, src, status = erasure.decode_records_into_batch(
+                [files_dev[i][: cnt * rec] if ok[i] else None for i in range(t)], S, cnt, targets=slots,
+                target_stride=S, algo=algo.value, stream=s)
             bad = [x for x in status if x != _lib.RSG_OK]
             if bad:
                 _lib.check(bad[0], "erasure decode")
-            torch.from_numpy(host_out[:cnt]).copy_(data[:, :bs], non_blocking=False)
+            for i in range(k):  # only the rebuilt shards cross the link back
+                if not src[i].all():
+                    torch.from_numpy(host_slots[i][: cnt * S]).copy_(slots[i][: cnt * S], non_blocking=True)
+            s.synchronize()
+            recs = [stage[j & 1][i][: cnt * rec].reshape(cnt, rec) for i in range(k)]
             for b in range(cnt):
                 o, n = block_geometry(offset, length, bs, b0 + b)
-                yield host_out[b, o:o + n].tobytes()
+                parts, pos, end = [], o, o + n
+                while pos < end:  # the window's bytes shard by shard
+                    i, off = divmod(pos, S)
+                    take = min(S - off, end - pos)
+                    if src[i, b]:
+                        parts.append(recs[i][b, 32 + off: 32 + off + take])
+                    else:
+                        parts.append(host_slots[i][b * S + off: b * S + off + take])
+                    pos += take
+                yield b"".join(parts)
     finally:
         th.join()

@@ -198,8 +198,8 @@ class _BreakWriters(io.BytesIO):
     def _fd_of(self, i):
         want = os.path.realpath(os.path.join(self.es.dirs[i], self.name, "part.1"))
         for fd in os.listdir("/proc/self/fd"):
-            try:
-                if os.path.realpath(f"/proc/self/fd/{fd}") == want:
+            try:  # the PUT writes part.1 under a temporary name until it commits
+                if os.path.realpath(f"/proc/self/fd/{fd}").startswith(want + ".tmp-"):
                     return int(fd)
             except OSError:
                 pass
@@ -257,3 +257,53 @@ def test_put_stream_disk_missing_from_start(gpu, tmp_path):
     finally:
         for fd in fds:
             os.close(fd)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("old_size,new_size", [(9 * BS + 777, 5 * BS + 3), (3 * BS + 997, 3 * BS + 1000)])
+def test_overwrite_with_dropped_writer(gpu, tmp_path, old_size, new_size):
+    """overwriting an object while shard 0's writer fails must not
+    leave disk 0 with the old version's meta or part (GET would read the old
+    size: a length mismatch fails every shard, an equal shard-file length
+    returns the wrong byte count); and a PUT below write quorum must leave the
+    old version readable.  (997 -> 1000 bytes of tail with k = 4: the same
+    shard-file length.)"""
+    from rustfs_amd.pipeline import WriteQuorumError
+    k, m = 4, 2
+    es, dirs = _set(tmp_path, k, m)
+    old = np.random.default_rng(1).integers(0, 256, old_size, dtype=np.uint8).tobytes()
+    new = np.random.default_rng(2).integers(0, 256, new_size, dtype=np.uint8).tobytes()
+    es.put_object_stream("b/o", io.BytesIO(old), old_size, batch_blocks=2, inflight_batches=1)
+    assert es.get_object("b/o") == old
+    es.put_object_stream("b/o", _BreakWriters(new, BS, es, "b/o", (0,)), new_size, batch_blocks=2,
+                         inflight_batches=1)
+    assert es.last_put["failed_shards"] == [0]
+    assert not os.path.exists(os.path.join(dirs[0], "b/o", "meta.json"))
+    assert not os.path.exists(os.path.join(dirs[0], "b/o", "part.1"))
+    assert es.get_object("b/o") == new
+    es.heal_object("b/o", [0])
+    assert es.get_object("b/o") == new
+    # below quorum: the PUT fails and the committed version stays readable
+    with pytest.raises(WriteQuorumError):
+        es.put_object_stream("b/o", _BreakWriters(old, BS, es, "b/o", (0, 1, 2)), old_size, batch_blocks=2,
+                             inflight_batches=1)
+    assert es.get_object("b/o") == new
+    assert not [f for d in dirs for f in os.listdir(os.path.join(d, "b/o")) if ".tmp" in f]
+
+
+@pytest.mark.gpu
+def test_meta_by_quorum(gpu, tmp_path):
+    """A stale meta.json left on a minority of disks (a version those disks
+    missed) is outvoted; their shard files are not read."""
+    import json
+    k, m = 2, 2
+    es, dirs = _set(tmp_path, k, m)
+    a = np.random.default_rng(3).integers(0, 256, 2 * BS + 5, dtype=np.uint8).tobytes()
+    b = np.random.default_rng(4).integers(0, 256, 2 * BS + 9, dtype=np.uint8).tobytes()
+    es.put_object("b/o", a)
+    stale = [open(os.path.join(dirs[3], "b/o", f), "rb").read() for f in ("meta.json", "part.1")]
+    es.put_object("b/o", b)
+    for f, raw in zip(("meta.json", "part.1"), stale):  # disk 3 rolled back to the old version
+        open(os.path.join(dirs[3], "b/o", f), "wb").write(raw)
+    assert json.load(open(os.path.join(dirs[3], "b/o", "meta.json")))["size"] == len(a)
+    assert es.get_object("b/o") == b
