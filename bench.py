@@ -63,6 +63,9 @@ def parse(argv=None):
                     help="rehearsal only: let ranks share GPUs when fewer are visible than ranks")
     ap.add_argument("--no-config-extras", action="store_true",
                     help="skip the config 4 (fused digests) and config 5 (RS(16,4)) encode extras")
+    ap.add_argument("--config4-batch", type=int, default=4096, help="config 4 extra: stripes per GPU")
+    ap.add_argument("--config5-total", type=int, default=32768,
+                    help="config 5 extra: RS(16,4) stripes split over all GPUs (one GPU: its 1/8 share)")
     ap.add_argument("--record-engine", choices=["auto", "one-pass", "two-pass"], default="auto",
                     help="GET/heal engine path for the engine extras (rsg_set_record_engine)")
     return ap.parse_args(argv)
@@ -285,11 +288,11 @@ def time_encode(e, stripes, digests, stream, reps, warm=3, warm_seconds=0.3):
     return sum(ms) / len(ms), min(ms)
 
 
-def encode_extra(name_workload, e, stripes, digests, k, m, S, n, stream, reps):
+def encode_extra(name_workload, e, stripes, digests, k, m, S, n, stream, reps, timed=None):
     """One encode configuration priced like the headline: algorithmic bytes =
     k*S read + m*S written per stripe (+ 32*(k+m) digest bytes with fused
-    digests), over the average launch time."""
-    avg, mn = time_encode(e, stripes, digests, stream, reps)
+    digests), over the average launch time (`timed`: already measured)."""
+    avg, mn = timed if timed else time_encode(e, stripes, digests, stream, reps)
     alg = n * (k + m) * S + (n * (k + m) * 32 if digests is not None else 0)
     return {"workload": name_workload, "k": k, "m": m, "shard_bytes": S, "stripes": n,
             "traffic": pmc_traffic(k, m, S, n, digests is not None),
@@ -299,32 +302,91 @@ def encode_extra(name_workload, e, stripes, digests, k, m, S, n, stream, reps):
             "frac": round(alg / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
-def config_extras(a, e_main, stripes, k, m, dev, stream, rank):
-    """BASELINE configs 4 and 5 at their per-GPU sizes, timed beside the
-    headline so the driver's default run carries them."""
+def config5_plan(world: int, rank: int, total: int):
+    """BASELINE config 5 (RS(16,4), 1 MiB stripes, a batch split across the
+    node's GPUs): (first stripe, stripes this rank encodes, stripes timed over
+    all ranks).  One GPU runs its share of the 8-GPU split (total / 8); N > 1
+    ranks split the whole batch contiguously (dispatch.split_batch: the
+    stripes are independent, encode.rs:795-919, so no collective)."""
+    from rustfs_amd.dispatch import split_batch
+    if world == 1:
+        return 0, total // 8, total // 8
+    s0, cnt = split_batch(total, world, rank)
+    return s0, cnt, total
+
+
+def gather_ranks(x, world: int):
+    if world == 1:
+        return [x]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, x)
+    return out
+
+
+def config_extras(a, e_main, stripes, k, m, dev, stream, rank, world=1):
+    """BASELINE configs 4 and 5 timed beside the headline so the driver's
+    default run carries them, at every N: config 4 (RS(8,4) encode + fused
+    HH256S, 4096 stripes per rank, weak) and config 5 (RS(16,4), S = 65536,
+    --config5-total stripes split over the ranks, strong; one GPU runs its
+    share of the 8-way split).  With N > 1 each is bracketed by a barrier and
+    its wall time is the max over ranks; every rank's kernel time, fraction
+    and device are reported."""
     import torch
     from rustfs_amd import Erasure
     out = {}
     reps = max(10, a.steps)
-    # config 4: RS(8,4) 1 MiB stripes, n = 4096, parity + all 12 HH256S
-    # digests in one pass (the PUT path's kernel, bitrot.rs:496-502)
-    n4, k4, m4 = 4096, 8, 4
+
+    def timed_ranks(name, e, st, dig, kk, mm, S, n, total):
+        torch.cuda.synchronize()
+        t_w = time.perf_counter()  # untimed warm-up (clock ramp after the previous extras)
+        while time.perf_counter() - t_w < 0.3:
+            for _ in range(4):
+                e.encode_batch(st, dig, stream=stream)
+            torch.cuda.synchronize()
+        barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        avg, mn = time_encode(e, st, dig, stream, reps, warm=0, warm_seconds=0.0)
+        el = max_over_ranks(time.perf_counter() - t0, world)
+        alg = n * (kk + mm) * S + (n * (kk + mm) * 32 if dig is not None else 0)
+        res = encode_extra(name, e, st, dig, kk, mm, S, n, stream, reps, timed=(avg, mn))
+        mine = {"kernel_ms": res["kernel_ms"], "frac": res["frac"], "stripes": n, "device": dev.index}
+        ranks = gather_ranks(mine, world)
+        if world > 1:
+            res.update({"n_gpus": world, "total_stripes": total,
+                        "GiB_s_payload_all_ranks": round(reps * total * kk * S / el / GiB, 2),
+                        "wall_ms_max_over_ranks": round(el * 1e3, 3),
+                        "per_rank_kernel_ms": [r["kernel_ms"] for r in ranks],
+                        "per_rank_frac": [r["frac"] for r in ranks],
+                        "per_rank_stripes": [r["stripes"] for r in ranks],
+                        "per_rank_device": [r["device"] for r in ranks],
+                        "alg_bytes_per_launch_this_rank": alg})
+        return res
+
+    # config 4: RS(8,4) 1 MiB stripes, parity + all 12 HH256S digests in one
+    # pass (the PUT path's kernel, bitrot.rs:496-502), a.config4_batch per rank
+    n4, k4, m4 = a.config4_batch, 8, 4
     S4 = -(-(1 << 20) // k4)
     if (k, m, a.stripe_bytes, stripes.shape[0]) == (k4, m4, 1 << 20, n4):
         st4, e4 = stripes, e_main
     else:
         st4, e4 = random_stripes(dev, k4, m4, S4, n4, 2000 + rank), Erasure(k4, m4, 1 << 20, device=dev.index)
     dig = torch.empty((n4, k4 + m4, 32), dtype=torch.uint8, device=dev)
-    out["encode_fused_hh256s"] = encode_extra("RS(8,4) encode + fused HighwayHash-256S digests, 1 MiB stripes, "
-                                              "batch 4096 (config 4)", e4, st4, dig, k4, m4, S4, n4, stream, reps)
+    out["encode_fused_hh256s"] = timed_ranks(
+        f"RS(8,4) encode + fused HighwayHash-256S digests, 1 MiB stripes, batch {n4} per GPU (config 4)",
+        e4, st4, dig, k4, m4, S4, n4, n4 * world)
     del dig, st4
-    # config 5, one GPU's share: RS(16,4), S = 65536, 8192 stripes
-    n5, k5, m5 = 8192, 16, 4
+    # config 5: RS(16,4), S = 65536, the batch split over the ranks
+    k5, m5 = 16, 4
     S5 = -(-(1 << 20) // k5)
+    _, n5, total5 = config5_plan(world, rank, a.config5_total)
     st5 = random_stripes(dev, k5, m5, S5, n5, 3000 + rank)
     e5 = Erasure(k5, m5, 1 << 20, device=dev.index)
-    out["encode_rs16_4"] = encode_extra("RS(16,4) encode, 1 MiB stripes, 8192 stripes per GPU (config 5)",
-                                        e5, st5, None, k5, m5, S5, n5, stream, reps)
+    what = (f"RS(16,4) encode, 1 MiB stripes, {total5} stripes split over {world} GPUs (config 5)" if world > 1 else
+            f"RS(16,4) encode, 1 MiB stripes, {n5} stripes: one GPU's share of the 8-GPU split of "
+            f"{a.config5_total} (config 5)")
+    out["encode_rs16_4"] = timed_ranks(what, e5, st5, None, k5, m5, S5, n5, total5)
     del st5
     torch.cuda.empty_cache()
     return out
@@ -587,8 +649,8 @@ def main(argv=None):
         extras["verify_all_ok_after_reconstruct"] = bool(ok.all().item())
         if not a.no_engines and world == 1 and not a.digests:
             extras["engines"] = engine_extras(e, stripes, k, m, S, n, stream, a.record_engine)
-        if not a.no_config_extras and world == 1:
-            extras.update(config_extras(a, e, stripes, k, m, dev, stream, rank))
+        if not a.no_config_extras:
+            extras.update(config_extras(a, e, stripes, k, m, dev, stream, rank, world))
 
     traffic = pmc_traffic(k, m, S, n, a.digests)
 

@@ -99,7 +99,8 @@ def test_bench_self_launch_two_ranks_rehearsal(gpu):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--allow-shared-device", "--batch", "256",
-           "--steps", "2", "--warmup", "1", "--warm-seconds", "0", "--no-cpu-baseline", "--no-extras"]
+           "--steps", "2", "--warmup", "1", "--warm-seconds", "0", "--no-cpu-baseline", "--no-engines",
+           "--config4-batch", "256", "--config5-total", "1001"]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=150)
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -111,3 +112,12 @@ def test_bench_self_launch_two_ranks_rehearsal(gpu):
     assert line["roofline"]["per_rank_device"] == [0, 1 % ndev]
     assert line["roofline"]["shared_device"] == (ndev < 2)
     assert len(line["roofline"]["per_rank_kernel_ms"]) == 2
+    # config 5 (RS(16,4), the batch split over the ranks) and config 4 (fused
+    # digests, per rank) ride on the N-GPU line
+    c5 = line["extras"]["encode_rs16_4"]
+    assert c5["n_gpus"] == 2 and c5["total_stripes"] == 1001 and c5["per_rank_stripes"] == [501, 500]
+    assert len(c5["per_rank_kernel_ms"]) == 2 and all(f > 0 for f in c5["per_rank_frac"])
+    assert c5["per_rank_device"] == [0, 1 % ndev] and c5["GiB_s_payload_all_ranks"] > 0
+    c4 = line["extras"]["encode_fused_hh256s"]
+    assert c4["n_gpus"] == 2 and c4["per_rank_stripes"] == [256, 256] and len(c4["per_rank_frac"]) == 2
+    assert line["extras"]["verify_all_ok_after_reconstruct"]

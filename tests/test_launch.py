@@ -136,3 +136,22 @@ def test_launcher_terminated_takes_ranks_along(tmp_path):
         else:
             os.kill(pid, signal.SIGKILL)
             raise AssertionError(f"rank process {pid} outlived the launcher")
+
+
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_config5_plan(world):
+    """Config 5 extra (RS(16,4), the batch split over the node's GPUs): every
+    stripe of the 32768-stripe batch is encoded by exactly one rank; one GPU
+    alone runs its 1/8 share."""
+    import bench
+    total = 32768
+    plans = [bench.config5_plan(world, r, total) for r in range(world)]
+    if world == 1:
+        assert plans == [(0, total // 8, total // 8)]
+        return
+    assert all(p[2] == total for p in plans)
+    covered = []
+    for s0, cnt, _ in plans:
+        covered += list(range(s0, s0 + cnt))
+    assert covered == list(range(total))
+    assert max(p[1] for p in plans) - min(p[1] for p in plans) <= 1
