@@ -313,6 +313,28 @@ __device__ __forceinline__ void hhq_finish(HHQuad& s, uint8_t* out, uint32_t q) 
 
 __device__ __forceinline__ void st64_any(uint8_t* p, uint64_t v) { __builtin_memcpy(p, &v, 8); }
 
+// The 8 bytes at p = shard + off of a shard of `len` bytes, those at or past
+// len read as zero (the partial last chunk of a shard of any length).
+__device__ __forceinline__ uint64_t ld64_part(const uint8_t* p, uint64_t off, uint64_t len) {
+    if (off + 8 <= len) return ld64_any(p);
+    uint64_t v = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 8; ++b)
+        if (off + b < len) v |= (uint64_t)p[b] << (8 * b);
+    return v;
+}
+
+// Store the bytes of v that fall before len (see ld64_part).
+__device__ __forceinline__ void st64_part(uint8_t* p, uint64_t v, uint64_t off, uint64_t len) {
+    if (off + 8 <= len) {
+        st64_any(p, v);
+        return;
+    }
+#pragma unroll
+    for (uint32_t b = 0; b < 8; ++b)
+        if (off + b < len) p[b] = (uint8_t)(v >> (8 * b));
+}
+
 __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only
     __builtin_amdgcn_s_barrier();

@@ -362,7 +362,7 @@ void k_encode_hash_fused(const GfApplyParams p,
     uint8_t* rows = lds_all + kTabBytes;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u, q = lane & 3u;
     const uint64_t n = h.n;
-    const uint32_t chunks = p.units;  // S / kFusedChunk
+    const uint32_t chunks = p.units;  // ceil(S / kFusedChunk)
 
     for (uint32_t i = threadIdx.x; i < (uint32_t)(C * R); i += blockDim.x) {
         const int c = i / R, r = i % R;
@@ -378,6 +378,15 @@ void k_encode_hash_fused(const GfApplyParams p,
         return;
     }
 
+    // Shards of any length (p.byte_end = S): chunks = ceil(S / 512); the
+    // last one holds `tail` bytes (1..512).  Its loads read nothing past the
+    // shard (zeros instead, so the parity bytes past S are zero too), its
+    // stores write nothing past it, and the hashers run its whole packets and
+    // then HighwayHash's remainder packet — RS(12,4) at 1 MiB blocks has
+    // S = 87382 (170 chunks + 342 bytes), and its shards sit at every
+    // alignment (8-byte accesses at any address: gfx950's unaligned mode).
+    const uint64_t S = p.byte_end;
+    const uint32_t tail = (uint32_t)(S - (uint64_t)(chunks - 1) * kFusedChunk);
     if (wave < (uint32_t)SPW) {
         // ------------------------------ encoder ------------------------------
         if constexpr (ABLATE & 32) __builtin_amdgcn_s_setprio(1);
@@ -386,18 +395,14 @@ void k_encode_hash_fused(const GfApplyParams p,
         uint8_t* sb = p.out_base + (live ? stripe : 0) * p.stripe_stride;
         uint8_t* my_rows = rows + wave * kStripeRows;
         const uint32_t m7 = vgpr_const(0x07070707u), m3 = vgpr_const(0x03030303u);
-        uint2 x[C];
-#pragma unroll
-        for (int c = 0; c < C; ++c) x[c] = *(const uint2*)(sb + p.in_off[c] + lane * 8u);
-#pragma unroll 1
-        for (uint32_t ch = 0; ch < chunks; ++ch) {
-            const uint64_t off = (uint64_t)ch * kFusedChunk + lane * 8u;
+        // the GF rows of one chunk (x: 8 bytes of every data shard per lane)
+        auto rows_of = [&](const uint2 (&x)[C], uint32_t (&acc)[R][2]) {
             // opaque per-iteration zero: keeps the table reads at their use
             // instead of hoisted out of the loop into (spilled) registers
             uint32_t tz;
             asm volatile("s_mov_b32 %0, 0" : "=s"(tz));
             const uint8_t* tabs = lds_all + tz;
-            uint32_t acc[R][2], pend[R][2];
+            uint32_t pend[R][2];
 #pragma unroll
             for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = pend[r][0] = pend[r][1] = 0u;
 #pragma unroll
@@ -428,26 +433,59 @@ void k_encode_hash_fused(const GfApplyParams p,
                     acc[r][1] ^= pend[r][1];
                 }
             }
-            if (live) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) *(uint2*)(sb + p.out_off[r] + off) = make_uint2(acc[r][0], acc[r][1]);
-            }
-            uint2 y[C];
-            if (ch + 1 < chunks) {
-#pragma unroll
-                for (int c = 0; c < C; ++c) y[c] = *(const uint2*)(sb + p.in_off[c] + off + kFusedChunk);
-            }
-            lds_barrier();  // A: the hashers are done with chunk ch-1's rows
+        };
+        // a chunk's data and parity rows into this stripe's LDS rows, between
+        // barrier A (the hashers are done with the previous chunk's rows) and
+        // B (this chunk's rows are ready)
+        auto publish = [&](const uint2 (&x)[C], const uint32_t (&acc)[R][2]) {
+            lds_barrier();  // A
 #pragma unroll
             for (int c = 0; c < C; ++c) *(uint2*)(my_rows + c * kFusedPitch + lane * 8u) = x[c];
 #pragma unroll
             for (int r = 0; r < R; ++r)
                 *(uint2*)(my_rows + (C + r) * kFusedPitch + lane * 8u) = make_uint2(acc[r][0], acc[r][1]);
-            lds_barrier();  // B: rows of chunk ch are ready
-            if (ch + 1 < chunks) {
+            lds_barrier();  // B
+        };
+        const uint32_t whole = tail == kFusedChunk ? chunks : chunks - 1;  // chunks of 512 bytes
+        uint2 x[C];
+        if (whole) {
+#pragma unroll
+            for (int c = 0; c < C; ++c) x[c] = __builtin_bit_cast(uint2, ld64_any(sb + p.in_off[c] + lane * 8u));
+        }
+#pragma unroll 1
+        for (uint32_t ch = 0; ch < whole; ++ch) {
+            const uint64_t off = (uint64_t)ch * kFusedChunk + lane * 8u;
+            uint32_t acc[R][2];
+            rows_of(x, acc);
+            if (live) {
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    st64_any(sb + p.out_off[r] + off, (uint64_t)acc[r][0] | ((uint64_t)acc[r][1] << 32));
+            }
+            uint2 y[C];
+            if (ch + 1 < whole) {
+#pragma unroll
+                for (int c = 0; c < C; ++c)
+                    y[c] = __builtin_bit_cast(uint2, ld64_any(sb + p.in_off[c] + off + kFusedChunk));
+            }
+            publish(x, acc);
+            if (ch + 1 < whole) {
 #pragma unroll
                 for (int c = 0; c < C; ++c) x[c] = y[c];
             }
+        }
+        if (whole < chunks) {  // the partial last chunk: nothing read or written at or past S
+            const uint64_t off = (uint64_t)whole * kFusedChunk + lane * 8u;
+#pragma unroll
+            for (int c = 0; c < C; ++c) x[c] = __builtin_bit_cast(uint2, ld64_part(sb + p.in_off[c] + off, off, S));
+            uint32_t acc[R][2];
+            rows_of(x, acc);
+            if (live) {
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    st64_part(sb + p.out_off[r] + off, (uint64_t)acc[r][0] | ((uint64_t)acc[r][1] << 32), off, S);
+            }
+            publish(x, acc);
         }
     } else {
         // ------------------------------ hasher -------------------------------
@@ -456,11 +494,12 @@ void k_encode_hash_fused(const GfApplyParams p,
         const uint32_t ls = g / T, shard = g - ls * T;        // local stripe, shard
         const uint64_t stripe = (uint64_t)blockIdx.x * SPW + ls;
         const bool live = g < (uint32_t)(SPW * T) && stripe < n;
-        const uint8_t* row = rows + (live ? ls * kStripeRows + shard * kFusedPitch : 0) + 8 * q;
+        const uint8_t* row0 = rows + (live ? ls * kStripeRows + shard * kFusedPitch : 0);
+        const uint8_t* row = row0 + 8 * q;
         HHQuad st;
         hhq_init(st, h.key, q);
 #pragma unroll 1
-        for (uint32_t ch = 0; ch < chunks; ++ch) {
+        for (uint32_t ch = 0; ch + 1 < chunks; ++ch) {
             lds_barrier();  // A
             lds_barrier();  // B
             if (live) {
@@ -475,7 +514,15 @@ void k_encode_hash_fused(const GfApplyParams p,
                 }
             }
         }
-        if (live) hhq_finish(st, h.out + (stripe * T + shard) * 32u, q);
+        lds_barrier();  // A (last chunk)
+        lds_barrier();  // B
+        if (live) {  // the last chunk's whole packets, then the remainder packet
+            const uint32_t full = tail / 32;
+#pragma unroll 1
+            for (uint32_t t = 0; t < full; ++t) hhq_update(st, __builtin_bit_cast(uint64_t, *(const u32x2*)(row + t * 32)));
+            if (tail % 32) hhq_remainder(st, row0 + full * 32, tail % 32, q);
+            hhq_finish(st, h.out + (stripe * T + shard) * 32u, q);
+        }
     }
 }
 
@@ -1277,9 +1324,22 @@ static FusedPick pick_fused(int C, int R, bool packed) {
     return {nullptr, 0, 0};
 }
 
+// The packed table kernel takes shards of any length at any alignment (a
+// partial last chunk); the ring, wide and DMA kernels need whole 16-byte
+// aligned steps (checked where they are picked).
 bool fused_supported(int C, int R, uint64_t shard_len) {
-    return C >= 1 && C <= kMaxC && R >= 1 && R <= 4 && shard_len >= kFusedChunk &&
-           shard_len % kFusedChunk == 0 && shard_len / kFusedChunk <= 0xffffffffull;
+    return C >= 1 && C <= kMaxC && R >= 1 && R <= 4 && shard_len >= 1 &&
+           (shard_len + kFusedChunk - 1) / kFusedChunk <= 0xffffffffull;
+}
+
+// 16-byte aligned shards and stripes (the ring kernel's 16-byte accesses)
+static bool aligned16(const GfApplyParams& p) {
+    if ((uintptr_t)p.base % 16 || p.stripe_stride % 16) return false;
+    for (uint32_t c = 0; c < p.C; ++c)
+        if (p.in_off[c] % 16) return false;
+    for (uint32_t r = 0; r < p.R; ++r)
+        if (p.out_off[r] % 16) return false;
+    return true;
 }
 
 // The DMA kernel bakes the RS(8,4) encode matrix in at compile time: it is
@@ -1405,7 +1465,7 @@ hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shar
     if (kind != 1 && kind != 3 && (kind == 2 || n_stripes < 2048)) {
         uint32_t E = n_stripes <= 768 ? 2u : 1u;
         if (E == 2 && !ring_supported((int)p.C, (int)p.R, shard_len, E)) E = 1;
-        if (ring_supported((int)p.C, (int)p.R, shard_len, E))
+        if (ring_supported((int)p.C, (int)p.R, shard_len, E) && aligned16(p))
             return launch_encode_hash_ring(p, h, shard_len, n_stripes, E, stream);
     }
     // RS(8,4), 2048+ stripes: the LDS-DMA bit-sliced kernel (RSG_FUSED_KIND=
@@ -1415,7 +1475,8 @@ hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shar
     const FusedPick f = pick_fused((int)p.C, (int)p.R, !unpacked);
     if (!f.k || !fused_supported((int)p.C, (int)p.R, shard_len) || n_stripes == 0 || n_stripes > 0x7fffffffull)
         return hipErrorInvalidValue;
-    p.units = (uint32_t)(shard_len / kFusedChunk);
+    p.units = (uint32_t)((shard_len + kFusedChunk - 1) / kFusedChunk);
+    p.byte_end = shard_len;
     h.n = n_stripes;
     const size_t lds = (size_t)p.C * p.R * 32 + (size_t)f.spw * (p.C + p.R) * kFusedPitch;
     const uint64_t blocks = (n_stripes + f.spw - 1) / f.spw;

@@ -989,8 +989,9 @@ int rsg_encode_batch_dev(rsg_ctx* ctx, int k, int m, size_t shard_len, size_t n,
     hipStream_t s = pick_stream(ctx, stream);
     const bool want_hash = d_digests && algo != RSG_HASH_NONE;
     if (want_hash && !hash_key(algo)) return RSG_ERR_INVALID_ARG;
-    const bool aligned = ((uintptr_t)d_stripes % 16 == 0) && shard_pitch % 16 == 0 && stripe_stride % 16 == 0;
-    if (want_hash && m > 0 && n > 0 && aligned && fused_enabled() && rsg::fused_supported(k, m, shard_len)) {
+    // the fused kernels take any shard length and alignment (the launcher
+    // picks one whose requirements the layout meets)
+    if (want_hash && m > 0 && n > 0 && shard_len > 0 && fused_enabled() && rsg::fused_supported(k, m, shard_len)) {
         // one pass: parity + all k+m digests (rs_kernels.hip k_encode_hash_fused)
         auto cd = get_codec(k, m);
         if (!cd) return RSG_ERR_INVALID_ARG;

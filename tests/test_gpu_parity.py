@@ -330,6 +330,14 @@ def test_host_batch_pipeline_matches_oracle(gpu, oracle, k, m, S, n, hashed):
     (8, 4, 1536, 3),     # packed kernel (S % 1024 != 0)
     (8, 4, 512, 2048),   # packed kernel (n >= 2048)
     (12, 4, 4096, 3),    # packed kernel (k > 8)
+    (12, 4, 87382, 3),   # packed kernel, partial last chunk (342 B), shards at every alignment: RS(12,4) at 1 MiB
+    (12, 4, 87382, 2100),  # the same over many workgroups
+    (6, 4, 174763, 3),   # RS(6,4) at 1 MiB: odd shard length
+    (10, 4, 104858, 3),  # RS(10,4) at 1 MiB
+    (3, 2, 31, 5),       # a shard shorter than one packet: the remainder packet alone
+    (5, 3, 1, 4),        # one-byte shards
+    (8, 4, 544, 3),      # one whole chunk + one whole packet
+    (7, 5, 1055, 9),     # partial chunk with a 31-byte remainder
 ])
 def test_fused_kernel_selection_matches_oracle(gpu, oracle, k, m, S, n):
     """Every fused encode+HH256S kernel the launcher can pick (ring E=1/2,
@@ -456,3 +464,31 @@ def test_host_encode_pinned_block_in_place(gpu, oracle, k, m, S):
     oracle.encode(k, m, ref)
     ReedSolomonEncoder(k, m).encode([blk[i] for i in range(k + m)])
     assert (blk == ref).all()
+
+
+@pytest.mark.parametrize("k,m,S,pitch", [(12, 4, 87382, 87387), (4, 2, 1000, 1003), (8, 4, 1536, 1537)])
+def test_fused_any_pitch_leaves_padding(gpu, oracle, k, m, S, pitch):
+    """Fused encode + HH256S on a layout whose shards are followed by padding
+    (shard_pitch > S, unaligned): parity and digests exact, and not one byte
+    of the padding after any shard is written (the partial last chunk's
+    stores stop at S)."""
+    import ctypes
+    import torch
+    from rustfs_amd import _lib
+    n, t = 3, k + m
+    g = torch.Generator(device="cuda").manual_seed(S)
+    buf = torch.full((n, t, pitch), 0xC3, dtype=torch.uint8, device="cuda")
+    buf[:, :k, :S] = torch.randint(0, 256, (n, k, S), dtype=torch.uint8, device="cuda", generator=g)
+    dig = torch.zeros((n, t, 32), dtype=torch.uint8, device="cuda")
+    _lib.check(_lib.load().rsg_encode_batch_dev(gpu.handle, k, m, S, n, buf.data_ptr(), pitch, t * pitch,
+                                                 dig.data_ptr(), _lib.RSG_HASH_HIGHWAY256S, None))
+    torch.cuda.synchronize()
+    host, hd = buf.cpu().numpy(), dig.cpu().numpy()
+    assert (host[:, :, S:] == 0xC3).all()
+    for s in range(n):
+        ref = np.ascontiguousarray(host[s, :, :S]).copy()
+        ref[k:] = 0
+        oracle.encode(k, m, ref)
+        assert (host[s, :, :S] == ref).all(), s
+        for i in range(t):
+            assert hd[s, i].tobytes() == oracle.hh256s(ref[i]), (s, i)
