@@ -89,6 +89,7 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_re
         uint8_t* ob = p.out_base + (live ? stripe : 0) * p.out_stripe_stride + lane * 8u;
         const uint32_t R = p.R, nst = p.n_store, cmask = p.copy_mask;
         const uint32_t m7 = vgpr_const(0x07070707u), m3 = vgpr_const(0x03030303u);
+        const uint32_t tail = walk_tail(p.byte_end, steps);  // a ragged walk's last step: first tail bytes only
         // row of present file f for this stripe: instruction f*HS + e%HS, half e/HS
         const uint32_t roff = (e % HS) * IP + (e / HS) * CH + lane * 8u;
         bool bad = false;  // this lane saw a surplus-parity mismatch
@@ -122,23 +123,31 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_re
                             __builtin_amdgcn_perm(t4.w, t4.z, s1b), __builtin_amdgcn_perm(t2, t2, s2b));
                 }
             }
+            const bool part = s + 1 == steps && tail != CH;  // wave-uniform
+            const uint64_t keep = part ? part_mask8(lane * 8u, tail) : ~0ull;
 #pragma unroll
             for (int r = 0; r < RM; ++r) {
                 if ((uint32_t)r >= R) break;
                 const uint2 v = make_uint2(acc[r][0], acc[r][1]);
                 if ((uint32_t)r < nst) {
-                    if (live) st16_nt_half(ob + p.out_off[r] + (uint64_t)s * CH, v);
+                    if (live) {
+                        if (!part) st16_nt_half(ob + p.out_off[r] + (uint64_t)s * CH, v);
+                        else st64_part(ob + p.out_off[r] + (uint64_t)s * CH, u64_of(v), lane * 8u, tail);
+                    }
                     if constexpr (TH > 0)
                         *(uint2*)(trow + (s & 1) * L::TSLOT + (r * SPW + e) * PP + lane * 8u) = v;
                 } else {
                     const uint2 o = *(const uint2*)(slot + (C + (r - nst)) * HS * IP);
-                    bad |= ((o.x ^ v.x) | (o.y ^ v.y)) != 0u;
+                    bad |= ((u64_of(o) ^ u64_of(v)) & keep) != 0ull;
                 }
             }
             if (live) {
 #pragma unroll
-                for (int c = 0; c < C; ++c)
-                    if ((cmask >> c) & 1u) st16_nt_half(ob + p.copy_off[c] + (uint64_t)s * CH, x[c]);
+                for (int c = 0; c < C; ++c) {
+                    if (!((cmask >> c) & 1u)) continue;
+                    if (!part) st16_nt_half(ob + p.copy_off[c] + (uint64_t)s * CH, x[c]);
+                    else st64_part(ob + p.copy_off[c] + (uint64_t)s * CH, u64_of(x[c]), lane * 8u, tail);
+                }
             }
             lds_barrier();  // B(s+1): done with slot s % D
         }
@@ -197,17 +206,22 @@ static bool launch_get_any(int k, int nf, int th, uint64_t n_stripes, const GfAp
     switch (k) {
         case 2: return launch_get_th<2, get_group(2)>(nf, th, n_stripes, p, h, stream);
         case 4: return launch_get_th<4, get_group(4)>(nf, th, n_stripes, p, h, stream);
+        case 6: return launch_get_th<6, get_group(6)>(nf, th, n_stripes, p, h, stream);
         case 8: return launch_get_th<8, get_group(8)>(nf, th, n_stripes, p, h, stream);
+        case 10: return launch_get_th<10, get_group(10)>(nf, th, n_stripes, p, h, stream);
+        case 12: return launch_get_th<12, get_group(12)>(nf, th, n_stripes, p, h, stream);
         case 16: return launch_get_th<16, get_group(16)>(nf, th, n_stripes, p, h, stream);
     }
     return false;
 }
 
-// Geometries with a one-pass kernel: k in {2, 4, 8, 16} (1 MiB blocks give
-// whole 512-byte steps exactly for powers of two), m <= 4, whole steps.
+// Geometries with a one-pass kernel: the data-shard counts of rustfs's
+// default sets and the powers of two (k in {2, 4, 6, 8, 10, 12, 16}: 4- to
+// 20-drive sets, storageclass.rs:24-31), m <= 4, any shard length (a ragged
+// last step, rs_records.h walk_tail).
 static bool one_pass_geometry(int k, int m, uint64_t shard_len) {
-    return (k == 2 || k == 4 || k == 8 || k == 16) && m >= 1 && m <= 4 && shard_len >= dma::CH &&
-           shard_len % dma::CH == 0 && shard_len / dma::CH <= 0xffffffffull;
+    return (k == 2 || k == 4 || k == 6 || k == 8 || k == 10 || k == 12 || k == 16) && m >= 1 && m <= 4 &&
+           shard_len >= 1 && (shard_len + dma::CH - 1) / dma::CH <= 0xffffffffull;
 }
 
 bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len) {
@@ -230,17 +244,22 @@ bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len) {
 static bool launch_net_if_listed(int heal, int k, int m, int nf, const uint8_t* coef, uint64_t n_stripes,
                                  const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
     if (m != 4 || !coef || !tuning().decode_net || p.C != (uint32_t)k) return false;
-    if (k == 16) {
-        const int pid = records_net16_pattern(heal, nf, (int)p.R, (int)p.n_store, coef);
+    using Part = bool (*)(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+    if (k == 16 || k == 12) {
+        const int pid = k == 16 ? records_net16_pattern(heal, nf, (int)p.R, (int)p.n_store, coef)
+                                : records_net12_pattern(heal, nf, (int)p.R, (int)p.n_store, coef);
         if (pid < 0) return false;
         const uint64_t blocks = (n_stripes + 3) / 4;
         if (blocks > 0x7fffffffull) return false;
-        using Part16 = bool (*)(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
-        static const Part16 parts16[RSG_NET_PARTS] = {launch_records_net16_part0, launch_records_net16_part1,
-                                                      launch_records_net16_part2, launch_records_net16_part3,
-                                                      launch_records_net16_part4, launch_records_net16_part5,
-                                                      launch_records_net16_part6, launch_records_net16_part7};
-        return parts16[pid % RSG_NET_PARTS](pid, blocks, p, h, stream);
+        static const Part parts16[RSG_NET_PARTS] = {launch_records_net16_part0, launch_records_net16_part1,
+                                                    launch_records_net16_part2, launch_records_net16_part3,
+                                                    launch_records_net16_part4, launch_records_net16_part5,
+                                                    launch_records_net16_part6, launch_records_net16_part7};
+        static const Part parts12[RSG_NET_PARTS] = {launch_records_net12_part0, launch_records_net12_part1,
+                                                    launch_records_net12_part2, launch_records_net12_part3,
+                                                    launch_records_net12_part4, launch_records_net12_part5,
+                                                    launch_records_net12_part6, launch_records_net12_part7};
+        return (k == 16 ? parts16 : parts12)[pid % RSG_NET_PARTS](pid, blocks, p, h, stream);
     }
     if (k != 8) return false;
     const int pid = records_net_pattern(heal, nf, (int)p.R, (int)p.n_store, coef);
@@ -249,7 +268,6 @@ static bool launch_net_if_listed(int heal, int k, int m, int nf, const uint8_t* 
     q.cached_stores = tuning().get_cached ? 1u : 0u;
     const uint64_t blocks = (n_stripes + 7) / 8;
     if (blocks > 0x7fffffffull) return false;
-    using Part = bool (*)(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
     static const Part parts[RSG_NET_PARTS] = {launch_records_net_part0, launch_records_net_part1,
                                               launch_records_net_part2, launch_records_net_part3,
                                               launch_records_net_part4, launch_records_net_part5,
@@ -257,17 +275,15 @@ static bool launch_net_if_listed(int heal, int k, int m, int nf, const uint8_t* 
     return parts[pid % RSG_NET_PARTS](pid, blocks, q, h, stream);
 }
 
-static bool dma_records_aligned(const HashParams& h, int nf) {
-    for (int f = 0; f < nf; ++f)
-        if ((uintptr_t)h.base[f] % 16) return false;
-    // 32-bit per-lane DMA offsets: up to G/2 records on plus a record body
-    return h.stripe_stride % 16 == 0 && 5 * h.stripe_stride < (1ull << 32);
-}
+// The record files' layout the DMA ring can walk: LDS-DMA takes sources at
+// any alignment, so records of any pitch (RS(12,4): 87414 bytes) qualify;
+// the per-lane DMA offsets are 32-bit (up to G/2 records on plus a body).
+static bool dma_records_walkable(const HashParams& h) { return 5 * h.stripe_stride < (1ull << 32); }
 
 bool heal_one_pass_shape(int k, int m, int nf, int targets, uint64_t shard_len) {
     return heal_dma_supported(k, m, nf, targets, shard_len) ||
-           (k == 16 && m == 4 && tuning().decode_net && one_pass_geometry(k, m, shard_len) && nf >= k &&
-            targets >= 1 && nf + targets <= k + m);
+           ((k == 16 || k == 12) && m == 4 && tuning().decode_net && one_pass_geometry(k, m, shard_len) &&
+            nf >= k && targets >= 1 && nf + targets <= k + m);
 }
 
 // hipErrorNotSupported: no one-pass kernel for this pattern (RS(16,4) heal
@@ -276,10 +292,11 @@ hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, 
                                    uint64_t shard_len, uint64_t n_stripes, const uint8_t* coef, hipStream_t stream) {
     p.wave_prio = dma_prio();
     if (!heal_one_pass_shape(k, m, nf, targets, shard_len) || (int)p.C != k || n_stripes == 0 || p.R > 4 ||
-        p.n_store != (uint32_t)targets || p.copy_mask || !dma_records_aligned(h, nf) ||
+        p.n_store != (uint32_t)targets || p.copy_mask || !dma_records_walkable(h) ||
         p.out_stripe_stride != h.stripe_stride)
         return hipErrorInvalidValue;
-    p.units = (uint32_t)(shard_len / dma::CH);
+    p.units = (uint32_t)((shard_len + dma::CH - 1) / dma::CH);
+    p.byte_end = shard_len;
     h.n = n_stripes;
     if (launch_net_if_listed(1, k, m, nf, coef, n_stripes, p, h, stream)) return hipGetLastError();
     if (!heal_dma_supported(k, m, nf, targets, shard_len)) return hipErrorNotSupported;
@@ -291,9 +308,10 @@ hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int k, int m
                                      uint64_t n_stripes, const uint8_t* coef, hipStream_t stream) {
     p.wave_prio = dma_prio();
     if (!decode_dma_supported(k, m, nf, shard_len) || (int)p.C != k || n_stripes == 0 || p.R > 4 ||
-        p.n_store > p.R || !dma_records_aligned(h, nf))
+        p.n_store > p.R || !dma_records_walkable(h))
         return hipErrorInvalidValue;
-    p.units = (uint32_t)(shard_len / dma::CH);
+    p.units = (uint32_t)((shard_len + dma::CH - 1) / dma::CH);
+    p.byte_end = shard_len;
     h.n = n_stripes;
     if (launch_net_if_listed(0, k, m, nf, coef, n_stripes, p, h, stream)) return hipGetLastError();
     if (!launch_get_any(k, nf, 0, n_stripes, p, h, stream)) return hipErrorInvalidValue;

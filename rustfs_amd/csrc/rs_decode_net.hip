@@ -43,8 +43,8 @@ namespace rsg {
 // the walk's 512-byte rows before they reach HBM (RS(8,4), n = 4096, GET with
 // 2 data lost 2.01 -> 1.97 ms, heal neutral; profiles/r03/ab_net/) — or
 // non-temporal (RSG_GET_CACHED=0)
-__device__ __forceinline__ void put8(uint8_t* p, const uint2& v, bool cached) {
-    if (cached) *(uint2*)p = v;
+__device__ __forceinline__ void put8(uint8_t* p, const uint2& v, bool cached) {  // any alignment
+    if (cached) st64_any(p, u64_of(v));
     else st16_nt_half(p, v);
 }
 
@@ -101,6 +101,7 @@ __device__ __forceinline__ void net_wave(const GfApplyParams& p, uint64_t n, uin
     // the 4 stripes sit at +0, +IP, +CH, +IP+CH
     const uint32_t goff = 2 * g * IP + lane * 8u;
     uint32_t diff[4] = {0u, 0u, 0u, 0u};  // OR of this lane's surplus-parity differences
+    const uint32_t tail = walk_tail(p.byte_end, steps);  // a ragged walk's last step: first tail bytes only
     lds_barrier();  // B(0)
 #pragma unroll 1
     for (uint32_t s = 0; s < steps; ++s) {
@@ -120,6 +121,7 @@ __device__ __forceinline__ void net_wave(const GfApplyParams& p, uint64_t n, uin
 #pragma unroll
             for (int j = 0; j < 8; ++j) P[8 * c + j] = w[j];
         }
+        const bool part = s + 1 == steps && tail != CH;  // wave-uniform
         uint32_t O[32];
 #if RSG_NET_ABLATE  // experiment builds only (exp/, tools/ab_ablate.sh): no arithmetic, rows = survivors
 #pragma unroll
@@ -139,15 +141,28 @@ __device__ __forceinline__ void net_wave(const GfApplyParams& p, uint64_t n, uin
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const uint2 v = make_uint2(w[2 * j], w[2 * j + 1]);
-                    if (live[j]) put8(ob[j] + p.out_off[r] + (uint64_t)s * CH, v, cached);
+                    if (live[j]) {
+                        if (!part) put8(ob[j] + p.out_off[r] + (uint64_t)s * CH, v, cached);
+                        else st64_part(ob[j] + p.out_off[r] + (uint64_t)s * CH, u64_of(v), lane * 8u, tail);
+                    }
                     if constexpr (TH > 0)
                         *(uint2*)(trow + (s & 1) * L::TSLOT + (r * SPW + mys[j]) * PP + lane * 8u) = v;
                 }
             } else {
                 uint2 o[4];
                 row4(slot, (C + (r - NST)) * HS * IP, o);
+                if (!part) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) diff[j] = or_diff(or_diff(diff[j], o[j].x, w[2 * j]), o[j].y, w[2 * j + 1]);
+                    for (int j = 0; j < 4; ++j)
+                        diff[j] = or_diff(or_diff(diff[j], o[j].x, w[2 * j]), o[j].y, w[2 * j + 1]);
+                } else {  // only the bytes before the ragged step's tail count
+                    const uint64_t keep = part_mask8(lane * 8u, tail);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint64_t d = (u64_of(o[j]) ^ ((uint64_t)w[2 * j] | ((uint64_t)w[2 * j + 1] << 32))) & keep;
+                        diff[j] |= (uint32_t)d | (uint32_t)(d >> 32);
+                    }
+                }
             }
         }
         if (!TH && cmask) {  // GET: the present data survivors copied through
@@ -157,8 +172,11 @@ __device__ __forceinline__ void net_wave(const GfApplyParams& p, uint64_t n, uin
                 uint2 x[4];
                 row4(slot, c * HS * IP, x);
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (live[j]) put8(ob[j] + p.copy_off[c] + (uint64_t)s * CH, x[j], cached);
+                for (int j = 0; j < 4; ++j) {
+                    if (!live[j]) continue;
+                    if (!part) put8(ob[j] + p.copy_off[c] + (uint64_t)s * CH, x[j], cached);
+                    else st64_part(ob[j] + p.copy_off[c] + (uint64_t)s * CH, u64_of(x[j]), lane * 8u, tail);
+                }
             }
         }
         lds_barrier();  // B(s+1): done with slot s % D

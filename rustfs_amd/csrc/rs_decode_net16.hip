@@ -1,19 +1,25 @@
-// rs_decode_net16.hip — the one-pass GET / heal kernel for RS(16,4) with its
-// rows as compile-time XOR networks per erasure pattern
+// rs_decode_net16.hip — the one-pass GET / heal kernel for RS(16,4) and
+// RS(12,4) with its rows as compile-time XOR networks per erasure pattern
 // (k_decode_records_net16<PID>; networks in the generated
-// rs164_decode_nets.h, tools/gen_decode_nets.py --k 16).  Compiled
-// RSG_NET_PARTS times (Makefile) like rs_decode_net.hip.
+// rs164_decode_nets.h / rs124_decode_nets.h, tools/gen_decode_nets.py --k 16
+// / --k 12).  Compiled RSG_NET_PARTS times per geometry (Makefile: RSG_NET_K
+// = 16 or 12) like rs_decode_net.hip.
+//
+// RS(12,4) is the default geometry of a 16-drive set (storageclass.rs:24-31);
+// at 1 MiB blocks its shards are 87382 bytes, so its record walks are ragged
+// (170 whole 512-byte steps and 342 bytes, rs_records.h walk_tail) and its
+// records sit at every alignment (LDS-DMA takes unaligned sources).
 //
 // The table kernel's RS(16,4) workgroup (k_decode_records_dma<16,NF,4,TH>:
 // 4 stripes, NF present record files DMA'd into a 3-slot LDS ring per
 // 512-byte step, ceil(2 NF / 8) DMA + verify-hash waves) with its 4 table-GF
 // waves (one per stripe, 16 survivors x 4 rows of v_perm lookups each)
 // replaced by two network waves over the one 4-stripe group (8 bytes of
-// each stripe per lane): the 16 survivors' 128 bit planes do not fit one
-// wave beside the rows, so
-//   wave B transposes survivors 8-15 and runs the pattern's net_hi (all R
-//     rows over those 64 planes) and hands its 32 partial planes to wave A
-//     through a double-buffered LDS area;
+// each stripe per lane): the 16 (12) survivors' 128 (96) bit planes do not
+// fit one wave beside the rows, so
+//   wave B transposes survivors 8..K-1 and runs the pattern's net_hi (all R
+//     rows over those 64 (32) planes) and hands its 32 partial planes to
+//     wave A through a double-buffered LDS area;
 //   wave A transposes survivors 0-7, runs net_lo, and one interval later
 //     XORs in B's half, transposes the rows back, stores the rebuilt rows
 //     (heal: also into the target-row area for the target hashers, now two
@@ -33,10 +39,22 @@
 #ifndef RSG_NET_PART
 #error "RSG_NET_PART (0 .. RSG_NET_PARTS-1) is set by the Makefile"
 #endif
+#ifndef RSG_NET_K
+#define RSG_NET_K 16
+#endif
 
 namespace rsg {
 
+#if RSG_NET_K == 16
 #include "rs164_decode_nets.h"
+namespace decnetk = decnet16;
+#elif RSG_NET_K == 12
+#include "rs124_decode_nets.h"
+namespace decnetk = decnet12;
+#else
+#error "RSG_NET_K is 16 or 12"
+#endif
+constexpr int kNetK = RSG_NET_K;
 
 template <int NF, int TH>
 struct Net16Shape : RecRing<NF, 4, TH> {
@@ -46,7 +64,7 @@ struct Net16Shape : RecRing<NF, 4, TH> {
     static constexpr int XB = TH ? 1 : 0;           // extra barrier: heal's target hashers trail by 2 steps
 };
 
-__device__ __forceinline__ void put8_16(uint8_t* p, const uint2& v) { *(uint2*)p = v; }
+__device__ __forceinline__ void put8_16(uint8_t* p, const uint2& v) { st64_any(p, u64_of(v)); }  // any alignment
 
 // Network wave A (survivors 0-7) or B (8-15) of the 4-stripe group.  Each
 // runs its half network for all R rows, keeps its half of the rows it
@@ -66,10 +84,10 @@ __device__ __forceinline__ void net16_wave(const GfApplyParams& p, uint64_t n, u
     using dma::IP;
     using dma::PP;
     using L = Net16Shape<NF, TH>;
-    constexpr decnet16::Pattern pat = decnet16::kPatterns[PID];
+    constexpr decnetk::Pattern pat = decnetk::kPatterns[PID];
     constexpr int R = pat.R, NST = pat.n_store, NCMP = R - NST, SPW = L::SPW, HS = L::HS;
     static_assert(pat.nf == NF && (pat.heal ? NST : 0) == TH && R <= 4 && NST <= R && HS == 2, "pattern shape");
-    constexpr int C0 = A ? 0 : 8;  // this wave's survivors [C0, C0 + 8)
+    constexpr int C0 = A ? 0 : 8, NC = A ? 8 : kNetK - 8;  // this wave's survivors [C0, C0 + NC)
     // heal (SF): A finishes the stored rows, B the compared ones; GET: A
     // finishes every row (B holding half the rows as well as GET's
     // copy-through spilled at the 256-VGPR cap)
@@ -99,6 +117,7 @@ __device__ __forceinline__ void net16_wave(const GfApplyParams& p, uint64_t n, u
         x[3] = *(const uint2*)(row + IP + CH);
     };
     uint32_t diff[4] = {0u, 0u, 0u, 0u};  // CMP: OR of this lane's surplus-parity differences
+    const uint32_t tail = walk_tail(p.byte_end, steps);  // a ragged walk's last step: first tail bytes only
     uint32_t keep[32];                    // step t-1's half of the rows it finishes ([8 K0, 8 (K0 + KN))), held across B(t)
     uint2 cmp[NCMP ? NCMP : 1][4];        // CMP: step t-1's surplus rows, held across B(t)
     // the exchange slot (direction to, step t) as lane-major dwords
@@ -107,9 +126,9 @@ __device__ __forceinline__ void net16_wave(const GfApplyParams& p, uint64_t n, u
     // the other wave's rows out to LDS; copy-through of its data survivors (GET)
     auto half = [&](uint32_t t) {
         const uint8_t* slot = ring + (t % D) * L::DSLOT + lane * 8u;
-        uint32_t P[64];
+        uint32_t P[64];  // B of RS(12,4): planes [0, 32) only
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
+        for (int c = 0; c < NC; ++c) {
             uint2 a[4];
             row4(slot + (C0 + c) * HS * IP, a);
             uint32_t w[8] = {a[0].x, a[0].y, a[1].x, a[1].y, a[2].x, a[2].y, a[3].x, a[3].y};
@@ -119,24 +138,28 @@ __device__ __forceinline__ void net16_wave(const GfApplyParams& p, uint64_t n, u
         }
         // the network writes every row straight into keep; the given-away
         // rows are stored to LDS from there and never read again
-        if constexpr (A) decnet16::net_lo<PID>(P, keep);
-        else decnet16::net_hi<PID>(P, keep);
+        if constexpr (A) decnetk::net_lo<PID>(P, keep);
+        else decnetk::net_hi<PID>(P, keep);
         uint32_t* xo = xb_at(A ? TO_B : TO_A, t);
 #pragma unroll
         for (int i = 0; i < 8 * GN; ++i) xo[64 * i] = keep[8 * G0 + i];
         if constexpr (CMP) {
 #pragma unroll
-            for (int r = 0; r < NCMP; ++r) row4(slot + (16 + r) * HS * IP, cmp[r]);
+            for (int r = 0; r < NCMP; ++r) row4(slot + (kNetK + r) * HS * IP, cmp[r]);
         }
         if (!TH && cmask) {  // GET: this wave's present data survivors copied through
+            const bool part = t + 1 == steps && tail != CH;  // wave-uniform
 #pragma unroll
-            for (int c = 0; c < 8; ++c) {
+            for (int c = 0; c < NC; ++c) {
                 if (!((cmask >> (C0 + c)) & 1u)) continue;  // wave-uniform
                 uint2 x[4];
                 row4(slot + (C0 + c) * HS * IP, x);
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (live[j]) put8_16(ob[j] + p.copy_off[C0 + c] + (uint64_t)t * CH, x[j]);
+                for (int j = 0; j < 4; ++j) {
+                    if (!live[j]) continue;
+                    if (!part) put8_16(ob[j] + p.copy_off[C0 + c] + (uint64_t)t * CH, x[j]);
+                    else st64_part(ob[j] + p.copy_off[C0 + c] + (uint64_t)t * CH, u64_of(x[j]), lane * 8u, tail);
+                }
             }
         }
     };
@@ -144,6 +167,7 @@ __device__ __forceinline__ void net16_wave(const GfApplyParams& p, uint64_t n, u
     // stores (A) / compares (B)
     auto finish = [&](uint32_t s) {
         const uint32_t* xi = xb_at(A ? TO_A : TO_B, s);
+        const bool part = s + 1 == steps && tail != CH;  // wave-uniform
 #pragma unroll
         for (int k = 0; k < KN; ++k) {
             const int r = K0 + k;  // the row (compile-time after unrolling)
@@ -155,15 +179,26 @@ __device__ __forceinline__ void net16_wave(const GfApplyParams& p, uint64_t n, u
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const uint2 v = make_uint2(w[2 * j], w[2 * j + 1]);
-                    if (live[j]) put8_16(ob[j] + p.out_off[r] + (uint64_t)s * CH, v);
+                    if (live[j]) {
+                        if (!part) put8_16(ob[j] + p.out_off[r] + (uint64_t)s * CH, v);
+                        else st64_part(ob[j] + p.out_off[r] + (uint64_t)s * CH, u64_of(v), lane * 8u, tail);
+                    }
                     if constexpr (TH > 0)
                         *(uint2*)(trow + (s & 1) * L::TSLOT + (r * SPW + j) * PP + lane * 8u) = v;
                 }
-            } else {
+            } else if (!part) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     diff[j] = or_diff(or_diff(diff[j], cmp[r - NST][j].x, w[2 * j]), cmp[r - NST][j].y,
                                       w[2 * j + 1]);
+            } else {  // only the bytes before the ragged step's tail count
+                const uint64_t keepm = part_mask8(lane * 8u, tail);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint64_t d =
+                        (u64_of(cmp[r - NST][j]) ^ ((uint64_t)w[2 * j] | ((uint64_t)w[2 * j + 1] << 32))) & keepm;
+                    diff[j] |= (uint32_t)d | (uint32_t)(d >> 32);
+                }
             }
         }
     };
@@ -231,7 +266,7 @@ using Net16Launch = void (*)(uint64_t blocks, const GfApplyParams& p, const Hash
 
 template <int PID>
 static void launch_net16(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
-    constexpr decnet16::Pattern pat = decnet16::kPatterns[PID];
+    constexpr decnetk::Pattern pat = decnetk::kPatterns[PID];
     constexpr int NF = pat.nf, TH = pat.heal ? pat.n_store : 0;
     hipLaunchKernelGGL((k_decode_records_net16<PID, NF, TH>), dim3((uint32_t)blocks),
                        dim3(64 * Net16Shape<NF, TH>::WAVES), 0, stream, p, h);
@@ -248,30 +283,33 @@ constexpr std::array<Net16Launch, sizeof...(I)> net16_table(std::index_sequence<
     return {pick_net16<(int)I>()...};
 }
 
-static const std::array<Net16Launch, decnet16::kCount> kNet16Part =
-    net16_table(std::make_index_sequence<decnet16::kCount>{});
+static const std::array<Net16Launch, decnetk::kCount> kNet16Part =
+    net16_table(std::make_index_sequence<decnetk::kCount>{});
 
-#define RSG_NET16_CAT2(a, b) a##b
-#define RSG_NET16_CAT(a, b) RSG_NET16_CAT2(a, b)
+#define RSG_NET16_CAT2(a, b, c) a##b##c
+#define RSG_NET16_CAT(a, b, c) RSG_NET16_CAT2(a, b, c)
 
-// This part's launcher: false if pattern `pid` is instantiated elsewhere.
-bool RSG_NET16_CAT(launch_records_net16_part, RSG_NET_PART)(int pid, uint64_t blocks, const GfApplyParams& p,
-                                                            const HashParams& h, hipStream_t stream) {
-    if (pid < 0 || pid >= decnet16::kCount || !kNet16Part[pid]) return false;
+// This part's launcher (launch_records_net16_partN / launch_records_net12_partN):
+// false if pattern `pid` is instantiated elsewhere.
+bool RSG_NET16_CAT(launch_records_net, RSG_NET_K, RSG_NET16_CAT(_part, RSG_NET_PART, ))(int pid, uint64_t blocks,
+                                                                                  const GfApplyParams& p,
+                                                                                  const HashParams& h,
+                                                                                  hipStream_t stream) {
+    if (pid < 0 || pid >= decnetk::kCount || !kNet16Part[pid]) return false;
     kNet16Part[pid](blocks, p, h, stream);
     return true;
 }
 
 #if RSG_NET_PART == 0
-// The RS(16,4) pattern whose coefficient rows equal the launch's (R x 16,
-// row-major), or -1.
-int records_net16_pattern(int heal, int nf, int R, int n_store, const uint8_t* coef) {
-    for (int i = 0; i < decnet16::kCount; ++i) {
-        const decnet16::Pattern& pt = decnet16::kPatterns[i];
+// The pattern whose coefficient rows equal the launch's (R x K, row-major),
+// or -1 (records_net16_pattern / records_net12_pattern).
+int RSG_NET16_CAT(records_net, RSG_NET_K, _pattern)(int heal, int nf, int R, int n_store, const uint8_t* coef) {
+    for (int i = 0; i < decnetk::kCount; ++i) {
+        const decnetk::Pattern& pt = decnetk::kPatterns[i];
         if (pt.heal != heal || pt.nf != nf || pt.R != R || pt.n_store != n_store) continue;
         bool eq = true;
         for (int r = 0; r < R && eq; ++r)
-            for (int c = 0; c < 16 && eq; ++c) eq = pt.coef[r][c] == coef[r * 16 + c];
+            for (int c = 0; c < kNetK && eq; ++c) eq = pt.coef[r][c] == coef[r * kNetK + c];
         if (eq) return i;
     }
     return -1;

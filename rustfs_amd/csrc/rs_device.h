@@ -313,6 +313,8 @@ __device__ __forceinline__ void hhq_finish(HHQuad& s, uint8_t* out, uint32_t q) 
 
 __device__ __forceinline__ void st64_any(uint8_t* p, uint64_t v) { __builtin_memcpy(p, &v, 8); }
 
+__device__ __forceinline__ uint64_t u64_of(const uint2& v) { return (uint64_t)v.x | ((uint64_t)v.y << 32); }
+
 // The 8 bytes at p = shard + off of a shard of `len` bytes, those at or past
 // len read as zero (the partial last chunk of a shard of any length).
 __device__ __forceinline__ uint64_t ld64_part(const uint8_t* p, uint64_t off, uint64_t len) {

@@ -114,9 +114,9 @@ hipError_t launch_hh256(const HashParams& p, hipStream_t stream);
 // digest output [n][C+R][32].  Requires shard_len % 512 == 0, C <= 16, R <= 4
 // and 16-B aligned shards.
 bool fused_supported(int C, int R, uint64_t shard_len);
-// One-pass degraded GET (k_decode_records_dma) for RS(k, m), k in {2, 4, 8,
-// 16}, m <= 4, over nf (k..k+m-1) present record files: false if the shape
-// is not supported.
+// One-pass degraded GET (k_decode_records_dma) for RS(k, m), k <= 16, m <= 4,
+// any shard length (a ragged last step), over nf (k..k+m-1) present record
+// files: false if the shape is not supported.
 bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len);
 // coef: the launch's R x k coefficient rows (host memory, row-major), matched
 // against the compile-time XOR-network patterns (rs_decode_net.hip); may be null.
@@ -160,6 +160,20 @@ RSG_NET16_PART_DECL(4)
 RSG_NET16_PART_DECL(5)
 RSG_NET16_PART_DECL(6)
 RSG_NET16_PART_DECL(7)
+// RS(12,4) (the same source built with RSG_NET_K = 12, rs124_decode_nets.h)
+int records_net12_pattern(int heal, int nf, int R, int n_store, const uint8_t* coef);
+#define RSG_NET16_PART_DECL12(i)                                                                               \
+    bool launch_records_net12_part##i(int pid, uint64_t blocks, const GfApplyParams& p, const HashParams& h, \
+                                      hipStream_t stream);
+RSG_NET16_PART_DECL12(0)
+RSG_NET16_PART_DECL12(1)
+RSG_NET16_PART_DECL12(2)
+RSG_NET16_PART_DECL12(3)
+RSG_NET16_PART_DECL12(4)
+RSG_NET16_PART_DECL12(5)
+RSG_NET16_PART_DECL12(6)
+RSG_NET16_PART_DECL12(7)
+#undef RSG_NET16_PART_DECL12
 #undef RSG_NET16_PART_DECL
 // One-pass heal possible for this shape: the table kernel (k <= 8) or, for
 // RS(16,4), a listed network pattern (decided at launch: RSG_ERR_UNSUPPORTED

@@ -25,12 +25,33 @@ struct RecRing {
     static constexpr int TW = (SPW * TH + 15) / 16;               // target-hasher waves
 };
 
+// A record walk of shard_len S bytes takes steps = ceil(S / CH) steps of CH
+// bytes; the last one holds `tail` = S - (steps - 1) CH bytes (1..CH).  A
+// ragged walk (tail < CH: RS(12,4) at 1 MiB blocks has S = 87382, 170 whole
+// steps and 342 bytes) brings its last step in through registers, byte-exact
+// (nothing past a record body is read: the last record of a file may end the
+// caller's buffer), hashes its whole packets and then HighwayHash's
+// remainder packet; the GF waves store and compare only its first tail bytes.
+__device__ __forceinline__ uint32_t walk_tail(uint64_t S, uint32_t steps) {
+    return (uint32_t)(S - (uint64_t)(steps - 1) * dma::CH);
+}
+
+// The bytes of this lane's 8 at step offset `off` that lie before `valid`
+// (all ones when the whole 8 do; the partial last step's compares).
+__device__ __forceinline__ uint64_t part_mask8(uint32_t off, uint32_t valid) {
+    if (off >= valid) return 0ull;
+    if (off + 8 <= valid) return ~0ull;
+    return (1ull << (8 * (valid - off))) - 1ull;
+}
+
 // DMA + verify-hash wave hw of a workgroup whose first stripe is s0: brings
 // its (up to) 8 DMA instructions of every step into the ring D-1 steps ahead
 // and hashes both halves of each straight out of the ring (quad j: instruction
 // 8 hw + (j & 7), half j >> 3); at the end lane 0 of each live quad writes its
 // record's verify flag whole (no memset before the launch).  One barrier per
-// step: B(0) before step 0, B(s+1) after step s.
+// step: B(0) before step 0, B(s+1) after step s.  Record bodies may sit at any
+// address (LDS-DMA takes unaligned sources); a ragged walk's last step is
+// loaded by the same wave through registers (walk_tail).
 template <int NF, int G, int XB = 0>
 __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t wave_prio, uint8_t* ring,
                                                   uint32_t hw, uint32_t steps, uint64_t s0) {
@@ -50,6 +71,8 @@ __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t 
     const uint32_t file = quad_on ? idx / HS : 0, stripe_l = (idx % HS) + HS * half;
     const uint32_t roff = (quad_on ? idx : 0) * IP + half * CH + 8 * q;
     const bool live = quad_on && s0 + stripe_l < n;
+    const uint32_t tail = walk_tail(h.len, steps);
+    const bool ragged = tail != CH;
     HHQuad st;
     hhq_init(st, h.key, q);
     // record sources as a wave-uniform base (SGPRs) + a 32-bit per-lane
@@ -63,7 +86,9 @@ __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t 
         ubo[i] = (lo < n ? lo : 0) * h.stripe_stride;
         vlane[i] = (lane & 31u) * 16u + ((lane >> 5) && hi < n ? (uint32_t)(HS * h.stripe_stride) : 0u);
     }
-    auto dma_step = [&](uint32_t step) {
+    // DMA of one step; false (nothing issued) for a ragged walk's last step
+    auto dma_step = [&](uint32_t step) -> bool {
+        if (ragged && step + 1 == steps) return false;
         uint32_t voff[HS];
 #pragma unroll
         for (int i = 0; i < HS; ++i) voff[i] = vlane[i] + step * CH;
@@ -76,24 +101,79 @@ __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t 
                 (const void*)src, (__attribute__((address_space(3))) void*)(ring + (step % D) * L::DSLOT + ins * IP), 16,
                 0, 0);
         }
+        return true;
     };
-    auto wait_next = [&]() {  // DMA of the next step landed (D - 2 steps younger in flight)
-        if (ndi == 8) __builtin_amdgcn_s_waitcnt(vmcnt_imm((D - 2) * 8));
+    // the ragged last step through registers: 16 bytes per lane per
+    // instruction, zero past the record body, then into its ring slot
+    uint64_t tlo[8], thi[8];
+    auto tail_load = [&]() {
+        const uint32_t boff = (steps - 1) * CH + (lane & 31u) * 16u;  // offset in the record body
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (k >= ndi) break;
+            const uint32_t ins = 8 * hw + k;
+            const uint8_t* src = h.base[ins / HS] + ubo[k % HS] + (uint64_t)vlane[k % HS] + (steps - 1) * CH;
+            tlo[k] = ld64_part(src, boff, h.len);
+            thi[k] = ld64_part(src + 8, boff + 8, h.len);
+        }
+    };
+    auto tail_store = [&]() {
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (k >= ndi) break;
+            const uint32_t ins = 8 * hw + k;
+            *(uint4*)(ring + ((steps - 1) % D) * L::DSLOT + ins * IP + lane * 16u) =
+                make_uint4((uint32_t)tlo[k], (uint32_t)(tlo[k] >> 32), (uint32_t)thi[k], (uint32_t)(thi[k] >> 32));
+        }
+    };
+    // the next step's DMA has landed (D - 2 steps younger in flight); after a
+    // step with nothing issued, everything in flight
+    auto wait_next = [&](bool issued) {
+        if (!issued) __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+        else if (ndi == 8) __builtin_amdgcn_s_waitcnt(vmcnt_imm((D - 2) * 8));
         else __builtin_amdgcn_s_waitcnt(vmcnt_imm((D - 2) * L::LAST));
     };
+    bool issued = true;
 #pragma unroll
-    for (int d = 0; d < D - 1; ++d) dma_step(d < (int)steps ? d : steps - 1);
-    wait_next();  // DMA(0) landed
+    for (int d = 0; d < D - 1; ++d) issued = dma_step(d < (int)steps ? d : steps - 1);
+    if (ragged && steps == 1) {  // the only step is the ragged one
+        tail_load();
+        tail_store();
+    }
+    wait_next(issued);  // DMA(0) landed
     lds_barrier();  // B(0)
 #pragma unroll 1
-    for (uint32_t s = 0; s < steps; ++s) {
-        dma_step(s + D - 1 < steps ? s + D - 1 : steps - 1);  // into the slot step s-1 used
+    for (uint32_t s = 0; s + 1 < steps; ++s) {
+        issued = dma_step(s + D - 1 < steps ? s + D - 1 : steps - 1);  // into the slot step s-1 used
+        const bool fill = ragged && s + 2 == steps;  // the ragged last step is next
+        if (fill) tail_load();
         uint64_t w[16];
         dma::read16(ring_base + (s % D) * L::DSLOT + roff, w);
 #pragma unroll
         for (int t = 0; t < 16; ++t) hhq_update(st, w[t]);
-        wait_next();
+        if (fill) tail_store();
+        wait_next(issued);
         lds_barrier();  // B(s+1)
+    }
+    {  // the last step (whole or ragged: its whole packets, then the remainder packet)
+        const uint32_t s = steps - 1;
+        if (!ragged) (void)dma_step(s);  // the clamped tail DMA (keeps every wave's count uniform)
+        uint64_t w[16];
+        dma::read16(ring_base + (s % D) * L::DSLOT + roff, w);
+        if (!ragged) {
+#pragma unroll
+            for (int t = 0; t < 16; ++t) hhq_update(st, w[t]);
+        } else {
+            const uint32_t full = tail / 32;
+#pragma unroll
+            for (int t = 0; t < 16; ++t)
+                if ((uint32_t)t < full) hhq_update(st, w[t]);  // wave-uniform
+            if (tail % 32)
+                hhq_remainder(st, (const uint8_t*)ring + (s % D) * L::DSLOT + roff - 8 * q + full * 32, tail % 32, q);
+        }
+        wait_next(!ragged);
+        lds_barrier();  // B(steps)
     }
     __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // the clamped tail DMA has landed before the wave ends
 #pragma unroll
@@ -127,16 +207,27 @@ __device__ __forceinline__ void records_target_hasher(const GfApplyParams& p, co
     const uint32_t r = on ? pi / SPW : 0, e = pi % SPW;
     const bool live = on && s0 + e < h.n;
     const uint32_t roff = (on ? pi : 0) * dma::PP + 8 * q;
+    const uint32_t tail = walk_tail(h.len, steps);
     HHQuad st;
     hhq_init(st, h.key, q);
     lds_barrier();  // B(0)
 #pragma unroll 1
     for (uint32_t t = 0; t < steps + LAG; ++t) {
         if (t >= (uint32_t)LAG) {  // target rows of step t-LAG, published by B(t)
+            const uint32_t base = (uint32_t)(uintptr_t)trow + ((t - LAG) & 1) * TSLOT + roff;
             uint64_t w[16];
-            dma::read16((uint32_t)(uintptr_t)trow + ((t - LAG) & 1) * TSLOT + roff, w);
+            dma::read16(base, w);
+            if (t - LAG + 1 < steps || tail == dma::CH) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) hhq_update(st, w[i]);
+                for (int i = 0; i < 16; ++i) hhq_update(st, w[i]);
+            } else {  // the ragged last step: whole packets, then the remainder packet
+                const uint32_t full = tail / 32;
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    if ((uint32_t)i < full) hhq_update(st, w[i]);  // wave-uniform
+                if (tail % 32)
+                    hhq_remainder(st, trow + ((t - LAG) & 1) * TSLOT + roff - 8 * q + full * 32, tail % 32, q);
+            }
         }
         if (t + 1 < steps + LAG) lds_barrier();  // B(t+1)
     }

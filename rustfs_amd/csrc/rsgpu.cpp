@@ -1533,12 +1533,9 @@ int get_begin(RecJob& j) {
                       lost_data + (j.verify_surplus ? surplus : 0) <= rsg::kMaxR && lost_disk_fast_enabled();
     if (fast) {
         j.phase = RecJob::FAST;
-        bool one_pass = get_dma_enabled(j.ctx, n) && rsg::decode_dma_supported(k, m, nfiles, j.S) && j.rec % 16 == 0;
-        for (int i : all_idx) one_pass = one_pass && (uintptr_t)(j.files[i] + 32) % 16 == 0;
-        if (j.out.into()) {  // the kernels' 8-byte row stores
-            one_pass = one_pass && j.out.tstride % 8 == 0;
-            for (int i = 0; i < k; ++i) one_pass = one_pass && (j.present0[i] || (uintptr_t)j.out.tg[i] % 8 == 0);
-        }
+        // (record files and slots at any alignment: the ring's LDS-DMA and
+        // the kernels' 8-byte stores take unaligned addresses)
+        const bool one_pass = get_dma_enabled(j.ctx, n) && rsg::decode_dma_supported(k, m, nfiles, j.S);
         j.one_pass = one_pass;
         if (one_pass) {
             // verify every present record, rebuild (and gather) and check
@@ -1778,9 +1775,8 @@ int heal_begin(RecJob& j) {
     }
     j.phase = RecJob::FAST;
     bool one_pass = get_dma_enabled(j.ctx, n) &&
-                    rsg::heal_one_pass_shape(k, m, (int)all_idx.size(), (int)tg_idx.size(), j.S) && j.rec % 16 == 0;
-    for (int i : all_idx) one_pass = one_pass && (uintptr_t)(j.files[i] + 32) % 16 == 0;
-    for (int i : tg_idx) one_pass = one_pass && !j.files[i] && (uintptr_t)(j.targets[i] + 32) % 8 == 0;
+                    rsg::heal_one_pass_shape(k, m, (int)all_idx.size(), (int)tg_idx.size(), j.S);
+    for (int i : tg_idx) one_pass = one_pass && !j.files[i];
     if (one_pass) {
         j.sc->tmark(j.s);
         st = launch_heal_one_pass(j, all_idx, tg_idx);

@@ -103,6 +103,9 @@ def test_decode_records_detects_inconsistent_parity(gpu, oracle, form):
     (8, 4, 512, 17, (0,)), (8, 4, 512, 3, (1, 2, 3, 4)), (8, 4, 1024, 8, (7, 8, 9)), (8, 4, 4608, 11, (6,)),
     (16, 4, 4096, 9, (0,)), (16, 4, 4096, 5, (3, 17)), (16, 4, 512, 13, (0, 5, 9, 15)), (16, 2, 1024, 4, (15,)),
     (16, 4, 65536, 6, (2, 11)), (2, 4, 2048, 6, (0, 1)), (4, 4, 1024, 5, (1, 2, 6)), (2, 2, 524288, 3, (1,)),
+    # ragged walks (S not a multiple of 512) at rustfs's default set geometries, 1 MiB blocks
+    (12, 4, 87382, 5, (0, 13)), (12, 4, 87382, 3, (4, 5, 6)), (10, 4, 104858, 3, (1,)), (6, 4, 174763, 3, (0, 2)),
+    (6, 3, 3001, 4, (5,)), (8, 4, 100, 9, (0,)), (8, 4, 1, 5, (7,)), (4, 2, 31, 7, (0,)),
 ])
 def test_decode_records_lost_disk_one_pass(gpu, oracle, form, k, m, S, n, lost):
     """A lost disk (whole data shard files missing) takes the one-pass GET

@@ -205,6 +205,96 @@ def _rs16_pattern(oracle, records16, heal, lost, form):
             assert np.array_equal(tgt2[i].cpu().numpy().reshape(N16, REC)[keep], recs[i][keep]), f"shard {i}"
 
 
+# ---------------------------------------------------------------- RS(12,4)
+# the default geometry of a 16-drive set (storageclass.rs:24-31); S12 = 1000:
+# a ragged walk (one whole 512-byte step and 488 bytes), records at every
+# alignment (pitch 1032)
+K12, T12, N12, S12 = 12, 16, 11, 1000
+REC12 = 32 + S12
+LISTED12 = _listed("rs124_decode_nets.h", T12)
+
+
+@pytest.fixture(scope="module")
+def records12(gpu, oracle):
+    import torch
+    rng = np.random.default_rng(124)
+    shards = np.zeros((N12, T12, S12), dtype=np.uint8)
+    recs = np.zeros((T12, N12, REC12), dtype=np.uint8)
+    for s in range(N12):
+        shards[s, :K12] = rng.integers(0, 256, (K12, S12), dtype=np.uint8)
+        oracle.encode(K12, 4, shards[s])
+        for i in range(T12):
+            recs[i, s, :32] = np.frombuffer(oracle.hh256s(shards[s, i].tobytes()), dtype=np.uint8)
+            recs[i, s, 32:] = shards[s, i]
+    files = [torch.from_numpy(recs[i].reshape(-1).copy()).cuda() for i in range(T12)]
+    return shards, recs, files
+
+
+def _rehashed12(torch, oracle, f, stripe, pos):
+    bad = f.clone()
+    body = bad[stripe * REC12 + 32:(stripe + 1) * REC12].cpu().numpy().copy()
+    body[pos] ^= 0x20
+    bad[stripe * REC12 + 32:(stripe + 1) * REC12] = torch.from_numpy(body).cuda()
+    bad[stripe * REC12:stripe * REC12 + 32] = torch.from_numpy(
+        np.frombuffer(oracle.hh256s(body.tobytes()), dtype=np.uint8).copy()).cuda()
+    return bad
+
+
+def test_rs12_table_lists_every_pattern():
+    """Every one- and two-shard loss of RS(12,4): 12 + 114 GET patterns (a
+    data shard among the lost) and 16 + 120 heal patterns."""
+    assert len([x for x in LISTED12 if not x[0]]) == 12 + 114
+    assert len([x for x in LISTED12 if x[0]]) == 16 + 120
+
+
+@pytest.mark.parametrize("heal,lost", LISTED12, ids=lambda x: str(x))
+def test_rs12_every_listed_pattern(gpu, oracle, records12, one_pass, heal, lost):
+    """k_decode_records_net16 built for RS(12,4) (two networks over survivors
+    0-7 and 8-11), on a ragged walk: GET in both forms and heal, bit-exact
+    against the oracle, with an altered surplus parity (in the ragged last
+    step) reported for its stripe alone."""
+    import torch
+    from rustfs_amd import Erasure, _lib
+    shards, recs, files = records12
+    e = Erasure(K12, 4, K12 * S12)
+    present = [i for i in range(T12) if i not in lost]
+    sur = present[K12:]
+    if not heal:
+        want = torch.from_numpy(shards[:, :K12].reshape(N12, K12 * S12).copy()).cuda()
+        f = [None if i in lost else files[i] for i in range(T12)]
+        for form in FORMS:
+            out, status = decode_get(e, f, S12, N12, form)
+            assert status == [0] * N12 and torch.equal(out, want), form
+        if sur:
+            stripe = sum(lost) % N12
+            f2 = list(f)
+            f2[sur[-1]] = _rehashed12(torch, oracle, files[sur[-1]], stripe, 600 + sum(lost))
+            for form in FORMS:
+                out, status = decode_get(e, f2, S12, N12, form)
+                assert [i for i, x in enumerate(status) if x] == [stripe], form
+                assert status[stripe] == _lib.RSG_ERR_INCONSISTENT_SOURCES
+                ok = torch.ones(N12, dtype=torch.bool, device="cuda")
+                ok[stripe] = False
+                assert torch.equal(out[ok], want[ok])
+        return
+    src = [None if i in lost else files[i] for i in range(T12)]
+    tgt = [torch.zeros(N12 * REC12, dtype=torch.uint8, device="cuda") if i in lost else None for i in range(T12)]
+    assert e.heal_records_batch(src, tgt, S12, N12) == [0] * N12
+    for i in lost:
+        assert np.array_equal(tgt[i].cpu().numpy().reshape(N12, REC12), recs[i]), f"shard {i}"
+    if sur:
+        stripe = (5 * sum(lost) + 1) % N12
+        src2 = list(src)
+        src2[sur[0]] = _rehashed12(torch, oracle, files[sur[0]], stripe, 7 * sum(lost) % S12)
+        tgt2 = [torch.zeros(N12 * REC12, dtype=torch.uint8, device="cuda") if i in lost else None for i in range(T12)]
+        status = e.heal_records_batch(src2, tgt2, S12, N12)
+        assert [i for i, x in enumerate(status) if x] == [stripe]
+        assert status[stripe] == _lib.RSG_ERR_INCONSISTENT_SOURCES
+        keep = [s for s in range(N12) if s != stripe]
+        for i in lost:
+            assert np.array_equal(tgt2[i].cpu().numpy().reshape(N12, REC12)[keep], recs[i][keep]), f"shard {i}"
+
+
 def test_rs16_heal_unlisted_pattern_falls_back(gpu, oracle, records16, one_pass):
     """A heal the network table does not list (three lost shards) takes the
     two-pass path even with the one-pass engine forced: still bit-exact."""
@@ -274,14 +364,14 @@ def test_network_knobs_in_own_process(gpu, oracle, env):
 SL = 4096  # 8 steps of 512 B: the 3-slot ring, the A/B exchange and the trailing target hashers wrap
 
 
-def _long_records(oracle, k, n, seed):
+def _long_records(oracle, k, n, seed, S=SL):
     import torch
     t = k + 4
     rng = np.random.default_rng(seed)
-    shards = np.zeros((n, t, SL), dtype=np.uint8)
-    recs = np.zeros((t, n, 32 + SL), dtype=np.uint8)
+    shards = np.zeros((n, t, S), dtype=np.uint8)
+    recs = np.zeros((t, n, 32 + S), dtype=np.uint8)
     for s in range(n):
-        shards[s, :k] = rng.integers(0, 256, (k, SL), dtype=np.uint8)
+        shards[s, :k] = rng.integers(0, 256, (k, S), dtype=np.uint8)
         oracle.encode(k, 4, shards[s])
         for i in range(t):
             recs[i, s, :32] = np.frombuffer(oracle.hh256s(shards[s, i].tobytes()), dtype=np.uint8)
@@ -294,6 +384,19 @@ LONG = [(8, 19, 0, (0,)), (8, 19, 0, (0, 3)), (8, 19, 0, (2, 9)), (8, 19, 0, (6,
         (8, 19, 1, (8,)), (8, 19, 1, (5,)), (8, 19, 1, (1, 8)), (8, 19, 1, (0, 5)), (8, 19, 1, (9, 11)),
         (16, 11, 0, (3,)), (16, 11, 0, (2, 11)), (16, 11, 0, (4, 17)),
         (16, 11, 1, (17,)), (16, 11, 1, (1, 16)), (16, 11, 1, (0, 5)), (16, 11, 1, (7,))]
+# ragged walks at the production shard sizes: RS(12,4) at 1 MiB (S = 87382,
+# 170 steps + 342 bytes) and RS(8,4) with a ragged tail (S = 4100)
+LONG_RAGGED = [(12, 5, 0, (0,), 87382), (12, 5, 0, (2, 13), 87382), (12, 5, 1, (3, 14), 87382),
+               (12, 5, 1, (15,), 87382), (12, 6, 0, (5, 7), 4100), (8, 9, 0, (0, 3), 4100), (8, 9, 1, (1, 8), 4100),
+               (8, 9, 0, (2,), 4100), (16, 5, 0, (4, 17), 65540), (16, 5, 1, (1, 16), 65540)]
+
+
+@pytest.mark.parametrize("k,n,heal,lost,S", LONG_RAGGED, ids=str)
+def test_long_ragged_walks(gpu, oracle, one_pass, k, n, heal, lost, S):
+    """Ragged record walks (S not a multiple of the 512-byte step, records at
+    every alignment) through the network kernels: GET in both forms and heal,
+    bit-exact; an inconsistent surplus flagged in the last stripe."""
+    _long_case(oracle, k, n, heal, lost, S)
 
 
 @pytest.mark.parametrize("k,n,heal,lost", LONG, ids=str)
@@ -302,10 +405,14 @@ def test_long_shards_every_shape(gpu, oracle, one_pass, k, n, heal, lost):
     3-slot ring; here one pattern of each kernel shape runs 8 steps, GET in
     both forms and heal, bit-exact against the oracle, with an inconsistent
     surplus caught for its stripe alone."""
+    _long_case(oracle, k, n, heal, lost, SL)
+
+
+def _long_case(oracle, k, n, heal, lost, SL):
     import torch
     from rustfs_amd import Erasure, _lib
     t = k + 4
-    shards, recs, files = _long_records(oracle, k, n, seed=k * 100 + sum(lost))
+    shards, recs, files = _long_records(oracle, k, n, seed=k * 100 + sum(lost), S=SL)
     e = Erasure(k, 4, k * SL)
     rec = 32 + SL
     present = [i for i in range(t) if i not in lost]
