@@ -86,6 +86,23 @@ __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t 
         ubo[i] = (lo < n ? lo : 0) * h.stripe_stride;
         vlane[i] = (lane & 31u) * 16u + ((lane >> 5) && hi < n ? (uint32_t)(HS * h.stripe_stride) : 0u);
     }
+    // the last step's hash: 16 packets from the ring (a ragged step: its
+    // whole packets, then the remainder packet)
+    auto hash_step = [&](uint32_t s) {
+        uint64_t w[16];
+        dma::read16(ring_base + (s % D) * L::DSLOT + roff, w);
+        if (!ragged || s + 1 < steps) {
+#pragma unroll
+            for (int t = 0; t < 16; ++t) hhq_update(st, w[t]);
+        } else {
+            const uint32_t full = tail / 32;
+#pragma unroll
+            for (int t = 0; t < 16; ++t)
+                if ((uint32_t)t < full) hhq_update(st, w[t]);  // wave-uniform
+            if (tail % 32)
+                hhq_remainder(st, (const uint8_t*)ring + (s % D) * L::DSLOT + roff - 8 * q + full * 32, tail % 32, q);
+        }
+    };
     // DMA of one step; false (nothing issued) for a ragged walk's last step
     auto dma_step = [&](uint32_t step) -> bool {
         if (ragged && step + 1 == steps) return false;
@@ -159,19 +176,7 @@ __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t 
     {  // the last step (whole or ragged: its whole packets, then the remainder packet)
         const uint32_t s = steps - 1;
         if (!ragged) (void)dma_step(s);  // the clamped tail DMA (keeps every wave's count uniform)
-        uint64_t w[16];
-        dma::read16(ring_base + (s % D) * L::DSLOT + roff, w);
-        if (!ragged) {
-#pragma unroll
-            for (int t = 0; t < 16; ++t) hhq_update(st, w[t]);
-        } else {
-            const uint32_t full = tail / 32;
-#pragma unroll
-            for (int t = 0; t < 16; ++t)
-                if ((uint32_t)t < full) hhq_update(st, w[t]);  // wave-uniform
-            if (tail % 32)
-                hhq_remainder(st, (const uint8_t*)ring + (s % D) * L::DSLOT + roff - 8 * q + full * 32, tail % 32, q);
-        }
+        hash_step(s);
         wait_next(!ragged);
         lds_barrier();  // B(steps)
     }

@@ -14,8 +14,9 @@ def main():
     from rustfs_amd import Erasure
     what = sys.argv[1] if len(sys.argv) > 1 else "get2"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-    k, m, n = 8, 4, 4096
-    S, t = 131072, 12
+    k = int(os.environ.get("EP_K", "8"))  # EP_K=12: RS(12,4), the 16-drive default (ragged walks)
+    m, n = 4, 4096
+    S, t = -(-(1 << 20) // k), k + 4
     rec = 32 + S
     e = Erasure(k, m, 1 << 20)
     early = os.environ.get("EP_FILES_FIRST") == "1"  # allocate the record files and output before the staging
