@@ -2,8 +2,7 @@
 # Round-4 GPU pass B: the unaligned LDS-DMA probe gates everything after it
 # (the one-pass kernels DMA records at any alignment); then the GPU suite,
 # smoke, the default bench line and the RS(12,4) line, rocprof kernel stats
-# of the RS(8,4) and RS(12,4) engine calls, and the register-prefetch A/B
-# (rustfs_amd/exp_pf4/librsgpu.so, RSG_REC_PREFETCH=4).
+# of the RS(8,4) and RS(12,4) engine calls.
 # Usage: bash tools/gpu_r4b.sh TAG [skip-tests]
 set -o pipefail
 TAG=${1:-r4b}
@@ -25,7 +24,6 @@ cd /tmp
 for k in 8 12; do
   for what in into0 into2 heal; do
     EP_K=$k timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $OUT/k${k}_$what -o run --output-format csv -- python3 $R/tools/engine_prof.py $what 10 > $OUT/k${k}_$what.txt 2>&1 || exit $?
-    RSG_LIB_PATH=$R/rustfs_amd/exp_pf4/librsgpu.so EP_K=$k timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $OUT/pf4_k${k}_$what -o run --output-format csv -- python3 $R/tools/engine_prof.py $what 10 > $OUT/pf4_k${k}_$what.txt 2>&1 || exit $?
   done
 done
 echo done
