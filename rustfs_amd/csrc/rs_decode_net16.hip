@@ -62,6 +62,13 @@ struct Net16Shape : RecRing<NF, 4, TH> {
     static constexpr int WAVES = RecRing<NF, 4, TH>::HW + NG + RecRing<NF, 4, TH>::TW;
     static constexpr uint32_t XSLOT = 32 * 64 * 4;  // a step's exchanged partial planes, lane-major (<= 8 KiB)
     static constexpr int XB = TH ? 1 : 0;           // extra barrier: heal's target hashers trail by 2 steps
+    // ring slots: 4 (three steps of DMA in flight) where the LDS holds them —
+    // every RS(12,4) shape (14-15 files) — else 3 (RS(16,4): 18-19 files).
+    // The walk is bound by the record bytes in flight per CU (a step takes
+    // about half the loaded HBM latency with two steps in flight), and the
+    // ring is what holds them.
+    static constexpr uint32_t LDS_REST = 4 * XSLOT + (TH ? 2 * RecRing<NF, 4, TH>::TSLOT : 16);
+    static constexpr int RD = 4 * RecRing<NF, 4, TH>::DSLOT + LDS_REST <= 160 * 1024 ? 4 : 3;
 };
 
 __device__ __forceinline__ void put8_16(uint8_t* p, const uint2& v) { st64_any(p, u64_of(v)); }  // any alignment
@@ -80,10 +87,10 @@ template <int PID, int NF, int TH, bool A>
 __device__ __forceinline__ void net16_wave(const GfApplyParams& p, uint64_t n, uint32_t steps, uint64_t s0,
                                            const uint8_t* ring, uint8_t* xbuf, uint8_t* trow) {
     using dma::CH;
-    using dma::D;
     using dma::IP;
     using dma::PP;
     using L = Net16Shape<NF, TH>;
+    constexpr int D = L::RD;
     constexpr decnetk::Pattern pat = decnetk::kPatterns[PID];
     constexpr int R = pat.R, NST = pat.n_store, NCMP = R - NST, SPW = L::SPW, HS = L::HS;
     static_assert(pat.nf == NF && (pat.heal ? NST : 0) == TH && R <= 4 && NST <= R && HS == 2, "pattern shape");
@@ -235,7 +242,7 @@ template <int PID, int NF, int TH>
 __global__ __launch_bounds__((64 * Net16Shape<NF, TH>::WAVES)) void k_decode_records_net16(const GfApplyParams p,
                                                                                            const HashParams h) {
     using L = Net16Shape<NF, TH>;
-    __shared__ __attribute__((aligned(16))) uint8_t ring[dma::D * L::DSLOT];
+    __shared__ __attribute__((aligned(16))) uint8_t ring[L::RD * L::DSLOT];
     __shared__ __attribute__((aligned(16))) uint8_t xbuf[4 * L::XSLOT];
     __shared__ __attribute__((aligned(16))) uint8_t trow[TH ? 2 * L::TSLOT : 16];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -253,9 +260,13 @@ __global__ __launch_bounds__((64 * Net16Shape<NF, TH>::WAVES)) void k_decode_rec
         net16_wave<PID, NF, TH, false>(p, h.n, steps, s0, ring, xbuf, trow);
         return;
     }
-    records_hash_wave<NF, 4, L::XB>(h, p.wave_prio, ring, wave, steps, s0);
+    records_hash_wave<NF, 4, L::XB, L::RD>(h, p.wave_prio, ring, wave, steps, s0);
 }
 
+static_assert(Net16Shape<19, 0>::RD * Net16Shape<19, 0>::DSLOT + Net16Shape<19, 0>::LDS_REST <= 160 * 1024 &&
+                  Net16Shape<14, 2>::RD == 4 && Net16Shape<15, 1>::RD == 4 && Net16Shape<14, 0>::RD == 4 &&
+                  Net16Shape<15, 0>::RD == 4 && Net16Shape<18, 0>::RD == 3,
+              "ring depth: 4 slots for RS(12,4), 3 for RS(16,4)");
 static_assert(dma::D * 2 * 19 * dma::IP + 4 * Net16Shape<19, 0>::XSLOT + 16 <= 160 * 1024, "RS(16,4) GET fits");
 static_assert(dma::D * 2 * 18 * dma::IP + 4 * Net16Shape<18, 2>::XSLOT + 2 * Net16Shape<18, 2>::TSLOT <= 160 * 1024,
               "RS(16,4) heal fits");

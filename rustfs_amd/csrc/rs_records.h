@@ -45,19 +45,19 @@ __device__ __forceinline__ uint64_t part_mask8(uint32_t off, uint32_t valid) {
 }
 
 // DMA + verify-hash wave hw of a workgroup whose first stripe is s0: brings
-// its (up to) 8 DMA instructions of every step into the ring D-1 steps ahead
+// its (up to) 8 DMA instructions of every step into the RD-slot ring RD-1 steps ahead
 // and hashes both halves of each straight out of the ring (quad j: instruction
 // 8 hw + (j & 7), half j >> 3); at the end lane 0 of each live quad writes its
 // record's verify flag whole (no memset before the launch).  One barrier per
 // step: B(0) before step 0, B(s+1) after step s.  Record bodies may sit at any
 // address (LDS-DMA takes unaligned sources); a ragged walk's last step is
 // loaded by the same wave through registers (walk_tail).
-template <int NF, int G, int XB = 0>
+template <int NF, int G, int XB = 0, int RD = dma::D>
 __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t wave_prio, uint8_t* ring,
                                                   uint32_t hw, uint32_t steps, uint64_t s0) {
     using dma::CH;
-    using dma::D;
     using dma::IP;
+    constexpr int D = RD;  // ring slots: D - 1 steps of DMA in flight
     using dma::vmcnt_imm;
     using L = RecRing<NF, G>;
     constexpr int HS = L::HS;
