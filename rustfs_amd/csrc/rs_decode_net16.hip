@@ -55,6 +55,11 @@ namespace decnetk = decnet12;
 #error "RSG_NET_K is 16 or 12"
 #endif
 constexpr int kNetK = RSG_NET_K;
+// survivors of network wave A (the rest are B's): 8 of RS(16,4)'s 16, 6 of
+// RS(12,4)'s 12 — equal halves, so the two waves transpose and combine the
+// same number of rows (8 / 4 left wave A alone on the critical path: RS(12,4)
+// GET with 2 data lost 1.80 ms, profiles/r04/c/)
+constexpr int kNetA = kNetK == 12 ? 6 : 8;
 
 template <int NF, int TH>
 struct Net16Shape : RecRing<NF, 4, TH> {
@@ -94,11 +99,11 @@ __device__ __forceinline__ void net16_wave(const GfApplyParams& p, uint64_t n, u
     constexpr decnetk::Pattern pat = decnetk::kPatterns[PID];
     constexpr int R = pat.R, NST = pat.n_store, NCMP = R - NST, SPW = L::SPW, HS = L::HS;
     static_assert(pat.nf == NF && (pat.heal ? NST : 0) == TH && R <= 4 && NST <= R && HS == 2, "pattern shape");
-    constexpr int C0 = A ? 0 : 8, NC = A ? 8 : kNetK - 8;  // this wave's survivors [C0, C0 + NC)
-    // heal (SF): A finishes the stored rows, B the compared ones; GET: A
-    // finishes every row (B holding half the rows as well as GET's
-    // copy-through spilled at the 256-VGPR cap)
-    constexpr bool SF = TH > 0;
+    constexpr int C0 = A ? 0 : kNetA, NC = A ? kNetA : kNetK - kNetA;  // this wave's survivors [C0, C0 + NC)
+    // heal and RS(12,4) (SF): A finishes the stored rows, B the compared
+    // ones; RS(16,4) GET: A finishes every row (B holding half the rows as
+    // well as GET's copy-through spilled at the 256-VGPR cap)
+    constexpr bool SF = TH > 0 || kNetK == 12;
     constexpr int K0 = A ? 0 : NST, KN = A ? (SF ? NST : R) : (SF ? NCMP : 0);  // rows it finishes
     constexpr int G0 = A ? NST : 0, GN = A ? (SF ? NCMP : 0) : (SF ? NST : R);  // rows it gives away
     constexpr bool CMP = K0 + KN > NST;  // it finishes compared rows (keeps the surplus rows, writes verdicts)
@@ -133,7 +138,7 @@ __device__ __forceinline__ void net16_wave(const GfApplyParams& p, uint64_t n, u
     // the other wave's rows out to LDS; copy-through of its data survivors (GET)
     auto half = [&](uint32_t t) {
         const uint8_t* slot = ring + (t % D) * L::DSLOT + lane * 8u;
-        uint32_t P[64];  // B of RS(12,4): planes [0, 32) only
+        uint32_t P[64];  // RS(12,4): planes [0, 48) only
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             uint2 a[4];

@@ -27,7 +27,7 @@ struct Tuning {
     bool fused = true;            // RSG_FUSED=0: encode, then a separate hash launch
     bool lost_disk_fast = true;   // RSG_LOST_DISK_FAST=0: general GET/heal order
     bool zero_copy = true;        // RSG_ZERO_COPY=0: stage pinned blocks through device memory
-    int vec_block = 64;           // RSG_VEC_BLOCK=256: 4-wave GF workgroups
+    int vec_block = 0;            // RSG_VEC_BLOCK=64|256: GF workgroup size for every launch (0: by layout)
     int vec_occ = -1;             // RSG_VEC_OCC=<0..8>: waves per SIMD for every GF launch (-1: default rule)
     bool rolled = false;          // RSG_ROLLED=1: rolled GF kernel for every C
     bool hash_direct_copy = false;  // RSG_HASH_COPY=1: 8-byte copy stores in the GET gather

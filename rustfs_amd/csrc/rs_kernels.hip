@@ -1130,7 +1130,8 @@ const Tuning& tuning() {
         v.fused = flag("RSG_FUSED", true);
         v.lost_disk_fast = flag("RSG_LOST_DISK_FAST", true);
         v.zero_copy = flag("RSG_ZERO_COPY", true);
-        v.vec_block = num("RSG_VEC_BLOCK", 64, 64, 256) == 256 ? 256 : 64;
+        v.vec_block = num("RSG_VEC_BLOCK", 0, 64, 256);
+        if (v.vec_block != 0 && v.vec_block != 256) v.vec_block = 64;
         v.vec_occ = num("RSG_VEC_OCC", -1, 0, 8);
         v.rolled = flag("RSG_ROLLED", false);
         v.hash_direct_copy = flag("RSG_HASH_COPY", false);
@@ -1197,7 +1198,23 @@ static GfKernel pick_vec_b(int C, int R) {
     return nullptr;
 }
 
-static int vec_block() { return tuning().vec_block; }
+// Workgroup size of a vector GF launch.  One-wave workgroups (the
+// dispatcher refills a SIMD wave by wave; RS(8,4) encode 1.090 -> 1.066 ms,
+// RS(16,4) 0.959 -> 0.934 ms, profiles/r02/ab_block/) where every shard row
+// starts on a 128-byte line; four-wave workgroups where any does not — each
+// workgroup's 16-byte loads of a shard span one contiguous run, and a run
+// that starts mid-line touches one line more than its length needs: 9 lines
+// per KiB for one wave, 33 per 4 KiB for four (RS(12,4) at 1 MiB blocks, S =
+// 87382: encode 1.274 -> 1.112 ms, 0.562 -> 0.644 of HBM,
+// profiles/r04/c/enc12_ab.txt).  Tuning::vec_block forces one for A/B runs.
+static int vec_block_for(const GfApplyParams& p) {
+    if (tuning().vec_block) return tuning().vec_block;
+    bool lines = (uintptr_t)p.base % 128 == 0 && (uintptr_t)p.out_base % 128 == 0 && p.stripe_stride % 128 == 0 &&
+                 p.out_stripe_stride % 128 == 0;
+    for (uint32_t c = 0; c < p.C && lines; ++c) lines = p.in_off[c] % 128 == 0;
+    for (uint32_t r = 0; r < p.R && lines; ++r) lines = p.out_off[r] % 128 == 0;
+    return lines ? 64 : 256;
+}
 
 // Resident waves per SIMD for a vector GF launch, imposed through padding LDS
 // (0 = as many as the registers allow; enforced with an otherwise unused
@@ -1211,8 +1228,8 @@ static int vec_occupancy(int C, int R, bool pre) {
     return (!pre && C == 8 && R <= 2) ? 2 : 0;
 }
 
-static GfKernel pick_vec(int C, int R, bool pre) {
-    if (vec_block() == 256) return pre ? pick_vec_b<256, true>(C, R) : pick_vec_b<256, false>(C, R);
+static GfKernel pick_vec(int C, int R, bool pre, int B) {
+    if (B == 256) return pre ? pick_vec_b<256, true>(C, R) : pick_vec_b<256, false>(C, R);
     return pre ? pick_vec_b<64, true>(C, R) : pick_vec_b<64, false>(C, R);
 }
 
@@ -1232,9 +1249,9 @@ static GfKernel pick_byte(int R) {
 
 hipError_t launch_gf_apply_vec(GfApplyParams p, uint64_t n_stripes, hipStream_t stream) {
     const bool pre = p.mode != GF_MODE_STORE || p.copy_mask != 0;
-    GfKernel k = pick_vec((int)p.C, (int)p.R, pre);
+    const uint32_t B = (uint32_t)vec_block_for(p);
+    GfKernel k = pick_vec((int)p.C, (int)p.R, pre, (int)B);
     if (!k || p.units == 0 || n_stripes == 0) return hipErrorInvalidValue;
-    const uint32_t B = (uint32_t)vec_block();
     p.chunks_per_stripe = (p.units + B - 1) / B;
     const uint64_t blocks = (uint64_t)p.chunks_per_stripe * n_stripes;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;

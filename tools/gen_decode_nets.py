@@ -26,8 +26,8 @@ listed (or any disagreement) keeps the run-time-table kernel.
 RS(16,4) (`--k 16`) and RS(12,4) (`--k 12`, the default geometry of a
 16-drive set, storageclass.rs:24-31): the survivors' 128 / 96 planes do not
 fit one wave's registers beside the rows, so each pattern gets TWO networks,
-one over survivors 0-7 and one over survivors 8..k-1, each producing all R
-rows; the kernel XORs the two halves (rs_decode_net16.hip) — headers
+one over survivors 0-7 (RS(12,4): 0-5) and one over the rest, each producing
+all R rows; the kernel XORs the two halves (rs_decode_net16.hip) — headers
 rs164_decode_nets.h / rs124_decode_nets.h.
 
 Usage: python tools/gen_decode_nets.py [seeds] [--k 16|12] [--only heal:1,16 get:0,3 ...]
@@ -205,7 +205,10 @@ def main():
     pats = patterns()
     if only:  # prototype builds: e.g. heal:1,16 get:0,3
         pats = [p for p in pats if f"{'heal' if p[1] else 'get'}:{','.join(str(i) for i in range(T) if p[0] >> i & 1)}" in only]
-    halves = [(0, 8)] if K == 8 else [(0, 8), (8, K - 8)]
+    # RS(16,4): survivors 0-7 / 8-15; RS(12,4): 0-5 / 6-11 (the two network
+    # waves then transpose and combine equal halves, rs_decode_net16.hip)
+    ka = K // 2 if K == 12 else 8
+    halves = [(0, 8)] if K == 8 else [(0, ka), (ka, K - ka)]
     tasks = [(p[5], seeds, c0, cn) for c0, cn in halves for p in pats]
     with multiprocessing.Pool(min(8, os.cpu_count() or 1)) as pool:
         res = pool.map(best_network, tasks)
@@ -217,7 +220,7 @@ def main():
         f"// RS({K},{M}) one-pass GET / heal rows as compile-time three-input XOR networks,",
         f"// one per erasure pattern of one or two lost shards: {len(pats)} patterns,",
         f"// {min(ops)}-{max(ops)} ops each (mean {sum(ops) / len(ops):.0f}).  P[c*8+j] = bit plane j of",
-        f"// survivor c (the first {K} present shards{'' if K == 8 else f', in halves 0-7 and 8-{K - 1}'}), O[r*8+i] = bit plane i of row r",
+        f"// survivor c (the first {K} present shards{'' if K == 8 else f', in halves 0-{ka - 1} and {ka}-{K - 1}'}), O[r*8+i] = bit plane i of row r",
         "// (rows [0, n_store) stored, the rest compared with the present",
         "// non-survivor parity in ascending order).  Included by rs_decode_net.hip",
         "// inside namespace rsg, after x3().",
@@ -248,13 +251,13 @@ def main():
             hdr += emit_net(pid, pat, nets[0][pid])
             hdr.append("")
     else:
-        hdr += [f"// net_lo: all rows over survivors 0-7 (planes P[0..64)); net_hi: over survivors 8-{K - 1} "
-                f"(planes P[0..{8 * (K - 8)}))",
+        hdr += [f"// net_lo: all rows over survivors 0-{ka - 1} (planes P[0..{8 * ka})); net_hi: over survivors "
+                f"{ka}-{K - 1} (planes P[0..{8 * (K - ka)}))",
                 "template <int PID>", "__device__ void net_lo(const uint32_t (&P)[64], uint32_t (&O)[32]);",
                 "template <int PID>", "__device__ void net_hi(const uint32_t (&P)[64], uint32_t (&O)[32]);", ""]
         for pid, pat in enumerate(pats):
-            hdr += emit_net(pid, pat, nets[0][pid], "net_lo", ", survivors 0-7")
-            hdr += emit_net(pid, pat, nets[1][pid], "net_hi", f", survivors 8-{K - 1}")
+            hdr += emit_net(pid, pat, nets[0][pid], "net_lo", f", survivors 0-{ka - 1}")
+            hdr += emit_net(pid, pat, nets[1][pid], "net_hi", f", survivors {ka}-{K - 1}")
             hdr.append("")
     hdr.append(f"}}  // namespace decnet{'' if K == 8 else K}")
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "rustfs_amd", "csrc", name)
