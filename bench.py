@@ -436,7 +436,7 @@ def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto"):
                      "frac_call": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "traffic": pmc_lookup(traffic_key) if traffic_key else None}
         # the engine's kernels alone (HIP events around its launches inside
-        # the call, rsg_set_kernel_timing), averaged over `reps` more calls
+        # the call, rsg_set_kernel_timing), the median of `reps` more calls
         kms = []
         _lib.check(L.rsg_set_kernel_timing(ctx, 1))
         try:
@@ -448,8 +448,9 @@ def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto"):
         finally:
             _lib.check(L.rsg_set_kernel_timing(ctx, 0))
         if kms and min(kms) > 0:
-            km = sum(kms) / len(kms)
-            res[name].update({"kernel_ms": round(km, 4), "frac": round(alg / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+            km = sorted(kms)[len(kms) // 2]  # the median (one call's outlier does not move it)
+            res[name].update({"kernel_ms": round(km, 4), "kernel_ms_each": [round(x, 4) for x in kms],
+                              "frac": round(alg / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
         else:
             res[name]["frac"] = res[name]["frac_call"]
 

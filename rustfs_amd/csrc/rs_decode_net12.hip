@@ -1,0 +1,367 @@
+// rs_decode_net12.hip — the one-pass GET / heal kernel for RS(12,4), the
+// default geometry of a 16-drive set (storageclass.rs:24-31), with its rows
+// as compile-time XOR networks per erasure pattern (k_decode_records_net12
+// <PID>; networks in the generated rs124_decode_nets.h,
+// tools/gen_decode_nets.py --k 12).  Compiled RSG_NET_PARTS times (Makefile)
+// like rs_decode_net.hip.
+//
+// At 1 MiB blocks RS(12,4)'s shards are 87382 bytes, so its record walks are
+// ragged (170 whole 512-byte steps and 342 bytes, rs_records.h walk_tail) and
+// its records sit at every alignment (LDS-DMA takes unaligned sources).
+//
+// The workgroup is the table kernel's (k_decode_records_dma<12,NF,4,TH>: 4
+// stripes, NF = 14-15 present record files DMA'd into an LDS ring per
+// 512-byte step by 4 DMA + verify-hash waves) with the GF work done by FOUR
+// network waves, one per SIMD beside one hash wave each: wave q transposes
+// survivors 3q..3q+2 of the 4-stripe group (8 bytes of each stripe per lane)
+// into 24 bit planes, runs the pattern's net_q<PID, q> (its part of all R <= 4
+// rows), keeps its part of row q and XORs its parts of the other rows into
+// their accumulators in a double-buffered LDS area (LDS atomic XOR,
+// ds_xor_b32: 8 KiB a step, not 24 for the parts side by side, which leaves
+// the LDS room for a 4-slot ring — three steps of DMA in flight); one
+// interval later it XORs row q's accumulator in, transposes the row back and
+// stores it (rows [0, NST): rebuilt data / heal targets, heal also into the
+// target-row area for the target hashers) or compares it with the surplus
+// parity row it kept from the ring.  Two network waves over halves
+// (rs_decode_net16.hip's shape) left both on SIMDs shared with a hash wave at
+// about 600 VALU a step each (RS(12,4) GET with 2 data lost 1.52 ms,
+// profiles/r04/d/); a quarter wave issues about 330.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include <array>
+#include <utility>
+
+#include "rs_device.h"
+#include "rs_kernels.h"
+#include "rs_records.h"
+
+#ifndef RSG_NET_PART
+#error "RSG_NET_PART (0 .. RSG_NET_PARTS-1) is set by the Makefile"
+#endif
+
+namespace rsg {
+
+#include "rs124_decode_nets.h"
+
+namespace {
+
+constexpr int kK12 = 12, kNQ = 4, kQC = 3;  // data shards, network waves, survivors per wave
+
+template <int NF, int TH>
+struct Net12Shape : RecRing<NF, 4, TH> {
+    static constexpr int WAVES = RecRing<NF, 4, TH>::HW + kNQ + RecRing<NF, 4, TH>::TW;
+    static constexpr uint32_t XROW = 8 * 64 * 4;  // one row's accumulator: 8 planes, lane-major dwords (2 KiB)
+    static constexpr uint32_t XSLOT = 4 * XROW;    // a step's exchange (8 KiB)
+    static constexpr int XB = TH ? 1 : 0;          // extra barrier: heal's target hashers trail by 2 steps
+    static constexpr int RD = 4;                   // ring slots (three steps of DMA in flight)
+    static constexpr uint32_t LDS = RD * RecRing<NF, 4, TH>::DSLOT + 2 * XSLOT +
+                                    (TH ? 2 * RecRing<NF, 4, TH>::TSLOT : 16) + 32;
+};
+
+__device__ __forceinline__ void put8_12(uint8_t* p, const uint2& v) { st64_any(p, u64_of(v)); }  // any alignment
+
+// Verdict of the compared rows, combined across the waves that finish them:
+// per-stripe mismatch bits OR-ed in and a count of waves done; the last one
+// writes each live stripe's verdict whole (no memset before the launch).
+struct Verdict {
+    uint32_t bad;
+    uint32_t done;
+};
+
+// Network wave Q of the 4-stripe group (survivors 3Q..3Q+2).
+template <int PID, int NF, int TH, int Q>
+__device__ __forceinline__ void net12_wave(const GfApplyParams& p, uint64_t n, uint32_t steps, uint64_t s0,
+                                           const uint8_t* ring, uint8_t* xbuf, uint8_t* trow, Verdict* vd) {
+    using dma::CH;
+    using dma::IP;
+    using dma::PP;
+    using L = Net12Shape<NF, TH>;
+    constexpr int D = L::RD;
+    constexpr decnet12::Pattern pat = decnet12::kPatterns[PID];
+    constexpr int R = pat.R, NST = pat.n_store, NCMP = R - NST, SPW = L::SPW, HS = L::HS;
+    static_assert(pat.nf == NF && (pat.heal ? NST : 0) == TH && R <= kNQ && NST <= R && HS == 2, "pattern shape");
+    constexpr int C0 = kQC * Q;             // this wave's survivors [C0, C0 + 3)
+    constexpr bool FIN = Q < R;             // it finishes row Q
+    constexpr bool CMP = FIN && Q >= NST;   // ... a compared one (keeps surplus row Q - NST from the ring)
+    if (p.wave_prio & kPrioGf) __builtin_amdgcn_s_setprio(2);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t m4 = vgpr_const(0x0f0f0f0fu), m2 = vgpr_const(0x33333333u), m1 = vgpr_const(0x55555555u);
+    const uint32_t cmask = p.copy_mask;
+    // stripe j of the group at ring row + {0, IP, CH, IP + CH}
+    bool live[4];  // wave-uniform: a dead stripe (past n) computes stripe 0's rows and stores nothing
+    uint8_t* ob[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        live[j] = s0 + j < n;
+        ob[j] = p.out_base + (live[j] ? s0 + j : 0) * p.out_stripe_stride + lane * 8u;
+    }
+    auto row4 = [&](const uint8_t* row, uint2 (&x)[4]) {
+        x[0] = *(const uint2*)row;
+        x[1] = *(const uint2*)(row + IP);
+        x[2] = *(const uint2*)(row + CH);
+        x[3] = *(const uint2*)(row + IP + CH);
+    };
+    uint32_t diff[4] = {0u, 0u, 0u, 0u};  // CMP: OR of this lane's surplus-parity differences
+    const uint32_t tail = walk_tail(p.byte_end, steps);  // a ragged walk's last step: first tail bytes only
+    uint32_t keep[8];   // step t-1's part of row Q, held across B(t)
+    uint2 cmp[4];       // CMP: step t-1's surplus row, held across B(t)
+    // row r's accumulator of step t, lane-major
+    auto xb_at = [&](int r, uint32_t t) { return (uint32_t*)(xbuf + (t & 1) * L::XSLOT + r * L::XROW) + lane; };
+    // step t: this wave's 3 survivors -> 24 planes -> its part of every row;
+    // the other rows' parts out to LDS; copy-through of its data survivors (GET)
+    auto part = [&](uint32_t t) {
+        const uint8_t* slot = ring + (t % D) * L::DSLOT + lane * 8u;
+        uint32_t P[64];  // planes [0, 24) only
+#pragma unroll
+        for (int c = 0; c < kQC; ++c) {
+            uint2 a[4];
+            row4(slot + (C0 + c) * HS * IP, a);
+            uint32_t w[8] = {a[0].x, a[0].y, a[1].x, a[1].y, a[2].x, a[2].y, a[3].x, a[3].y};
+            dma::transpose(w, m4, m2, m1);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) P[8 * c + j] = w[j];
+        }
+        uint32_t O[32];
+        decnet12::net_q<PID, Q>(P, O);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (r == Q) continue;
+            uint32_t* xo = xb_at(r, t);
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                __hip_atomic_fetch_xor(xo + 64 * i, O[8 * r + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if constexpr (FIN) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) keep[i] = O[8 * Q + i];
+        }
+        if constexpr (CMP) row4(slot + (kK12 + Q - NST) * HS * IP, cmp);
+        if (!TH && cmask) {  // GET: this wave's present data survivors copied through
+            const bool ragged = t + 1 == steps && tail != CH;  // wave-uniform
+#pragma unroll
+            for (int c = 0; c < kQC; ++c) {
+                if (!((cmask >> (C0 + c)) & 1u)) continue;  // wave-uniform
+                uint2 x[4];
+                row4(slot + (C0 + c) * HS * IP, x);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (!live[j]) continue;
+                    if (!ragged) put8_12(ob[j] + p.copy_off[C0 + c] + (uint64_t)t * CH, x[j]);
+                    else st64_part(ob[j] + p.copy_off[C0 + c] + (uint64_t)t * CH, u64_of(x[j]), lane * 8u, tail);
+                }
+            }
+        }
+    };
+    // step s (in interval s+1): the other waves' parts of row Q in (the
+    // accumulator cleared for step s+2, whose parts come after B(s+2)), the
+    // row back to bytes, stored or compared
+    auto finish = [&](uint32_t s) {
+        const bool ragged = s + 1 == steps && tail != CH;  // wave-uniform
+        uint32_t* xa = xb_at(Q, s);
+        uint32_t w[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[i] = keep[i] ^ xa[64 * i];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) xa[64 * i] = 0u;
+        dma::transpose(w, m4, m2, m1);
+        if constexpr (Q < NST) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint2 v = make_uint2(w[2 * j], w[2 * j + 1]);
+                if (live[j]) {
+                    if (!ragged) put8_12(ob[j] + p.out_off[Q] + (uint64_t)s * CH, v);
+                    else st64_part(ob[j] + p.out_off[Q] + (uint64_t)s * CH, u64_of(v), lane * 8u, tail);
+                }
+                if constexpr (TH > 0) *(uint2*)(trow + (s & 1) * L::TSLOT + (Q * SPW + j) * PP + lane * 8u) = v;
+            }
+        } else if (!ragged) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                diff[j] = or_diff(or_diff(diff[j], cmp[j].x, w[2 * j]), cmp[j].y, w[2 * j + 1]);
+        } else {  // only the bytes before the ragged step's tail count
+            const uint64_t keepm = part_mask8(lane * 8u, tail);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint64_t d = (u64_of(cmp[j]) ^ ((uint64_t)w[2 * j] | ((uint64_t)w[2 * j + 1] << 32))) & keepm;
+                diff[j] |= (uint32_t)d | (uint32_t)(d >> 32);
+            }
+        }
+    };
+    if constexpr (FIN) {  // both accumulators of row Q start cleared
+#pragma unroll
+        for (int i = 0; i < 8; ++i) xb_at(Q, 0)[64 * i] = xb_at(Q, 1)[64 * i] = 0u;
+    }
+    lds_barrier();  // B(0)
+    if constexpr (!FIN) {  // R = 3: wave 3 hands its parts over only
+#pragma unroll 1
+        for (uint32_t t = 0; t < steps; ++t) {
+            part(t);
+            lds_barrier();  // B(t+1)
+        }
+    } else {
+        // interval t: finish step t-1 (the other parts published by B(t)), then step t's part
+#pragma unroll 1
+        for (uint32_t t = 0; t <= steps; ++t) {
+            if (t > 0) finish(t - 1);
+            if (t < steps) {
+                part(t);
+                lds_barrier();  // B(t+1)
+            }
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < L::XB; ++b) lds_barrier();  // B(steps+1): the last target rows published
+    if constexpr (CMP) {
+        uint32_t bad = 0u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bad |= (__builtin_amdgcn_ballot_w64(diff[j] != 0u) != 0 ? 1u : 0u) << j;
+        if (lane == 0) {
+            if (NCMP > 1) {
+                __hip_atomic_fetch_or(&vd->bad, bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (__hip_atomic_fetch_add(&vd->done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) + 1 !=
+                    (uint32_t)NCMP)
+                    return;  // another compare wave writes the verdicts
+                bad = __hip_atomic_load(&vd->bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (live[j]) p.ok_flags[s0 + j] = (bad >> j) & 1u ? 0 : 1;
+        }
+    }
+}
+
+// ENC: the fused encode + HH256S (k_encode_hash_net12 below): the heal of
+// all four parity shards over a stripe buffer, every digest written to the
+// batch digest layout.
+template <int PID, int NF, int TH, bool ENC = false>
+__global__ __launch_bounds__((64 * Net12Shape<NF, TH>::WAVES)) void k_decode_records_net12(const GfApplyParams p,
+                                                                                           const HashParams h) {
+    using L = Net12Shape<NF, TH>;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[L::RD * L::DSLOT];
+    __shared__ __attribute__((aligned(16))) uint8_t xbuf[2 * L::XSLOT];
+    __shared__ __attribute__((aligned(16))) uint8_t trow[TH ? 2 * L::TSLOT : 16];
+    __shared__ Verdict vd;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t steps = p.units;
+    const uint64_t s0 = (uint64_t)blockIdx.x * L::SPW;
+    if (TH && wave >= (uint32_t)(L::HW + kNQ)) {
+        records_target_hasher<4, TH, 2, ENC>(p, h, trow, wave - L::HW - kNQ, steps, s0);
+        return;
+    }
+    if (wave >= (uint32_t)L::HW) {
+        const uint32_t q = wave - L::HW;
+        if (q == 0 && threadIdx.x % 64 == 0) vd = Verdict{0u, 0u};  // ordered before the compares by B(0)
+        if (q == 0) net12_wave<PID, NF, TH, 0>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
+        else if (q == 1) net12_wave<PID, NF, TH, 1>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
+        else if (q == 2) net12_wave<PID, NF, TH, 2>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
+        else net12_wave<PID, NF, TH, 3>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
+        return;
+    }
+    records_hash_wave<NF, 4, L::XB, L::RD, ENC>(h, p.wave_prio, ring, wave, steps, s0);
+}
+
+static_assert(Net12Shape<15, 0>::LDS <= 160 * 1024 && Net12Shape<14, 0>::LDS <= 160 * 1024 &&
+                  Net12Shape<15, 1>::LDS <= 160 * 1024 && Net12Shape<14, 2>::LDS <= 160 * 1024,
+              "RS(12,4) GET / heal workgroups fit the LDS");
+
+using Net12Launch = void (*)(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream);
+
+template <int PID>
+void launch_net12(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
+    constexpr decnet12::Pattern pat = decnet12::kPatterns[PID];
+    constexpr int NF = pat.nf, TH = pat.heal ? pat.n_store : 0;
+    hipLaunchKernelGGL((k_decode_records_net12<PID, NF, TH>), dim3((uint32_t)blocks),
+                       dim3(64 * Net12Shape<NF, TH>::WAVES), 0, stream, p, h);
+}
+
+template <int PID>
+constexpr Net12Launch pick_net12() {
+    if constexpr (PID % RSG_NET_PARTS == RSG_NET_PART) return &launch_net12<PID>;
+    else return nullptr;
+}
+
+template <size_t... I>
+constexpr std::array<Net12Launch, sizeof...(I)> net12_table(std::index_sequence<I...>) {
+    return {pick_net12<(int)I>()...};
+}
+
+const std::array<Net12Launch, decnet12::kCount> kNet12Part =
+    net12_table(std::make_index_sequence<decnet12::kCount>{});
+
+}  // namespace
+
+#define RSG_NET12_CAT2(a, b) a##b
+#define RSG_NET12_CAT(a, b) RSG_NET12_CAT2(a, b)
+
+// This part's launcher (launch_records_net12_partN): false if pattern `pid`
+// is instantiated elsewhere.
+bool RSG_NET12_CAT(launch_records_net12_part, RSG_NET_PART)(int pid, uint64_t blocks, const GfApplyParams& p,
+                                                           const HashParams& h, hipStream_t stream) {
+    if (pid < 0 || pid >= decnet12::kCount || !kNet12Part[pid]) return false;
+    kNet12Part[pid](blocks, p, h, stream);
+    return true;
+}
+
+#if RSG_NET_PART == 0
+// The fused encode + HH256S of RS(12,4) (BitrotWriter over an encoded block,
+// bitrot.rs:464-510 after erasure encode): the heal kernel of all four parity
+// shards (pattern kEncodePid, rows = the encode matrix) walking the data
+// shards of a stripe buffer in place — 12 data rows DMA'd and hashed, 4
+// parity rows computed by the network waves, stored and hashed by the target
+// hasher — every digest to h.out (stripe-major, 16 per stripe).
+namespace {
+constexpr int encode_pid() {
+    for (int i = 0; i < decnet12::kCount; ++i)
+        if (decnet12::kPatterns[i].heal && decnet12::kPatterns[i].absent == 0xF000) return i;
+    return -1;
+}
+constexpr int kEncodePid = encode_pid();
+static_assert(kEncodePid >= 0 && decnet12::kPatterns[kEncodePid].nf == 12 && decnet12::kPatterns[kEncodePid].R == 4,
+              "rs124_decode_nets.h lists the heal of every parity shard");
+}  // namespace
+
+const uint8_t* encode_net12_coef() { return &decnet12::kPatterns[kEncodePid].coef[0][0]; }
+
+// p: the encode's table-GF launch (in place: base == out_base, in_off = the
+// data shards, out_off = the parity shards); h: key, out (digests).
+hipError_t launch_encode_hash_net12(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
+                                    hipStream_t stream) {
+    using L = Net12Shape<12, 4>;
+    if (p.C != 12 || p.R != 4 || n_stripes == 0 || shard_len == 0 || p.base != p.out_base ||
+        p.stripe_stride != p.out_stripe_stride || 5 * p.stripe_stride >= (1ull << 32) ||
+        (n_stripes + L::SPW - 1) / L::SPW > 0x7fffffffull || (shard_len + dma::CH - 1) / dma::CH > 0xffffffffull)
+        return hipErrorInvalidValue;
+    p.n_store = 4;
+    p.copy_mask = 0;
+    p.wave_prio = (uint32_t)tuning().get_prio;  // as the GET / heal (RSG_DMA_PRIO)
+    p.units = (uint32_t)((shard_len + dma::CH - 1) / dma::CH);
+    p.byte_end = shard_len;
+    h.len = shard_len;
+    h.n = n_stripes;
+    h.shards = 16;
+    h.stripe_stride = p.stripe_stride;
+    h.nbases = 12;
+    for (int c = 0; c < 12; ++c) h.base[c] = p.base + p.in_off[c];
+    hipLaunchKernelGGL((k_decode_records_net12<kEncodePid, 12, 4, true>),
+                       dim3((uint32_t)((n_stripes + L::SPW - 1) / L::SPW)), dim3(64 * L::WAVES), 0, stream, p, h);
+    return hipGetLastError();
+}
+
+// The pattern whose coefficient rows equal the launch's (R x 12, row-major),
+// or -1.
+int records_net12_pattern(int heal, int nf, int R, int n_store, const uint8_t* coef) {
+    for (int i = 0; i < decnet12::kCount; ++i) {
+        const decnet12::Pattern& pt = decnet12::kPatterns[i];
+        if (pt.heal != heal || pt.nf != nf || pt.R != R || pt.n_store != n_store) continue;
+        bool eq = true;
+        for (int r = 0; r < R && eq; ++r)
+            for (int c = 0; c < kK12 && eq; ++c) eq = pt.coef[r][c] == coef[r * kK12 + c];
+        if (eq) return i;
+    }
+    return -1;
+}
+#endif
+
+}  // namespace rsg

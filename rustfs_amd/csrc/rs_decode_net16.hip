@@ -1,24 +1,19 @@
-// rs_decode_net16.hip — the one-pass GET / heal kernel for RS(16,4) and
-// RS(12,4) with its rows as compile-time XOR networks per erasure pattern
-// (k_decode_records_net16<PID>; networks in the generated
-// rs164_decode_nets.h / rs124_decode_nets.h, tools/gen_decode_nets.py --k 16
-// / --k 12).  Compiled RSG_NET_PARTS times per geometry (Makefile: RSG_NET_K
-// = 16 or 12) like rs_decode_net.hip.
-//
-// RS(12,4) is the default geometry of a 16-drive set (storageclass.rs:24-31);
-// at 1 MiB blocks its shards are 87382 bytes, so its record walks are ragged
-// (170 whole 512-byte steps and 342 bytes, rs_records.h walk_tail) and its
-// records sit at every alignment (LDS-DMA takes unaligned sources).
+// rs_decode_net16.hip — the one-pass GET / heal kernel for RS(16,4) with its
+// rows as compile-time XOR networks per erasure pattern
+// (k_decode_records_net16<PID>; networks in the generated rs164_decode_nets.h,
+// tools/gen_decode_nets.py --k 16).  Compiled RSG_NET_PARTS times (Makefile)
+// like rs_decode_net.hip.  RS(12,4) has its own four-wave form
+// (rs_decode_net12.hip).
 //
 // The table kernel's RS(16,4) workgroup (k_decode_records_dma<16,NF,4,TH>:
 // 4 stripes, NF present record files DMA'd into a 3-slot LDS ring per
 // 512-byte step, ceil(2 NF / 8) DMA + verify-hash waves) with its 4 table-GF
 // waves (one per stripe, 16 survivors x 4 rows of v_perm lookups each)
 // replaced by two network waves over the one 4-stripe group (8 bytes of
-// each stripe per lane): the 16 (12) survivors' 128 (96) bit planes do not
-// fit one wave beside the rows, so
-//   wave B transposes survivors 8..K-1 and runs the pattern's net_hi (all R
-//     rows over those 64 (32) planes) and hands its 32 partial planes to
+// each stripe per lane): the 16 survivors' 128 bit planes do not fit one
+// wave beside the rows, so
+//   wave B transposes survivors 8-15 and runs the pattern's net_hi (all R
+//     rows over those 64 planes) and hands its 32 partial planes to
 //     wave A through a double-buffered LDS area;
 //   wave A transposes survivors 0-7, runs net_lo, and one interval later
 //     XORs in B's half, transposes the rows back, stores the rebuilt rows
@@ -39,27 +34,13 @@
 #ifndef RSG_NET_PART
 #error "RSG_NET_PART (0 .. RSG_NET_PARTS-1) is set by the Makefile"
 #endif
-#ifndef RSG_NET_K
-#define RSG_NET_K 16
-#endif
 
 namespace rsg {
 
-#if RSG_NET_K == 16
 #include "rs164_decode_nets.h"
 namespace decnetk = decnet16;
-#elif RSG_NET_K == 12
-#include "rs124_decode_nets.h"
-namespace decnetk = decnet12;
-#else
-#error "RSG_NET_K is 16 or 12"
-#endif
-constexpr int kNetK = RSG_NET_K;
-// survivors of network wave A (the rest are B's): 8 of RS(16,4)'s 16, 6 of
-// RS(12,4)'s 12 — equal halves, so the two waves transpose and combine the
-// same number of rows (8 / 4 left wave A alone on the critical path: RS(12,4)
-// GET with 2 data lost 1.80 ms, profiles/r04/c/)
-constexpr int kNetA = kNetK == 12 ? 6 : 8;
+constexpr int kNetK = 16;
+constexpr int kNetA = 8;  // survivors of network wave A (the rest are B's)
 
 template <int NF, int TH>
 struct Net16Shape : RecRing<NF, 4, TH> {
@@ -67,13 +48,8 @@ struct Net16Shape : RecRing<NF, 4, TH> {
     static constexpr int WAVES = RecRing<NF, 4, TH>::HW + NG + RecRing<NF, 4, TH>::TW;
     static constexpr uint32_t XSLOT = 32 * 64 * 4;  // a step's exchanged partial planes, lane-major (<= 8 KiB)
     static constexpr int XB = TH ? 1 : 0;           // extra barrier: heal's target hashers trail by 2 steps
-    // ring slots: 4 (three steps of DMA in flight) where the LDS holds them —
-    // every RS(12,4) shape (14-15 files) — else 3 (RS(16,4): 18-19 files).
-    // The walk is bound by the record bytes in flight per CU (a step takes
-    // about half the loaded HBM latency with two steps in flight), and the
-    // ring is what holds them.
     static constexpr uint32_t LDS_REST = 4 * XSLOT + (TH ? 2 * RecRing<NF, 4, TH>::TSLOT : 16);
-    static constexpr int RD = 4 * RecRing<NF, 4, TH>::DSLOT + LDS_REST <= 160 * 1024 ? 4 : 3;
+    static constexpr int RD = dma::D;  // ring slots (18-19 files: 3 is what the LDS holds)
 };
 
 __device__ __forceinline__ void put8_16(uint8_t* p, const uint2& v) { st64_any(p, u64_of(v)); }  // any alignment
@@ -100,10 +76,10 @@ __device__ __forceinline__ void net16_wave(const GfApplyParams& p, uint64_t n, u
     constexpr int R = pat.R, NST = pat.n_store, NCMP = R - NST, SPW = L::SPW, HS = L::HS;
     static_assert(pat.nf == NF && (pat.heal ? NST : 0) == TH && R <= 4 && NST <= R && HS == 2, "pattern shape");
     constexpr int C0 = A ? 0 : kNetA, NC = A ? kNetA : kNetK - kNetA;  // this wave's survivors [C0, C0 + NC)
-    // heal and RS(12,4) (SF): A finishes the stored rows, B the compared
-    // ones; RS(16,4) GET: A finishes every row (B holding half the rows as
-    // well as GET's copy-through spilled at the 256-VGPR cap)
-    constexpr bool SF = TH > 0 || kNetK == 12;
+    // heal (SF): A finishes the stored rows, B the compared ones; GET: A
+    // finishes every row (B holding half the rows as well as GET's
+    // copy-through spilled at the 256-VGPR cap)
+    constexpr bool SF = TH > 0;
     constexpr int K0 = A ? 0 : NST, KN = A ? (SF ? NST : R) : (SF ? NCMP : 0);  // rows it finishes
     constexpr int G0 = A ? NST : 0, GN = A ? (SF ? NCMP : 0) : (SF ? NST : R);  // rows it gives away
     constexpr bool CMP = K0 + KN > NST;  // it finishes compared rows (keeps the surplus rows, writes verdicts)
@@ -138,7 +114,7 @@ __device__ __forceinline__ void net16_wave(const GfApplyParams& p, uint64_t n, u
     // the other wave's rows out to LDS; copy-through of its data survivors (GET)
     auto half = [&](uint32_t t) {
         const uint8_t* slot = ring + (t % D) * L::DSLOT + lane * 8u;
-        uint32_t P[64];  // RS(12,4): planes [0, 48) only
+        uint32_t P[64];
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             uint2 a[4];
@@ -268,10 +244,6 @@ __global__ __launch_bounds__((64 * Net16Shape<NF, TH>::WAVES)) void k_decode_rec
     records_hash_wave<NF, 4, L::XB, L::RD>(h, p.wave_prio, ring, wave, steps, s0);
 }
 
-static_assert(Net16Shape<19, 0>::RD * Net16Shape<19, 0>::DSLOT + Net16Shape<19, 0>::LDS_REST <= 160 * 1024 &&
-                  Net16Shape<14, 2>::RD == 4 && Net16Shape<15, 1>::RD == 4 && Net16Shape<14, 0>::RD == 4 &&
-                  Net16Shape<15, 0>::RD == 4 && Net16Shape<18, 0>::RD == 3,
-              "ring depth: 4 slots for RS(12,4), 3 for RS(16,4)");
 static_assert(dma::D * 2 * 19 * dma::IP + 4 * Net16Shape<19, 0>::XSLOT + 16 <= 160 * 1024, "RS(16,4) GET fits");
 static_assert(dma::D * 2 * 18 * dma::IP + 4 * Net16Shape<18, 2>::XSLOT + 2 * Net16Shape<18, 2>::TSLOT <= 160 * 1024,
               "RS(16,4) heal fits");
@@ -305,21 +277,19 @@ static const std::array<Net16Launch, decnetk::kCount> kNet16Part =
 #define RSG_NET16_CAT2(a, b, c) a##b##c
 #define RSG_NET16_CAT(a, b, c) RSG_NET16_CAT2(a, b, c)
 
-// This part's launcher (launch_records_net16_partN / launch_records_net12_partN):
-// false if pattern `pid` is instantiated elsewhere.
-bool RSG_NET16_CAT(launch_records_net, RSG_NET_K, RSG_NET16_CAT(_part, RSG_NET_PART, ))(int pid, uint64_t blocks,
-                                                                                  const GfApplyParams& p,
-                                                                                  const HashParams& h,
-                                                                                  hipStream_t stream) {
+// This part's launcher (launch_records_net16_partN): false if pattern `pid`
+// is instantiated elsewhere.
+bool RSG_NET16_CAT(launch_records_net16_part, RSG_NET_PART, )(int pid, uint64_t blocks, const GfApplyParams& p,
+                                                             const HashParams& h, hipStream_t stream) {
     if (pid < 0 || pid >= decnetk::kCount || !kNet16Part[pid]) return false;
     kNet16Part[pid](blocks, p, h, stream);
     return true;
 }
 
 #if RSG_NET_PART == 0
-// The pattern whose coefficient rows equal the launch's (R x K, row-major),
-// or -1 (records_net16_pattern / records_net12_pattern).
-int RSG_NET16_CAT(records_net, RSG_NET_K, _pattern)(int heal, int nf, int R, int n_store, const uint8_t* coef) {
+// The pattern whose coefficient rows equal the launch's (R x 16, row-major),
+// or -1.
+int records_net16_pattern(int heal, int nf, int R, int n_store, const uint8_t* coef) {
     for (int i = 0; i < decnetk::kCount; ++i) {
         const decnetk::Pattern& pt = decnetk::kPatterns[i];
         if (pt.heal != heal || pt.nf != nf || pt.R != R || pt.n_store != n_store) continue;

@@ -111,9 +111,14 @@ hipError_t launch_hh256(const HashParams& p, hipStream_t stream);
 
 // Fused encode + per-shard HighwayHash (one pass).  p: the encode RowSet with
 // in_off = data shards, out_off = parity shards, base == out_base; h: key and
-// digest output [n][C+R][32].  Requires shard_len % 512 == 0, C <= 16, R <= 4
-// and 16-B aligned shards.
+// digest output [n][C+R][32].  C <= 16, R <= 4, any shard length.
 bool fused_supported(int C, int R, uint64_t shard_len);
+// RS(12,4): the fused encode as the one-pass network heal of every parity
+// shard (rs_decode_net12.hip, k_encode_hash_net12); its 4 x 12 coefficient
+// rows, which the launch's tables must match.
+const uint8_t* encode_net12_coef();
+hipError_t launch_encode_hash_net12(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
+                                    hipStream_t stream);
 // One-pass degraded GET (k_decode_records_dma) for RS(k, m), k <= 16, m <= 4,
 // any shard length (a ragged last step), over nf (k..k+m-1) present record
 // files: false if the shape is not supported.
@@ -160,7 +165,7 @@ RSG_NET16_PART_DECL(4)
 RSG_NET16_PART_DECL(5)
 RSG_NET16_PART_DECL(6)
 RSG_NET16_PART_DECL(7)
-// RS(12,4) (the same source built with RSG_NET_K = 12, rs124_decode_nets.h)
+// RS(12,4) (rs_decode_net12.hip, k_decode_records_net12): the same for R x 12 rows
 int records_net12_pattern(int heal, int nf, int R, int n_store, const uint8_t* coef);
 #define RSG_NET16_PART_DECL12(i)                                                                               \
     bool launch_records_net12_part##i(int pid, uint64_t blocks, const GfApplyParams& p, const HashParams& h, \

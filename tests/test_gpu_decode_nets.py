@@ -242,17 +242,20 @@ def _rehashed12(torch, oracle, f, stripe, pos):
 
 def test_rs12_table_lists_every_pattern():
     """Every one- and two-shard loss of RS(12,4): 12 + 114 GET patterns (a
-    data shard among the lost) and 16 + 120 heal patterns."""
+    data shard among the lost) and 16 + 120 heal patterns, plus the heal of
+    all four parity shards (the encode's rows)."""
     assert len([x for x in LISTED12 if not x[0]]) == 12 + 114
-    assert len([x for x in LISTED12 if x[0]]) == 16 + 120
+    assert len([x for x in LISTED12 if x[0]]) == 16 + 120 + 1
+    assert (1, (12, 13, 14, 15)) in LISTED12
 
 
 @pytest.mark.parametrize("heal,lost", LISTED12, ids=lambda x: str(x))
 def test_rs12_every_listed_pattern(gpu, oracle, records12, one_pass, heal, lost):
-    """k_decode_records_net16 built for RS(12,4) (two networks over survivors
-    0-7 and 8-11), on a ragged walk: GET in both forms and heal, bit-exact
-    against the oracle, with an altered surplus parity (in the ragged last
-    step) reported for its stripe alone."""
+    """k_decode_records_net12 (four network waves over survivors 0-2 / 3-5 /
+    6-8 / 9-11, each finishing one row), on a ragged walk: GET in both forms
+    and heal, bit-exact against the oracle, with an altered surplus parity (in
+    the ragged last step; which surplus — so which wave compares it — varies
+    with the pattern) reported for its stripe alone."""
     import torch
     from rustfs_amd import Erasure, _lib
     shards, recs, files = records12
@@ -268,7 +271,8 @@ def test_rs12_every_listed_pattern(gpu, oracle, records12, one_pass, heal, lost)
         if sur:
             stripe = sum(lost) % N12
             f2 = list(f)
-            f2[sur[-1]] = _rehashed12(torch, oracle, files[sur[-1]], stripe, 600 + sum(lost))
+            bad = sur[sum(lost) % len(sur)]
+            f2[bad] = _rehashed12(torch, oracle, files[bad], stripe, 600 + sum(lost))
             for form in FORMS:
                 out, status = decode_get(e, f2, S12, N12, form)
                 assert [i for i, x in enumerate(status) if x] == [stripe], form
@@ -285,7 +289,8 @@ def test_rs12_every_listed_pattern(gpu, oracle, records12, one_pass, heal, lost)
     if sur:
         stripe = (5 * sum(lost) + 1) % N12
         src2 = list(src)
-        src2[sur[0]] = _rehashed12(torch, oracle, files[sur[0]], stripe, 7 * sum(lost) % S12)
+        bad = sur[(sum(lost) + 1) % len(sur)]
+        src2[bad] = _rehashed12(torch, oracle, files[bad], stripe, 7 * sum(lost) % S12)
         tgt2 = [torch.zeros(N12 * REC12, dtype=torch.uint8, device="cuda") if i in lost else None for i in range(T12)]
         status = e.heal_records_batch(src2, tgt2, S12, N12)
         assert [i for i, x in enumerate(status) if x] == [stripe]

@@ -331,7 +331,12 @@ def test_host_batch_pipeline_matches_oracle(gpu, oracle, k, m, S, n, hashed):
     (8, 4, 512, 2048),   # packed kernel (n >= 2048)
     (12, 4, 4096, 3),    # packed kernel (k > 8)
     (12, 4, 87382, 3),   # packed kernel, partial last chunk (342 B), shards at every alignment: RS(12,4) at 1 MiB
-    (12, 4, 87382, 2100),  # the same over many workgroups
+    (12, 4, 87382, 2100),  # network kernel (RS(12,4), n >= 1024): ragged walk, records at every alignment
+    (12, 4, 1000, 1027),   # network kernel: one whole step + 488 bytes, a last workgroup of 3 stripes
+    (12, 4, 4096, 1024),   # network kernel: whole steps only (the 4-slot ring wraps)
+    (12, 4, 512, 1025),    # network kernel: exactly one step
+    (12, 4, 31, 1030),     # network kernel: the remainder packet alone
+    (12, 4, 1, 1024),      # network kernel: one-byte shards
     (6, 4, 174763, 3),   # RS(6,4) at 1 MiB: odd shard length
     (10, 4, 104858, 3),  # RS(10,4) at 1 MiB
     (3, 2, 31, 5),       # a shard shorter than one packet: the remainder packet alone
@@ -341,8 +346,8 @@ def test_host_batch_pipeline_matches_oracle(gpu, oracle, k, m, S, n, hashed):
 ])
 def test_fused_kernel_selection_matches_oracle(gpu, oracle, k, m, S, n):
     """Every fused encode+HH256S kernel the launcher can pick (ring E=1/2,
-    packed) against the oracle; large batches are checked on a sample of
-    stripes that includes the first and last."""
+    packed, RS(12,4)'s network kernel) against the oracle; large batches are
+    checked on a sample of stripes that includes the first and last."""
     import torch
     from rustfs_amd import Erasure
     st = _device_batch(torch, n, k, m, S, seed=7 * S + n)

@@ -25,10 +25,12 @@ listed (or any disagreement) keeps the run-time-table kernel.
 
 RS(16,4) (`--k 16`) and RS(12,4) (`--k 12`, the default geometry of a
 16-drive set, storageclass.rs:24-31): the survivors' 128 / 96 planes do not
-fit one wave's registers beside the rows, so each pattern gets TWO networks,
-one over survivors 0-7 (RS(12,4): 0-5) and one over the rest, each producing
-all R rows; the kernel XORs the two halves (rs_decode_net16.hip) — headers
-rs164_decode_nets.h / rs124_decode_nets.h.
+fit one wave's registers beside the rows, so each pattern gets one network
+per part of the survivors, each producing all R rows, and the kernel XORs the
+parts: RS(16,4) two (survivors 0-7 / 8-15, rs_decode_net16.hip,
+rs164_decode_nets.h `net_lo` / `net_hi`), RS(12,4) four (0-2 / 3-5 / 6-8 /
+9-11, one network wave per SIMD, rs_decode_net12.hip, rs124_decode_nets.h
+`net_q<PID, Q>`).
 
 Usage: python tools/gen_decode_nets.py [seeds] [--k 16|12] [--only heal:1,16 get:0,3 ...]
 (writes the header)
@@ -97,8 +99,12 @@ def patterns():
     """(absent mask, heal, nf, R, n_store, coef rows) for 1 and 2 lost shards."""
     out, seen = [], set()
     losses = [(a,) for a in range(T)] + [(a, b) for a in range(T) for b in range(a + 1, T)]
+    # RS(12,4): also the heal of all four parity shards — rows = the encode
+    # matrix over the data shards, which the fused encode + HH256S kernel
+    # (rs_decode_net12.hip, k_encode_hash_net12) runs as its network
+    every_parity = [tuple(range(K, T))] if K == 12 else []
     for heal in (0, 1):
-        for lost in losses:
+        for lost in losses + (every_parity if heal else []):
             present = [0 if i in lost else 1 for i in range(T)]
             files = [i for i in range(T) if present[i]]
             mat, surv, inv = plan(present)
@@ -157,7 +163,7 @@ def check(pr, temps, rr):
             assert got == want, o
 
 
-def emit_net(pid, pat, net, fn="net", what=""):
+def emit_net(pid, pat, net, fn="net", what="", targs=None):
     mask, heal, nf, R, nst, rows = pat
     total, temps, rr, seed = net
     name = lambda v: f"P[{v}]" if v < 64 else f"t{v}"
@@ -165,7 +171,8 @@ def emit_net(pid, pat, net, fn="net", what=""):
     out = [f"// pattern {pid}: {'heal' if heal else 'GET'}, lost {lost}, {nf} present, R = {R} "
            f"({nst} stored){what}, {total} ops (seed {seed})",
            "template <>",
-           f"__device__ __forceinline__ void {fn}<{pid}>(const uint32_t (&P)[64], uint32_t (&O)[32]) {{"]
+           f"__device__ __forceinline__ void {fn}<{pid if targs is None else targs}>(const uint32_t (&P)[64], "
+           "uint32_t (&O)[32]) {"]
     for v, *t in temps:
         if len(t) == 3:
             out.append(f"    const uint32_t t{v} = x3({name(t[0])}, {name(t[1])}, {name(t[2])});")
@@ -205,10 +212,11 @@ def main():
     pats = patterns()
     if only:  # prototype builds: e.g. heal:1,16 get:0,3
         pats = [p for p in pats if f"{'heal' if p[1] else 'get'}:{','.join(str(i) for i in range(T) if p[0] >> i & 1)}" in only]
-    # RS(16,4): survivors 0-7 / 8-15; RS(12,4): 0-5 / 6-11 (the two network
-    # waves then transpose and combine equal halves, rs_decode_net16.hip)
-    ka = K // 2 if K == 12 else 8
-    halves = [(0, 8)] if K == 8 else [(0, ka), (ka, K - ka)]
+    # RS(16,4): survivors 0-7 / 8-15 (two network waves, rs_decode_net16.hip);
+    # RS(12,4): quarters 0-2 / 3-5 / 6-8 / 9-11 (four network waves, one per
+    # SIMD, rs_decode_net12.hip)
+    ka = 8
+    halves = {8: [(0, 8)], 16: [(0, 8), (8, 8)], 12: [(0, 3), (3, 3), (6, 3), (9, 3)]}[K]
     tasks = [(p[5], seeds, c0, cn) for c0, cn in halves for p in pats]
     with multiprocessing.Pool(min(8, os.cpu_count() or 1)) as pool:
         res = pool.map(best_network, tasks)
@@ -220,7 +228,7 @@ def main():
         f"// RS({K},{M}) one-pass GET / heal rows as compile-time three-input XOR networks,",
         f"// one per erasure pattern of one or two lost shards: {len(pats)} patterns,",
         f"// {min(ops)}-{max(ops)} ops each (mean {sum(ops) / len(ops):.0f}).  P[c*8+j] = bit plane j of",
-        f"// survivor c (the first {K} present shards{'' if K == 8 else f', in halves 0-{ka - 1} and {ka}-{K - 1}'}), O[r*8+i] = bit plane i of row r",
+        f"// survivor c (the first {K} present shards{'' if K == 8 else ', in parts ' + ', '.join(f'{c0}-{c0 + cn - 1}' for c0, cn in halves)}), O[r*8+i] = bit plane i of row r",
         "// (rows [0, n_store) stored, the rest compared with the present",
         "// non-survivor parity in ascending order).  Included by rs_decode_net.hip",
         "// inside namespace rsg, after x3().",
@@ -249,6 +257,13 @@ def main():
         hdr += ["template <int PID>", "__device__ void net(const uint32_t (&P)[64], uint32_t (&O)[32]);", ""]
         for pid, pat in enumerate(pats):
             hdr += emit_net(pid, pat, nets[0][pid])
+            hdr.append("")
+    elif K == 12:
+        hdr += ["// net_q<PID, Q>: all rows over survivors 3Q-3Q+2 (planes P[0..24))",
+                "template <int PID, int Q>", "__device__ void net_q(const uint32_t (&P)[64], uint32_t (&O)[32]);", ""]
+        for pid, pat in enumerate(pats):
+            for q, (c0, cn) in enumerate(halves):
+                hdr += emit_net(pid, pat, nets[q][pid], "net_q", f", survivors {c0}-{c0 + cn - 1}", f"{pid}, {q}")
             hdr.append("")
     else:
         hdr += [f"// net_lo: all rows over survivors 0-{ka - 1} (planes P[0..{8 * ka})); net_hi: over survivors "
