@@ -440,11 +440,17 @@ def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto"):
         kms = []
         _lib.check(L.rsg_set_kernel_timing(ctx, 1))
         try:
+            ev[0].record(stream)
             for _ in range(reps):
                 fn()
                 v = ctypes.c_float(-1)
                 _lib.check(L.rsg_last_kernel_ms(ctx, ctypes.byref(v)))
                 kms.append(v.value)
+            ev[1].record(stream)
+            torch.cuda.synchronize()
+            # the same calls' whole time with the hook on (against call_ms:
+            # whether the hook's events change the calls themselves)
+            res[name]["call_ms_hooked"] = round(ev[0].elapsed_time(ev[1]) / reps, 4)
         finally:
             _lib.check(L.rsg_set_kernel_timing(ctx, 0))
         if kms and min(kms) > 0:

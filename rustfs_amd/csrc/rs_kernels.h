@@ -108,6 +108,9 @@ struct HashParams {
 hipError_t launch_gf_apply_vec(GfApplyParams p, uint64_t n_stripes, hipStream_t stream);
 hipError_t launch_gf_apply_byte(GfApplyParams p, uint64_t n_stripes, hipStream_t stream);
 hipError_t launch_hh256(const HashParams& p, hipStream_t stream);
+// n bytes of device memory to page-locked host memory (dst = its device
+// view), as a kernel on the stream; 16-byte aligned ends.
+hipError_t launch_copy_to_host(uint8_t* dst, const uint8_t* src, uint64_t n, hipStream_t stream);
 
 // Fused encode + per-shard HighwayHash (one pass).  p: the encode RowSet with
 // in_off = data shards, out_off = parity shards, base == out_base; h: key and

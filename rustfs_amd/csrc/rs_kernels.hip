@@ -1272,6 +1272,24 @@ hipError_t launch_gf_apply_byte(GfApplyParams p, uint64_t n_stripes, hipStream_t
     return hipGetLastError();
 }
 
+// Bytes [0, n) of device memory src to dst, the device view of page-locked
+// host memory: the record engines' verdicts (a few KiB of flags) copied back
+// by a kernel on the call's stream.  A copy-engine transfer there made the
+// next call's kernels wait for the handoff to the copy engine and back.
+__global__ __launch_bounds__(256) void k_copy_to_host(uint8_t* dst, const uint8_t* src, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x, w = n / 16;
+    if (i < w) ((uint4*)dst)[i] = ((const uint4*)src)[i];
+    else if (i == w)
+        for (uint64_t b = w * 16; b < n; ++b) dst[b] = src[b];
+}
+
+hipError_t launch_copy_to_host(uint8_t* dst, const uint8_t* src, uint64_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    if (((uintptr_t)dst | (uintptr_t)src) % 16 || n / 16 / 256 + 1 > 0x7fffffffull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_copy_to_host, dim3((uint32_t)(n / 16 / 256 + 1)), dim3(256), 0, stream, dst, src, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_hh256(const HashParams& p, hipStream_t stream) {
     if (p.n == 0) return hipSuccess;
     const uint64_t blocks = (p.n * 4u + 255u) / 256u;  // one quad per message

@@ -488,6 +488,7 @@ struct RecScratch {
     uint8_t* d = nullptr;
     size_t dcap = 0;
     uint8_t* h = nullptr;
+    uint8_t* hdev = nullptr;  // h as the device addresses it
     size_t hcap = 0;
     bool timing = false;
     std::vector<hipEvent_t> tev;
@@ -519,8 +520,19 @@ struct RecScratch {
             hipError_t e = hipHostMalloc((void**)&h, want, hipHostMallocDefault);
             if (e != hipSuccess) return hip_status(e);
             hcap = want;
+            if ((e = hipHostGetDevicePointer((void**)&hdev, h, 0)) != hipSuccess) {
+                (void)hipHostFree(h);
+                h = hdev = nullptr;
+                hcap = 0;
+                return hip_status(e);
+            }
         }
         return RSG_OK;
+    }
+    // the call's verdicts (bytes at src, written by its work on s) into h, by
+    // a kernel on s (rsg::launch_copy_to_host)
+    int copy_back(hipStream_t s, const uint8_t* src, size_t bytes) {
+        return hip_status(rsg::launch_copy_to_host(hdev, src, bytes, s));
     }
     // HIP event pairs around the kernel launches on the call's stream
     void tmark(hipStream_t s) {
@@ -1330,7 +1342,7 @@ int verify_data_begin(RecJob& j, uint8_t* d_out) {
     if ((st = launch_verify_group(data_idx, j.files.data(), j.d_flags(), j.k, j.S, j.n, 0, j.n, j.key, d_out, j.s)))
         return st;
     j.sc->tmark(j.s);
-    return hip_status(hipMemcpyAsync(j.sc->h, j.d_flags(), (size_t)j.k * j.n, hipMemcpyDeviceToHost, j.s));
+    return j.sc->copy_back(j.s, j.d_flags(), (size_t)j.k * j.n);
 }
 
 // Second half, once the data flags have landed: the parity records are
@@ -1559,7 +1571,7 @@ int get_begin(RecJob& j) {
             j.sc->tmark(j.s);
         }
         // the verified map and the surplus verdict (adjacent in scratch) in one copy
-        return hip_status(hipMemcpyAsync(j.sc->h, j.d_flags(), (size_t)(t + 1) * n, hipMemcpyDeviceToHost, j.s));
+        return j.sc->copy_back(j.s, j.d_flags(), (size_t)(t + 1) * n);
     }
     if (lost_data == 0) {
         j.phase = RecJob::DATA_VERIFIED;
@@ -1805,7 +1817,7 @@ int heal_begin(RecJob& j) {
             return st;
         j.sc->tmark(j.s);
     }
-    return hip_status(hipMemcpyAsync(j.sc->h, j.d_flags(), (size_t)(t + 1) * n, hipMemcpyDeviceToHost, j.s));
+    return j.sc->copy_back(j.s, j.d_flags(), (size_t)(t + 1) * n);
 }
 
 int heal_finish(RecJob& j) {
