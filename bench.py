@@ -423,6 +423,11 @@ def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto"):
     def timed(name, fn, alg, check, reps=5, traffic_key=None):
         fn()
         torch.cuda.synchronize()
+        # each loop starts from an idle GPU: after ~20 back-to-back one-pass
+        # calls the clock drops (a power transient: the hooked loop right
+        # after the plain one ran 1.62 ms per call against 1.38 ms,
+        # profiles/r04/h/bench.json), which would set the two loops apart
+        time.sleep(0.5)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record(stream)
         for _ in range(reps):
@@ -438,6 +443,7 @@ def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto"):
         # the engine's kernels alone (HIP events around its launches inside
         # the call, rsg_set_kernel_timing), the median of `reps` more calls
         kms = []
+        time.sleep(0.5)
         _lib.check(L.rsg_set_kernel_timing(ctx, 1))
         try:
             ev[0].record(stream)
@@ -467,6 +473,7 @@ def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto"):
         verdicts, so the per-call time approaches the kernel time."""
         submit().wait()
         torch.cuda.synchronize()
+        time.sleep(0.5)  # from an idle GPU, as timed()
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record(stream)
         tk = submit()
