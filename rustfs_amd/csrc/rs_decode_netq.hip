@@ -1,31 +1,39 @@
-// rs_decode_net12.hip — the one-pass GET / heal kernel for RS(12,4), the
-// default geometry of a 16-drive set (storageclass.rs:24-31), with its rows
-// as compile-time XOR networks per erasure pattern (k_decode_records_net12
-// <PID>; networks in the generated rs124_decode_nets.h,
-// tools/gen_decode_nets.py --k 12).  Compiled RSG_NET_PARTS times (Makefile)
-// like rs_decode_net.hip.
+// rs_decode_netq.hip — the one-pass GET / heal kernel for RS(12,4), the
+// default geometry of a 16-drive set (storageclass.rs:24-31), with FOUR
+// network waves (k_decode_records_net12<PID>): its rows as compile-time XOR
+// networks per erasure pattern in four parts of the survivors (generated
+// rs124_decode_nets.h, tools/gen_decode_nets.py --k 12).  Compiled
+// RSG_NET_PARTS times (Makefile, RSG_NETQ_K=12) like rs_decode_net.hip.
 //
 // At 1 MiB blocks RS(12,4)'s shards are 87382 bytes, so its record walks are
 // ragged (170 whole 512-byte steps and 342 bytes, rs_records.h walk_tail) and
 // its records sit at every alignment (LDS-DMA takes unaligned sources).
 //
 // The workgroup is the table kernel's (k_decode_records_dma<12,NF,4,TH>: 4
-// stripes, NF = 14-15 present record files DMA'd into an LDS ring per
-// 512-byte step by 4 DMA + verify-hash waves) with the GF work done by FOUR
-// network waves, one per SIMD beside one hash wave each: wave q transposes
-// survivors 3q..3q+2 of the 4-stripe group (8 bytes of each stripe per lane)
-// into 24 bit planes, runs the pattern's net_q<PID, q> (its part of all R <= 4
-// rows), keeps its part of row q and XORs its parts of the other rows into
-// their accumulators in a double-buffered LDS area (LDS atomic XOR,
-// ds_xor_b32: 8 KiB a step, not 24 for the parts side by side, which leaves
-// the LDS room for a 4-slot ring — three steps of DMA in flight); one
-// interval later it XORs row q's accumulator in, transposes the row back and
-// stores it (rows [0, NST): rebuilt data / heal targets, heal also into the
-// target-row area for the target hashers) or compares it with the surplus
-// parity row it kept from the ring.  Two network waves over halves
-// (rs_decode_net16.hip's shape) left both on SIMDs shared with a hash wave at
-// about 600 VALU a step each (RS(12,4) GET with 2 data lost 1.52 ms,
-// profiles/r04/d/); a quarter wave issues about 330.
+// stripes, NF present record files DMA'd into an LDS ring per 512-byte step
+// by DMA + verify-hash waves) with the GF work done by four network waves,
+// one per SIMD beside a hash wave: wave q transposes survivors 3q..3q+2 of
+// the 4-stripe group (8 bytes of each stripe per lane) into 24 bit planes,
+// runs the pattern's net_q<PID, q> (its part of all R <= 4 rows), keeps its
+// part of row q and XORs its parts of the other rows into their
+// accumulators in a double-buffered LDS area (LDS atomic XOR, ds_xor_b32:
+// 8 KiB a step, not 24 for the parts side by side); one interval later it
+// XORs row q's accumulator in, transposes the row back and stores it (rows
+// [0, NST): rebuilt data / heal targets, heal also into the target-row area
+// for the target hashers) or compares it with the surplus parity row it kept
+// from the ring.
+//
+// Ring depth and workgroups per CU: GET takes a 2-slot ring, so two
+// workgroups (two hash and two network waves per SIMD) share a CU and each
+// hides the other's dependent hash chains and network latency — 2 data lost
+// 1.39 against 1.50 ms with one workgroup and a 4-slot ring (interleaved on
+// one box, profiles/r04/k/).  The heal's target rows do not fit two
+// workgroups' LDS; it keeps one and a 4-slot ring.  Two network waves over
+// halves (rs_decode_net16.hip's shape) ran GET 2 lost at 1.52 ms
+// (profiles/r04/d/): both shared a SIMD with a hash wave at ~600 VALU a step.
+// The same four-wave form for RS(8,4) (2 survivors a wave, 4-stripe
+// workgroups, two per CU) measured 3-4 % slower than rs_decode_net.hip's
+// 8-stripe workgroups (profiles/r04/l/) and is not built.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -40,27 +48,41 @@
 #ifndef RSG_NET_PART
 #error "RSG_NET_PART (0 .. RSG_NET_PARTS-1) is set by the Makefile"
 #endif
+#ifndef RSG_NETQ_K
+#error "RSG_NETQ_K (12 or 8) is set by the Makefile"
+#endif
+
+#define RSG_NETQ_CAT2(a, b) a##b
+#define RSG_NETQ_CAT(a, b) RSG_NETQ_CAT2(a, b)
+#if RSG_NETQ_K == 12
+#define RSG_NETQ_TAG net12
+#else
+#error "RSG_NETQ_K is 12 (RS(8,4) in this form measured slower: see the header)"
+#endif
+// k_decode_records_net12, launch_records_net12_partN, records_net12_pattern
+#define RSG_NETQ_NAME(pre, post) RSG_NETQ_CAT(RSG_NETQ_CAT(pre, RSG_NETQ_TAG), post)
 
 namespace rsg {
 
 #include "rs124_decode_nets.h"
+namespace decq = decnet12;
 
 namespace {
 
-constexpr int kK12 = 12, kNQ = 4, kQC = 3;  // data shards, network waves, survivors per wave
+constexpr int kKQ = RSG_NETQ_K, kNQ = 4, kQC = kKQ / 4;  // data shards, network waves, survivors per wave
 
-template <int NF, int TH>
-struct Net12Shape : RecRing<NF, 4, TH> {
+template <int NF, int TH, int RDX = 4>
+struct NetQShape : RecRing<NF, 4, TH> {
     static constexpr int WAVES = RecRing<NF, 4, TH>::HW + kNQ + RecRing<NF, 4, TH>::TW;
     static constexpr uint32_t XROW = 8 * 64 * 4;  // one row's accumulator: 8 planes, lane-major dwords (2 KiB)
     static constexpr uint32_t XSLOT = 4 * XROW;    // a step's exchange (8 KiB)
     static constexpr int XB = TH ? 1 : 0;          // extra barrier: heal's target hashers trail by 2 steps
-    static constexpr int RD = 4;                   // ring slots (three steps of DMA in flight)
+    static constexpr int RD = RDX;                 // ring slots (RD - 1 steps of DMA in flight)
     static constexpr uint32_t LDS = RD * RecRing<NF, 4, TH>::DSLOT + 2 * XSLOT +
                                     (TH ? 2 * RecRing<NF, 4, TH>::TSLOT : 16) + 32;
 };
 
-__device__ __forceinline__ void put8_12(uint8_t* p, const uint2& v) { st64_any(p, u64_of(v)); }  // any alignment
+__device__ __forceinline__ void put8_q(uint8_t* p, const uint2& v) { st64_any(p, u64_of(v)); }  // any alignment
 
 // Verdict of the compared rows, combined across the waves that finish them:
 // per-stripe mismatch bits OR-ed in and a count of waves done; the last one
@@ -71,18 +93,18 @@ struct Verdict {
 };
 
 // Network wave Q of the 4-stripe group (survivors 3Q..3Q+2).
-template <int PID, int NF, int TH, int Q>
-__device__ __forceinline__ void net12_wave(const GfApplyParams& p, uint64_t n, uint32_t steps, uint64_t s0,
+template <int PID, int NF, int TH, int Q, int RDX>
+__device__ __forceinline__ void netq_wave(const GfApplyParams& p, uint64_t n, uint32_t steps, uint64_t s0,
                                            const uint8_t* ring, uint8_t* xbuf, uint8_t* trow, Verdict* vd) {
     using dma::CH;
     using dma::IP;
     using dma::PP;
-    using L = Net12Shape<NF, TH>;
+    using L = NetQShape<NF, TH, RDX>;
     constexpr int D = L::RD;
-    constexpr decnet12::Pattern pat = decnet12::kPatterns[PID];
+    constexpr decq::Pattern pat = decq::kPatterns[PID];
     constexpr int R = pat.R, NST = pat.n_store, NCMP = R - NST, SPW = L::SPW, HS = L::HS;
     static_assert(pat.nf == NF && (pat.heal ? NST : 0) == TH && R <= kNQ && NST <= R && HS == 2, "pattern shape");
-    constexpr int C0 = kQC * Q;             // this wave's survivors [C0, C0 + 3)
+    constexpr int C0 = kQC * Q;             // this wave's survivors [C0, C0 + kQC)
     constexpr bool FIN = Q < R;             // it finishes row Q
     constexpr bool CMP = FIN && Q >= NST;   // ... a compared one (keeps surplus row Q - NST from the ring)
     if (p.wave_prio & kPrioGf) __builtin_amdgcn_s_setprio(2);
@@ -124,7 +146,7 @@ __device__ __forceinline__ void net12_wave(const GfApplyParams& p, uint64_t n, u
             for (int j = 0; j < 8; ++j) P[8 * c + j] = w[j];
         }
         uint32_t O[32];
-        decnet12::net_q<PID, Q>(P, O);
+        decq::net_q<PID, Q>(P, O);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             if (r == Q) continue;
@@ -137,7 +159,7 @@ __device__ __forceinline__ void net12_wave(const GfApplyParams& p, uint64_t n, u
 #pragma unroll
             for (int i = 0; i < 8; ++i) keep[i] = O[8 * Q + i];
         }
-        if constexpr (CMP) row4(slot + (kK12 + Q - NST) * HS * IP, cmp);
+        if constexpr (CMP) row4(slot + (kKQ + Q - NST) * HS * IP, cmp);
         if (!TH && cmask) {  // GET: this wave's present data survivors copied through
             const bool ragged = t + 1 == steps && tail != CH;  // wave-uniform
 #pragma unroll
@@ -148,7 +170,7 @@ __device__ __forceinline__ void net12_wave(const GfApplyParams& p, uint64_t n, u
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     if (!live[j]) continue;
-                    if (!ragged) put8_12(ob[j] + p.copy_off[C0 + c] + (uint64_t)t * CH, x[j]);
+                    if (!ragged) put8_q(ob[j] + p.copy_off[C0 + c] + (uint64_t)t * CH, x[j]);
                     else st64_part(ob[j] + p.copy_off[C0 + c] + (uint64_t)t * CH, u64_of(x[j]), lane * 8u, tail);
                 }
             }
@@ -171,7 +193,7 @@ __device__ __forceinline__ void net12_wave(const GfApplyParams& p, uint64_t n, u
             for (int j = 0; j < 4; ++j) {
                 const uint2 v = make_uint2(w[2 * j], w[2 * j + 1]);
                 if (live[j]) {
-                    if (!ragged) put8_12(ob[j] + p.out_off[Q] + (uint64_t)s * CH, v);
+                    if (!ragged) put8_q(ob[j] + p.out_off[Q] + (uint64_t)s * CH, v);
                     else st64_part(ob[j] + p.out_off[Q] + (uint64_t)s * CH, u64_of(v), lane * 8u, tail);
                 }
                 if constexpr (TH > 0) *(uint2*)(trow + (s & 1) * L::TSLOT + (Q * SPW + j) * PP + lane * 8u) = v;
@@ -235,10 +257,10 @@ __device__ __forceinline__ void net12_wave(const GfApplyParams& p, uint64_t n, u
 // ENC: the fused encode + HH256S (k_encode_hash_net12 below): the heal of
 // all four parity shards over a stripe buffer, every digest written to the
 // batch digest layout.
-template <int PID, int NF, int TH, bool ENC = false>
-__global__ __launch_bounds__((64 * Net12Shape<NF, TH>::WAVES)) void k_decode_records_net12(const GfApplyParams p,
-                                                                                           const HashParams h) {
-    using L = Net12Shape<NF, TH>;
+template <int PID, int NF, int TH, bool ENC = false, int RDX = 4>
+__global__ __launch_bounds__((64 * NetQShape<NF, TH>::WAVES)) void RSG_NETQ_NAME(k_decode_records_, )(
+    const GfApplyParams p, const HashParams h) {
+    using L = NetQShape<NF, TH, RDX>;
     __shared__ __attribute__((aligned(16))) uint8_t ring[L::RD * L::DSLOT];
     __shared__ __attribute__((aligned(16))) uint8_t xbuf[2 * L::XSLOT];
     __shared__ __attribute__((aligned(16))) uint8_t trow[TH ? 2 * L::TSLOT : 16];
@@ -253,58 +275,72 @@ __global__ __launch_bounds__((64 * Net12Shape<NF, TH>::WAVES)) void k_decode_rec
     if (wave >= (uint32_t)L::HW) {
         const uint32_t q = wave - L::HW;
         if (q == 0 && threadIdx.x % 64 == 0) vd = Verdict{0u, 0u};  // ordered before the compares by B(0)
-        if (q == 0) net12_wave<PID, NF, TH, 0>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
-        else if (q == 1) net12_wave<PID, NF, TH, 1>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
-        else if (q == 2) net12_wave<PID, NF, TH, 2>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
-        else net12_wave<PID, NF, TH, 3>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
+        if (q == 0) netq_wave<PID, NF, TH, 0, RDX>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
+        else if (q == 1) netq_wave<PID, NF, TH, 1, RDX>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
+        else if (q == 2) netq_wave<PID, NF, TH, 2, RDX>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
+        else netq_wave<PID, NF, TH, 3, RDX>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
         return;
     }
     records_hash_wave<NF, 4, L::XB, L::RD, ENC>(h, p.wave_prio, ring, wave, steps, s0);
 }
 
-static_assert(Net12Shape<15, 0>::LDS <= 160 * 1024 && Net12Shape<14, 0>::LDS <= 160 * 1024 &&
-                  Net12Shape<15, 1>::LDS <= 160 * 1024 && Net12Shape<14, 2>::LDS <= 160 * 1024,
+#if RSG_NETQ_K == 12
+static_assert(NetQShape<15, 0>::LDS <= 160 * 1024 && NetQShape<14, 0>::LDS <= 160 * 1024 &&
+                  NetQShape<15, 1>::LDS <= 160 * 1024 && NetQShape<14, 2>::LDS <= 160 * 1024,
               "RS(12,4) GET / heal workgroups fit the LDS");
+static_assert(NetQShape<15, 0, 2>::LDS <= 80 * 1024 && NetQShape<14, 0, 2>::LDS <= 80 * 1024,
+              "RS(12,4) GET with a 2-slot ring: two workgroups per CU");
+#endif
 
-using Net12Launch = void (*)(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream);
+using NetQLaunch = void (*)(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream);
 
 template <int PID>
-void launch_net12(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
-    constexpr decnet12::Pattern pat = decnet12::kPatterns[PID];
+void launch_netq(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
+    constexpr decq::Pattern pat = decq::kPatterns[PID];
     constexpr int NF = pat.nf, TH = pat.heal ? pat.n_store : 0;
-    hipLaunchKernelGGL((k_decode_records_net12<PID, NF, TH>), dim3((uint32_t)blocks),
-                       dim3(64 * Net12Shape<NF, TH>::WAVES), 0, stream, p, h);
+    // GET: a 2-slot ring and two workgroups per CU (RSG_NET12_RD=4: the
+    // 4-slot form); heal: its target rows do not fit two workgroups' LDS
+    const dim3 block(64 * NetQShape<NF, TH>::WAVES);
+    if constexpr (TH == 0) {
+        if (tuning().net12_rd == 2)
+            hipLaunchKernelGGL((RSG_NETQ_NAME(k_decode_records_, )<PID, NF, TH, false, 2>), dim3((uint32_t)blocks),
+                               block, 0, stream, p, h);
+        else
+            hipLaunchKernelGGL((RSG_NETQ_NAME(k_decode_records_, )<PID, NF, TH>), dim3((uint32_t)blocks), block, 0,
+                               stream, p, h);
+    } else {
+        hipLaunchKernelGGL((RSG_NETQ_NAME(k_decode_records_, )<PID, NF, TH>), dim3((uint32_t)blocks), block, 0,
+                           stream, p, h);
+    }
 }
 
 template <int PID>
-constexpr Net12Launch pick_net12() {
-    if constexpr (PID % RSG_NET_PARTS == RSG_NET_PART) return &launch_net12<PID>;
+constexpr NetQLaunch pick_netq() {
+    if constexpr (PID % RSG_NET_PARTS == RSG_NET_PART) return &launch_netq<PID>;
     else return nullptr;
 }
 
 template <size_t... I>
-constexpr std::array<Net12Launch, sizeof...(I)> net12_table(std::index_sequence<I...>) {
-    return {pick_net12<(int)I>()...};
+constexpr std::array<NetQLaunch, sizeof...(I)> netq_table(std::index_sequence<I...>) {
+    return {pick_netq<(int)I>()...};
 }
 
-const std::array<Net12Launch, decnet12::kCount> kNet12Part =
-    net12_table(std::make_index_sequence<decnet12::kCount>{});
+const std::array<NetQLaunch, decq::kCount> kNetQPart =
+    netq_table(std::make_index_sequence<decq::kCount>{});
 
 }  // namespace
 
-#define RSG_NET12_CAT2(a, b) a##b
-#define RSG_NET12_CAT(a, b) RSG_NET12_CAT2(a, b)
-
 // This part's launcher (launch_records_net12_partN): false if pattern `pid`
 // is instantiated elsewhere.
-bool RSG_NET12_CAT(launch_records_net12_part, RSG_NET_PART)(int pid, uint64_t blocks, const GfApplyParams& p,
-                                                           const HashParams& h, hipStream_t stream) {
-    if (pid < 0 || pid >= decnet12::kCount || !kNet12Part[pid]) return false;
-    kNet12Part[pid](blocks, p, h, stream);
+bool RSG_NETQ_NAME(launch_records_, RSG_NETQ_CAT(_part, RSG_NET_PART))(int pid, uint64_t blocks,
+                                                                       const GfApplyParams& p, const HashParams& h,
+                                                                       hipStream_t stream) {
+    if (pid < 0 || pid >= decq::kCount || !kNetQPart[pid]) return false;
+    kNetQPart[pid](blocks, p, h, stream);
     return true;
 }
 
-#if RSG_NET_PART == 0
+#if RSG_NET_PART == 0 && RSG_NETQ_K == 12
 // The fused encode + HH256S of RS(12,4) (BitrotWriter over an encoded block,
 // bitrot.rs:464-510 after erasure encode): the heal kernel of all four parity
 // shards (pattern kEncodePid, rows = the encode matrix) walking the data
@@ -313,22 +349,22 @@ bool RSG_NET12_CAT(launch_records_net12_part, RSG_NET_PART)(int pid, uint64_t bl
 // hasher — every digest to h.out (stripe-major, 16 per stripe).
 namespace {
 constexpr int encode_pid() {
-    for (int i = 0; i < decnet12::kCount; ++i)
-        if (decnet12::kPatterns[i].heal && decnet12::kPatterns[i].absent == 0xF000) return i;
+    for (int i = 0; i < decq::kCount; ++i)
+        if (decq::kPatterns[i].heal && decq::kPatterns[i].absent == 0xF000) return i;
     return -1;
 }
 constexpr int kEncodePid = encode_pid();
-static_assert(kEncodePid >= 0 && decnet12::kPatterns[kEncodePid].nf == 12 && decnet12::kPatterns[kEncodePid].R == 4,
+static_assert(kEncodePid >= 0 && decq::kPatterns[kEncodePid].nf == 12 && decq::kPatterns[kEncodePid].R == 4,
               "rs124_decode_nets.h lists the heal of every parity shard");
 }  // namespace
 
-const uint8_t* encode_net12_coef() { return &decnet12::kPatterns[kEncodePid].coef[0][0]; }
+const uint8_t* encode_net12_coef() { return &decq::kPatterns[kEncodePid].coef[0][0]; }
 
 // p: the encode's table-GF launch (in place: base == out_base, in_off = the
 // data shards, out_off = the parity shards); h: key, out (digests).
 hipError_t launch_encode_hash_net12(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                     hipStream_t stream) {
-    using L = Net12Shape<12, 4>;
+    using L = NetQShape<12, 4>;
     if (p.C != 12 || p.R != 4 || n_stripes == 0 || shard_len == 0 || p.base != p.out_base ||
         p.stripe_stride != p.out_stripe_stride || 5 * p.stripe_stride >= (1ull << 32) ||
         (n_stripes + L::SPW - 1) / L::SPW > 0x7fffffffull || (shard_len + dma::CH - 1) / dma::CH > 0xffffffffull)
@@ -349,15 +385,18 @@ hipError_t launch_encode_hash_net12(GfApplyParams p, HashParams h, uint64_t shar
     return hipGetLastError();
 }
 
-// The pattern whose coefficient rows equal the launch's (R x 12, row-major),
-// or -1.
-int records_net12_pattern(int heal, int nf, int R, int n_store, const uint8_t* coef) {
-    for (int i = 0; i < decnet12::kCount; ++i) {
-        const decnet12::Pattern& pt = decnet12::kPatterns[i];
+#endif
+
+#if RSG_NET_PART == 0
+// The pattern whose coefficient rows equal the launch's (R x K, row-major),
+// or -1 (records_net12_pattern).
+int RSG_NETQ_NAME(records_, _pattern)(int heal, int nf, int R, int n_store, const uint8_t* coef) {
+    for (int i = 0; i < decq::kCount; ++i) {
+        const decq::Pattern& pt = decq::kPatterns[i];
         if (pt.heal != heal || pt.nf != nf || pt.R != R || pt.n_store != n_store) continue;
         bool eq = true;
         for (int r = 0; r < R && eq; ++r)
-            for (int c = 0; c < kK12 && eq; ++c) eq = pt.coef[r][c] == coef[r * kK12 + c];
+            for (int c = 0; c < kKQ && eq; ++c) eq = pt.coef[r][c] == coef[r * kKQ + c];
         if (eq) return i;
     }
     return -1;

@@ -40,6 +40,7 @@ struct Tuning {
     int dma_spw = 8;              // RSG_DMA_SPW=4: four stripes per fused DMA workgroup
     int get_prio = 2;             // RSG_DMA_PRIO=<0..3>: wave priorities of the one-pass GET/heal
     bool decode_net = true;       // RSG_DECODE_NET=0: run-time-table GF waves for every one-pass pattern
+    int net12_rd = 2;             // RSG_NET12_RD=4: RS(12,4) GET ring of 4 slots, one workgroup per CU (A/B)
     bool get_cached = true;       // RSG_GET_CACHED=0: non-temporal output stores in the network GET/heal kernel
 };
 const Tuning& tuning();
@@ -168,7 +169,7 @@ RSG_NET16_PART_DECL(4)
 RSG_NET16_PART_DECL(5)
 RSG_NET16_PART_DECL(6)
 RSG_NET16_PART_DECL(7)
-// RS(12,4) (rs_decode_net12.hip, k_decode_records_net12): the same for R x 12 rows
+// RS(12,4) (rs_decode_netq.hip, k_decode_records_net12): the same for R x 12 rows
 int records_net12_pattern(int heal, int nf, int R, int n_store, const uint8_t* coef);
 #define RSG_NET16_PART_DECL12(i)                                                                               \
     bool launch_records_net12_part##i(int pid, uint64_t blocks, const GfApplyParams& p, const HashParams& h, \

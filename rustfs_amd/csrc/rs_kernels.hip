@@ -1148,6 +1148,7 @@ const Tuning& tuning() {
         v.dma_spw = num("RSG_DMA_SPW", 8, 4, 8) == 4 ? 4 : 8;
         v.get_prio = num("RSG_DMA_PRIO", 2, 0, 3);
         v.decode_net = flag("RSG_DECODE_NET", true);
+        v.net12_rd = num("RSG_NET12_RD", 2, 2, 4) == 4 ? 4 : 2;
         v.get_cached = flag("RSG_GET_CACHED", true);
         return v;
     }();

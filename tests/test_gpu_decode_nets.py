@@ -324,7 +324,8 @@ L = _lib.load()
 _lib.check(L.rsg_set_record_engine(_lib.context(0).handle, _lib.RSG_RECORD_ENGINE_ONE_PASS))
 S = 1024
 REC = 32 + S
-for k, n, gets, heals in ((8, 19, [(0, 3), (2, 9), (5,)], [(1, 8), (0, 11), (4,)]), (16, 11, [(0, 3)], [(1, 16)])):
+for k, n, gets, heals in ((8, 19, [(0, 3), (2, 9), (5,)], [(1, 8), (0, 11), (4,)]), (16, 11, [(0, 3)], [(1, 16)]),
+                          (12, 7, [(0, 3), (1,)], [(2, 13)])):
     t = k + 4
     rng = np.random.default_rng(k)
     shards = np.zeros((n, t, S), dtype=np.uint8)
@@ -350,13 +351,14 @@ print("ok")
 """
 
 
-@pytest.mark.parametrize("env", [{"RSG_DECODE_NET": "0"}, {"RSG_GET_CACHED": "0"}])
+@pytest.mark.parametrize("env", [{"RSG_DECODE_NET": "0"}, {"RSG_GET_CACHED": "0"}, {"RSG_NET12_RD": "4"}])
 def test_network_knobs_in_own_process(gpu, oracle, env):
     """The A/B knobs of the network GET/heal path (read once per process, so
     each in its own process): RSG_DECODE_NET=0 sends listed RS(8,4) patterns
     to the run-time-table one-pass kernel and RS(16,4) heal to the two-pass
-    path; RSG_GET_CACHED=0 makes the network kernels' stores non-temporal.
-    Bit-exact against the oracle either way."""
+    path; RSG_GET_CACHED=0 makes the RS(8,4) network kernel's stores
+    non-temporal; RSG_NET12_RD=4 runs RS(12,4)'s GET on a 4-slot ring, one
+    workgroup per CU.  Bit-exact against the oracle either way."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -29,8 +29,10 @@ fit one wave's registers beside the rows, so each pattern gets one network
 per part of the survivors, each producing all R rows, and the kernel XORs the
 parts: RS(16,4) two (survivors 0-7 / 8-15, rs_decode_net16.hip,
 rs164_decode_nets.h `net_lo` / `net_hi`), RS(12,4) four (0-2 / 3-5 / 6-8 /
-9-11, one network wave per SIMD, rs_decode_net12.hip, rs124_decode_nets.h
-`net_q<PID, Q>`).
+9-11, one network wave per SIMD, rs_decode_netq.hip, rs124_decode_nets.h
+`net_q<PID, Q>`).  `--quarters` writes RS(8,4) in the same four-part form
+(rs84q_decode_nets.h): measured 3-4 % slower than the one-wave RS(8,4)
+networks (DESIGN.md, profiles/r04/l/) and not built.
 
 Usage: python tools/gen_decode_nets.py [seeds] [--k 16|12] [--only heal:1,16 get:0,3 ...]
 (writes the header)
@@ -207,6 +209,9 @@ def main():
         i = args.index("--only")
         only = set(args[i + 1:])
         del args[i:]
+    quarters = "--quarters" in args  # RS(8,4) in four parts of 2 survivors (rs_decode_netq.hip)
+    if quarters:
+        args.remove("--quarters")
     seeds = int(args[0]) if args else 4
     set_geometry(k, 4)
     pats = patterns()
@@ -217,12 +222,15 @@ def main():
     # SIMD, rs_decode_net12.hip)
     ka = 8
     halves = {8: [(0, 8)], 16: [(0, 8), (8, 8)], 12: [(0, 3), (3, 3), (6, 3), (9, 3)]}[K]
+    if quarters:
+        halves = [(c0, K // 4) for c0 in range(0, K, K // 4)]
     tasks = [(p[5], seeds, c0, cn) for c0, cn in halves for p in pats]
     with multiprocessing.Pool(min(8, os.cpu_count() or 1)) as pool:
         res = pool.map(best_network, tasks)
     nets = [res[h * len(pats):(h + 1) * len(pats)] for h in range(len(halves))]
     ops = [sum(n[i][0] for n in nets) for i in range(len(pats))]
-    name = "rs84_decode_nets.h" if K == 8 else f"rs{K}{M}_decode_nets.h"
+    name = ("rs84q_decode_nets.h" if quarters else "rs84_decode_nets.h") if K == 8 else f"rs{K}{M}_decode_nets.h"
+    space = f"decnet{'' if K == 8 and not quarters else K}{'q' if quarters else ''}"
     hdr = [
         f"// {name} — GENERATED by tools/gen_decode_nets.py (do not edit).",
         f"// RS({K},{M}) one-pass GET / heal rows as compile-time three-input XOR networks,",
@@ -230,11 +238,11 @@ def main():
         f"// {min(ops)}-{max(ops)} ops each (mean {sum(ops) / len(ops):.0f}).  P[c*8+j] = bit plane j of",
         f"// survivor c (the first {K} present shards{'' if K == 8 else ', in parts ' + ', '.join(f'{c0}-{c0 + cn - 1}' for c0, cn in halves)}), O[r*8+i] = bit plane i of row r",
         "// (rows [0, n_store) stored, the rest compared with the present",
-        "// non-survivor parity in ascending order).  Included by rs_decode_net.hip",
+        f"// non-survivor parity in ascending order).  Included by {'rs_decode_net.hip' if K == 8 and not quarters else 'rs_decode_net16.hip' if K == 16 else 'rs_decode_netq.hip'}",
         "// inside namespace rsg, after x3().",
         "#pragma once",
         "",
-        f"namespace decnet{'' if K == 8 else K} {{",
+        f"namespace {space} {{",
         "",
         "struct Pattern {",
         "    uint16_t absent;  // bit i: shard i lost" if T <= 16 else "    uint32_t absent;  // bit i: shard i lost",
@@ -253,13 +261,14 @@ def main():
         cs = ", ".join("{" + ", ".join(str(x) for x in r) + "}" for r in rr)
         hdr.append(f"    {{0x{mask:03x}, {heal}, {nf}, {R}, {nst}, {{{cs}}}}},  // {pid}")
     hdr += ["};", ""]
-    if K == 8:
+    if K == 8 and not quarters:
         hdr += ["template <int PID>", "__device__ void net(const uint32_t (&P)[64], uint32_t (&O)[32]);", ""]
         for pid, pat in enumerate(pats):
             hdr += emit_net(pid, pat, nets[0][pid])
             hdr.append("")
-    elif K == 12:
-        hdr += ["// net_q<PID, Q>: all rows over survivors 3Q-3Q+2 (planes P[0..24))",
+    elif K == 12 or quarters:
+        qc = K // 4
+        hdr += [f"// net_q<PID, Q>: all rows over survivors {qc}Q-{qc}Q+{qc - 1} (planes P[0..{8 * qc}))",
                 "template <int PID, int Q>", "__device__ void net_q(const uint32_t (&P)[64], uint32_t (&O)[32]);", ""]
         for pid, pat in enumerate(pats):
             for q, (c0, cn) in enumerate(halves):
@@ -274,7 +283,7 @@ def main():
             hdr += emit_net(pid, pat, nets[0][pid], "net_lo", f", survivors 0-{ka - 1}")
             hdr += emit_net(pid, pat, nets[1][pid], "net_hi", f", survivors {ka}-{K - 1}")
             hdr.append("")
-    hdr.append(f"}}  // namespace decnet{'' if K == 8 else K}")
+    hdr.append(f"}}  // namespace {space}")
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "rustfs_amd", "csrc", name)
     with open(path, "w") as f:
         f.write("\n".join(hdr) + "\n")

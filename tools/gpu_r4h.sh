@@ -19,4 +19,6 @@ for CTRS in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS
   done
   EP_K=8 timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $CTRS -d $OUT/k8_heal/p$i -o run --output-format csv -- python3 $R/tools/engine_prof.py heal 3 > $OUT/k8_heal_p$i.txt 2>&1 || exit $?
 done
+cd $R
+timeout -k 10 400 python -u bench.py --no-cpu-baseline > $OUT/bench.json 2> $OUT/bench.err || exit 1
 echo done
