@@ -545,7 +545,7 @@ def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto"):
                     n * ((t - 2) * rec + 2 * rec), ok_heal)
     timed("bitrot_verify_all_files",
           lambda: bitrot_verify_batch(files, n * rec, n * S, HashAlgorithm.HighwayHash256S, S, stream=stream),
-          t * n * rec, ok_verify)
+          t * n * rec, ok_verify, traffic_key=f"verify_all_rs{k}{m}_S{S}_n{n}")
     del files, lost, tg, src, out, slots
     torch.cuda.empty_cache()
     return res
@@ -655,6 +655,7 @@ def main(argv=None):
             extras[f"reconstruct_e{len(miss)}"] = {
                 "GiB_s_payload": round(payload / (ms * 1e-3) / GiB, 2),
                 "kernel_ms": round(ms, 4), "alg_bytes": rb,
+                "traffic": pmc_lookup(f"reconstruct_e{len(miss)}_rs{k}{m}_S{S}_n{n}"),
                 "hbm_GB_s": round(rb / (ms * 1e-3) / 1e9, 1),
                 "frac": round(rb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
         # round trip correctness of the last pattern (cheap, on device)
