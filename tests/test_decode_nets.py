@@ -164,3 +164,55 @@ def test_rs16_decode_nets_rebuild_true_shards(oracle):
         hi = _run(_program(src, p["pid"], "net_hi"), _planes(st[files[8:16]]))
         got = _bytes([a ^ b for a, b in zip(lo, hi)], p["R"])
         assert np.array_equal(got, st[want_idx]), p["pid"]
+
+
+# ---------------------------------------------------------------- RS(12,4)
+HEADER12 = os.path.join(ROOT, "rustfs_amd", "csrc", "rs124_decode_nets.h")
+
+
+def test_rs12_decode_nets_rebuild_true_shards(oracle):
+    """RS(12,4) (rs124_decode_nets.h, k_decode_records_net12, four network
+    waves): per pattern the four part networks over survivors 0-2, 3-5, 6-8
+    and 9-11, XOR-combined, must give the true shards; the table is every 1-
+    and 2-shard loss (GET: a data shard lost; heal: every loss) plus the heal
+    of all four parity shards — the fused encode's rows, which must be the
+    oracle's encode matrix — and its rows are the oracle's decode matrix rows."""
+    k, t = 12, 16
+    src = open(HEADER12).read()
+    pats = []
+    for m in re.finditer(r"\{0x([0-9a-f]+), (\d), (\d+), (\d), (\d), \{(.*?)\}\},  // (\d+)", src):
+        rows = [[int(x) for x in r.split(",")] for r in re.findall(r"\{([0-9, ]+)\}", m.group(6))]
+        pats.append(dict(absent=int(m.group(1), 16), heal=int(m.group(2)), nf=int(m.group(3)), R=int(m.group(4)),
+                         nst=int(m.group(5)), coef=rows, pid=int(m.group(7))))
+    assert len(pats) == int(re.search(r"kCount = (\d+)", src).group(1))
+    assert sum(1 for p in pats if p["heal"]) == 16 + 120 + 1
+    assert sum(1 for p in pats if not p["heal"]) == 12 + 114
+    enc = [p for p in pats if p["heal"] and p["absent"] == 0xF000]
+    assert len(enc) == 1
+    gm = oracle.matrix(k, 4)
+    assert enc[0]["coef"] == [[int(x) for x in gm[k + r]] for r in range(4)]
+    rng = np.random.default_rng(124)
+    for p in pats:
+        lost = [i for i in range(t) if p["absent"] >> i & 1]
+        files = [i for i in range(t) if i not in lost]
+        store = lost if p["heal"] else [i for i in lost if i < k]
+        want_idx = store + files[k:]
+        assert p["R"] == len(want_idx) and p["nst"] == len(store) and p["nf"] == len(files)
+        inv = oracle.invert(gm[files[:k]])
+        for r, idx in enumerate(want_idx):
+            row = []
+            for c in range(k):
+                a = 0
+                for i in range(k):
+                    a ^= oracle.gf_mul(int(gm[idx][i]), int(inv[i][c]))
+                row.append(a)
+            assert row == p["coef"][r], (p["pid"], r)
+        st = np.zeros((t, 32), dtype=np.uint8)
+        st[:k] = rng.integers(0, 256, (k, 32), dtype=np.uint8)
+        oracle.encode(k, 4, st)
+        acc = [0] * 32
+        for q in range(4):
+            part = _run(_program(src, f"{p['pid']}, {q}", "net_q"), _planes(st[files[3 * q:3 * q + 3]]))
+            acc = [a ^ b for a, b in zip(acc, part)]
+        got = _bytes(acc, p["R"])
+        assert np.array_equal(got, st[want_idx]), p["pid"]
