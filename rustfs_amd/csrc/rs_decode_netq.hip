@@ -71,15 +71,22 @@ namespace {
 
 constexpr int kKQ = RSG_NETQ_K, kNQ = 4, kQC = kKQ / 4;  // data shards, network waves, survivors per wave
 
-template <int NF, int TH, int RDX = 4>
+// ENC (the fused encode): the accumulators are also the target-row area —
+// a row's finisher writes its bytes over the accumulator it has just read and
+// the target hasher clears it after hashing it, so three slots (the hasher
+// trails two steps) replace two slots plus the double-buffered row area.
+template <int NF, int TH, int RDX = 4, bool ENC = false>
 struct NetQShape : RecRing<NF, 4, TH> {
     static constexpr int WAVES = RecRing<NF, 4, TH>::HW + kNQ + RecRing<NF, 4, TH>::TW;
-    static constexpr uint32_t XROW = 8 * 64 * 4;  // one row's accumulator: 8 planes, lane-major dwords (2 KiB)
-    static constexpr uint32_t XSLOT = 4 * XROW;    // a step's exchange (8 KiB)
+    // one row's accumulator: 8 planes, lane-major dwords (2 KiB); ENC: also
+    // the row's 4 stripes at the target hasher's pitch
+    static constexpr uint32_t XROW = ENC ? 4 * dma::PP : 8 * 64 * 4;
+    static constexpr uint32_t XSLOT = 4 * XROW;    // a step's exchange (8-8.5 KiB)
+    static constexpr int NXB = ENC ? 3 : 2;        // exchange slots
     static constexpr int XB = TH ? 1 : 0;          // extra barrier: heal's target hashers trail by 2 steps
     static constexpr int RD = RDX;                 // ring slots (RD - 1 steps of DMA in flight)
-    static constexpr uint32_t LDS = RD * RecRing<NF, 4, TH>::DSLOT + 2 * XSLOT +
-                                    (TH ? 2 * RecRing<NF, 4, TH>::TSLOT : 16) + 32;
+    static constexpr uint32_t LDS = RD * RecRing<NF, 4, TH>::DSLOT + NXB * XSLOT +
+                                    (TH && !ENC ? 2 * RecRing<NF, 4, TH>::TSLOT : 16) + 32;
 };
 
 __device__ __forceinline__ void put8_q(uint8_t* p, const uint2& v) { st64_any(p, u64_of(v)); }  // any alignment
@@ -93,13 +100,13 @@ struct Verdict {
 };
 
 // Network wave Q of the 4-stripe group (survivors 3Q..3Q+2).
-template <int PID, int NF, int TH, int Q, int RDX>
+template <int PID, int NF, int TH, int Q, int RDX, bool ENC>
 __device__ __forceinline__ void netq_wave(const GfApplyParams& p, uint64_t n, uint32_t steps, uint64_t s0,
                                            const uint8_t* ring, uint8_t* xbuf, uint8_t* trow, Verdict* vd) {
     using dma::CH;
     using dma::IP;
     using dma::PP;
-    using L = NetQShape<NF, TH, RDX>;
+    using L = NetQShape<NF, TH, RDX, ENC>;
     constexpr int D = L::RD;
     constexpr decq::Pattern pat = decq::kPatterns[PID];
     constexpr int R = pat.R, NST = pat.n_store, NCMP = R - NST, SPW = L::SPW, HS = L::HS;
@@ -130,7 +137,9 @@ __device__ __forceinline__ void netq_wave(const GfApplyParams& p, uint64_t n, ui
     uint32_t keep[8];   // step t-1's part of row Q, held across B(t)
     uint2 cmp[4];       // CMP: step t-1's surplus row, held across B(t)
     // row r's accumulator of step t, lane-major
-    auto xb_at = [&](int r, uint32_t t) { return (uint32_t*)(xbuf + (t & 1) * L::XSLOT + r * L::XROW) + lane; };
+    auto xb_at = [&](int r, uint32_t t) {
+        return (uint32_t*)(xbuf + (t % L::NXB) * L::XSLOT + r * L::XROW) + lane;
+    };
     // step t: this wave's 3 survivors -> 24 planes -> its part of every row;
     // the other rows' parts out to LDS; copy-through of its data survivors (GET)
     auto part = [&](uint32_t t) {
@@ -185,8 +194,10 @@ __device__ __forceinline__ void netq_wave(const GfApplyParams& p, uint64_t n, ui
         uint32_t w[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) w[i] = keep[i] ^ xa[64 * i];
+        if constexpr (!ENC) {  // ENC: the target hasher clears it
 #pragma unroll
-        for (int i = 0; i < 8; ++i) xa[64 * i] = 0u;
+            for (int i = 0; i < 8; ++i) xa[64 * i] = 0u;
+        }
         dma::transpose(w, m4, m2, m1);
         if constexpr (Q < NST) {
 #pragma unroll
@@ -196,7 +207,16 @@ __device__ __forceinline__ void netq_wave(const GfApplyParams& p, uint64_t n, ui
                     if (!ragged) put8_q(ob[j] + p.out_off[Q] + (uint64_t)s * CH, v);
                     else st64_part(ob[j] + p.out_off[Q] + (uint64_t)s * CH, u64_of(v), lane * 8u, tail);
                 }
-                if constexpr (TH > 0) *(uint2*)(trow + (s & 1) * L::TSLOT + (Q * SPW + j) * PP + lane * 8u) = v;
+                if constexpr (ENC)  // over the accumulator just read
+                    *(uint2*)(xbuf + (s % L::NXB) * L::XSLOT + Q * L::XROW + j * PP + lane * 8u) = v;
+                else if constexpr (TH > 0)
+                    *(uint2*)(trow + (s & 1) * L::TSLOT + (Q * SPW + j) * PP + lane * 8u) = v;
+            }
+            if constexpr (ENC) {  // the accumulator's words the rows' pitch skips (the hasher clears the rest)
+                static_assert(PP - dma::CH == 32 && L::XROW >= 8 * 64 * 4, "row pitch against the plane words");
+                if (lane < 24u)
+                    *(uint32_t*)(xbuf + (s % L::NXB) * L::XSLOT + Q * L::XROW + dma::CH + (lane / 8u) * PP +
+                                 (lane % 8u) * 4u) = 0u;
             }
         } else if (!ragged) {
 #pragma unroll
@@ -211,9 +231,11 @@ __device__ __forceinline__ void netq_wave(const GfApplyParams& p, uint64_t n, ui
             }
         }
     };
-    if constexpr (FIN) {  // both accumulators of row Q start cleared
+    if constexpr (FIN) {  // every accumulator of row Q starts cleared
 #pragma unroll
-        for (int i = 0; i < 8; ++i) xb_at(Q, 0)[64 * i] = xb_at(Q, 1)[64 * i] = 0u;
+        for (int b = 0; b < L::NXB; ++b)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) xb_at(Q, b)[64 * i] = 0u;
     }
     lds_barrier();  // B(0)
     if constexpr (!FIN) {  // R = 3: wave 3 hands its parts over only
@@ -260,25 +282,28 @@ __device__ __forceinline__ void netq_wave(const GfApplyParams& p, uint64_t n, ui
 template <int PID, int NF, int TH, bool ENC = false, int RDX = 4>
 __global__ __launch_bounds__((64 * NetQShape<NF, TH>::WAVES)) void RSG_NETQ_NAME(k_decode_records_, )(
     const GfApplyParams p, const HashParams h) {
-    using L = NetQShape<NF, TH, RDX>;
+    using L = NetQShape<NF, TH, RDX, ENC>;
     __shared__ __attribute__((aligned(16))) uint8_t ring[L::RD * L::DSLOT];
-    __shared__ __attribute__((aligned(16))) uint8_t xbuf[2 * L::XSLOT];
-    __shared__ __attribute__((aligned(16))) uint8_t trow[TH ? 2 * L::TSLOT : 16];
+    __shared__ __attribute__((aligned(16))) uint8_t xbuf[L::NXB * L::XSLOT];
+    __shared__ __attribute__((aligned(16))) uint8_t trow[TH && !ENC ? 2 * L::TSLOT : 16];
     __shared__ Verdict vd;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t steps = p.units;
     const uint64_t s0 = (uint64_t)blockIdx.x * L::SPW;
     if (TH && wave >= (uint32_t)(L::HW + kNQ)) {
-        records_target_hasher<4, TH, 2, ENC>(p, h, trow, wave - L::HW - kNQ, steps, s0);
+        if constexpr (ENC)  // the target rows in the exchange slots, cleared once hashed
+            records_target_hasher<4, TH, 2, true, L::NXB, L::XSLOT, true>(p, h, xbuf, wave - L::HW - kNQ, steps, s0);
+        else
+            records_target_hasher<4, TH, 2>(p, h, trow, wave - L::HW - kNQ, steps, s0);
         return;
     }
     if (wave >= (uint32_t)L::HW) {
         const uint32_t q = wave - L::HW;
         if (q == 0 && threadIdx.x % 64 == 0) vd = Verdict{0u, 0u};  // ordered before the compares by B(0)
-        if (q == 0) netq_wave<PID, NF, TH, 0, RDX>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
-        else if (q == 1) netq_wave<PID, NF, TH, 1, RDX>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
-        else if (q == 2) netq_wave<PID, NF, TH, 2, RDX>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
-        else netq_wave<PID, NF, TH, 3, RDX>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
+        if (q == 0) netq_wave<PID, NF, TH, 0, RDX, ENC>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
+        else if (q == 1) netq_wave<PID, NF, TH, 1, RDX, ENC>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
+        else if (q == 2) netq_wave<PID, NF, TH, 2, RDX, ENC>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
+        else netq_wave<PID, NF, TH, 3, RDX, ENC>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
         return;
     }
     records_hash_wave<NF, 4, L::XB, L::RD, ENC>(h, p.wave_prio, ring, wave, steps, s0);
@@ -288,8 +313,9 @@ __global__ __launch_bounds__((64 * NetQShape<NF, TH>::WAVES)) void RSG_NETQ_NAME
 static_assert(NetQShape<15, 0>::LDS <= 160 * 1024 && NetQShape<14, 0>::LDS <= 160 * 1024 &&
                   NetQShape<15, 1>::LDS <= 160 * 1024 && NetQShape<14, 2>::LDS <= 160 * 1024,
               "RS(12,4) GET / heal workgroups fit the LDS");
-static_assert(NetQShape<15, 0, 2>::LDS <= 80 * 1024 && NetQShape<14, 0, 2>::LDS <= 80 * 1024,
-              "RS(12,4) GET with a 2-slot ring: two workgroups per CU");
+static_assert(NetQShape<15, 0, 2>::LDS <= 80 * 1024 && NetQShape<14, 0, 2>::LDS <= 80 * 1024 &&
+                  NetQShape<12, 4, 2, true>::LDS <= 80 * 1024,
+              "RS(12,4) GET and fused encode with a 2-slot ring: two workgroups per CU");
 #endif
 
 using NetQLaunch = void (*)(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream);
@@ -380,8 +406,13 @@ hipError_t launch_encode_hash_net12(GfApplyParams p, HashParams h, uint64_t shar
     h.stripe_stride = p.stripe_stride;
     h.nbases = 12;
     for (int c = 0; c < 12; ++c) h.base[c] = p.base + p.in_off[c];
-    hipLaunchKernelGGL((k_decode_records_net12<kEncodePid, 12, 4, true>),
-                       dim3((uint32_t)((n_stripes + L::SPW - 1) / L::SPW)), dim3(64 * L::WAVES), 0, stream, p, h);
+    // two workgroups per CU on a 2-slot ring (RSG_NET12_RD=4: one, 4 slots)
+    if (tuning().net12_rd == 2)
+        hipLaunchKernelGGL((k_decode_records_net12<kEncodePid, 12, 4, true, 2>),
+                           dim3((uint32_t)((n_stripes + L::SPW - 1) / L::SPW)), dim3(64 * L::WAVES), 0, stream, p, h);
+    else
+        hipLaunchKernelGGL((k_decode_records_net12<kEncodePid, 12, 4, true, 4>),
+                           dim3((uint32_t)((n_stripes + L::SPW - 1) / L::SPW)), dim3(64 * L::WAVES), 0, stream, p, h);
     return hipGetLastError();
 }
 

@@ -363,6 +363,31 @@ constexpr uint32_t vmcnt_imm(int n) {
 }
 
 // 16 packets of one stream (8 B per lane, 32 B apart) from LDS, one asm.
+// zeros over the 16 8-byte words read16 reads at LDS address a
+__device__ __forceinline__ void zero16(uint32_t a) {
+    const uint64_t z = 0;
+    asm volatile(
+        "ds_write_b64 %0, %1 offset:0\n\t"
+        "ds_write_b64 %0, %1 offset:32\n\t"
+        "ds_write_b64 %0, %1 offset:64\n\t"
+        "ds_write_b64 %0, %1 offset:96\n\t"
+        "ds_write_b64 %0, %1 offset:128\n\t"
+        "ds_write_b64 %0, %1 offset:160\n\t"
+        "ds_write_b64 %0, %1 offset:192\n\t"
+        "ds_write_b64 %0, %1 offset:224\n\t"
+        "ds_write_b64 %0, %1 offset:256\n\t"
+        "ds_write_b64 %0, %1 offset:288\n\t"
+        "ds_write_b64 %0, %1 offset:320\n\t"
+        "ds_write_b64 %0, %1 offset:352\n\t"
+        "ds_write_b64 %0, %1 offset:384\n\t"
+        "ds_write_b64 %0, %1 offset:416\n\t"
+        "ds_write_b64 %0, %1 offset:448\n\t"
+        "ds_write_b64 %0, %1 offset:480"
+        :
+        : "v"(a), "v"(z)
+        : "memory");
+}
+
 __device__ __forceinline__ void read16(uint32_t a, uint64_t (&w)[16]) {
     asm volatile(
         "ds_read_b64 %0, %16 offset:0\n\t"

@@ -213,13 +213,16 @@ __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t 
 // interval its data is in the ring), and writes the target record's digest
 // header in front of its body at out_base + stripe * out_stripe_stride +
 // out_off[r] - 32 (ENC: parity row r's digest to the batch digest layout, as
-// shard p.C + r).  steps + LAG barriers.
-template <int G, int TH, int LAG = 1, bool ENC = false>
+// shard p.C + r).  steps + LAG barriers.  The row area has NS slots of SLOT
+// bytes (0: RecRing's TSLOT) used round robin; ZERO: each row cleared once
+// hashed (k_decode_records_net12's fused encode keeps its rows in the
+// network waves' accumulators).
+template <int G, int TH, int LAG = 1, bool ENC = false, int NS = 2, uint32_t SLOT = 0, bool ZERO = false>
 __device__ __forceinline__ void records_target_hasher(const GfApplyParams& p, const HashParams& h,
                                                       const uint8_t* trow, uint32_t tw, uint32_t steps,
                                                       uint64_t s0) {
     constexpr int SPW = G;
-    constexpr uint32_t TSLOT = RecRing<1, G, TH>::TSLOT;
+    constexpr uint32_t TSLOT = SLOT ? SLOT : RecRing<1, G, TH>::TSLOT;
     if (p.wave_prio & kPrioHash) __builtin_amdgcn_s_setprio(2);
     const uint32_t lane = threadIdx.x & 63u, q = lane & 3u;
     const uint32_t pi = 16 * tw + (lane >> 2);  // r * SPW + stripe
@@ -234,7 +237,7 @@ __device__ __forceinline__ void records_target_hasher(const GfApplyParams& p, co
 #pragma unroll 1
     for (uint32_t t = 0; t < steps + LAG; ++t) {
         if (t >= (uint32_t)LAG) {  // target rows of step t-LAG, published by B(t)
-            const uint32_t base = (uint32_t)(uintptr_t)trow + ((t - LAG) & 1) * TSLOT + roff;
+            const uint32_t base = (uint32_t)(uintptr_t)trow + ((t - LAG) % NS) * TSLOT + roff;
             uint64_t w[16];
             dma::read16(base, w);
             if (t - LAG + 1 < steps || tail == dma::CH) {
@@ -246,7 +249,10 @@ __device__ __forceinline__ void records_target_hasher(const GfApplyParams& p, co
                 for (int i = 0; i < 16; ++i)
                     if ((uint32_t)i < full) hhq_update(st, w[i]);  // wave-uniform
                 if (tail % 32)
-                    hhq_remainder(st, trow + ((t - LAG) & 1) * TSLOT + roff - 8 * q + full * 32, tail % 32, q);
+                    hhq_remainder(st, trow + ((t - LAG) % NS) * TSLOT + roff - 8 * q + full * 32, tail % 32, q);
+            }
+            if constexpr (ZERO) {
+                if (on) dma::zero16(base);
             }
         }
         if (t + 1 < steps + LAG) lds_barrier();  // B(t+1)
