@@ -41,6 +41,7 @@ struct Tuning {
     int get_prio = 2;             // RSG_DMA_PRIO=<0..3>: wave priorities of the one-pass GET/heal
     bool decode_net = true;       // RSG_DECODE_NET=0: run-time-table GF waves for every one-pass pattern
     int net12_rd = 2;             // RSG_NET12_RD=4: RS(12,4) GET ring of 4 slots, one workgroup per CU (A/B)
+    bool hash_unal = true;        // RSG_HASH_UNAL=0: unaligned 8-byte loads for unaligned messages (A/B)
     bool get_cached = true;       // RSG_GET_CACHED=0: non-temporal output stores in the network GET/heal kernel
 };
 const Tuning& tuning();

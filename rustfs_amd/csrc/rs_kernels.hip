@@ -186,7 +186,17 @@ __global__ __launch_bounds__(256) void k_gf_apply_byte(const GfApplyParams p) {
 // per instruction) instead of 16 scattered 32-byte pieces of 8 B per lane.
 // The whole wave stays in the loop (a quad past n hashes message 0 and stores
 // nothing) because its lanes store other quads' bytes.
-template <int COPY, int DEPTH>
+//
+// UNAL (verify / digest launches with messages at odd offsets: BitrotWriter
+// records of RS(6,4) at 1 MiB blocks, 32 + 174763 bytes): each lane loads
+// the aligned 8-byte word of its packet piece and the quad rebuilds the
+// message bytes with a funnel shift across neighbouring lanes (one DPP quad
+// rotation per word and v_alignbyte_b32), instead of 8-byte loads at odd
+// addresses — which ran the all-present RS(6,4) GET at 0.53 of HBM against
+// 0.78 for aligned RS(8,4) records (profiles/r04/n/).  Lane 3's last word of a batch starts the next
+// packet: the quad loads that aligned word too (it holds a message byte, so
+// the load stays inside the caller's buffer).
+template <int COPY, int DEPTH, bool UNAL = false>
 __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
     const uint64_t j0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 2;
     const uint32_t q = threadIdx.x & 3u;
@@ -228,13 +238,45 @@ __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
     hhq_init(s, p.key, q);
     const uint64_t packets = p.len >> 5;
     uint64_t t = 0;
+    const uint32_t mis = UNAL ? (uint32_t)((uintptr_t)msg & 7u) : 0u;  // the message's byte offset in its word
+    const uint8_t* const am = msg - mis;
     // 8-byte loads at any alignment (records put data 32 B after the digest,
-    // shards of unaligned length are common)
-    auto fetch = [&](uint64_t (&w)[8], uint64_t t0) {
+    // shards of unaligned length are common); UNAL: aligned words, w[8] = the
+    // word that starts the next packet
+    auto fetch = [&](uint64_t (&w)[9], uint64_t t0) {
+        if constexpr (UNAL) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) w[i] = ld64_any(msg + (t0 + i) * 32 + 8 * q);
+            for (int i = 0; i < 8; ++i) w[i] = *(const uint64_t*)(am + (t0 + i) * 32 + 8 * q);
+            w[8] = mis ? *(const uint64_t*)(am + (t0 + 8) * 32) : 0ull;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) w[i] = ld64_any(msg + (t0 + i) * 32 + 8 * q);
+        }
     };
-    auto consume = [&](const uint64_t (&w)[8], uint64_t t0) {
+    // UNAL: lane q's message word = its aligned word >> 8 mis, filled from the
+    // next lane's (lane 3: the next packet's first word)
+    auto realign = [&](uint64_t (&w)[9]) {
+        uint64_t nx[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const u32x2 v = __builtin_bit_cast(u32x2, w[i]);
+            u32x2 r;
+            r.x = (uint32_t)__builtin_amdgcn_mov_dpp((int)v.x, 0x39, 0xF, 0xF, false);  // quad_perm [1,2,3,0]
+            r.y = (uint32_t)__builtin_amdgcn_mov_dpp((int)v.y, 0x39, 0xF, 0xF, false);
+            nx[i] = __builtin_bit_cast(uint64_t, r);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint64_t hi = q == 3 ? (i < 7 ? nx[i + 1] : w[8]) : nx[i];
+            const uint32_t l0 = (uint32_t)w[i], l1 = (uint32_t)(w[i] >> 32), h0 = (uint32_t)hi,
+                           h1 = (uint32_t)(hi >> 32);
+            const uint32_t a0 = __builtin_amdgcn_alignbyte(l1, l0, mis), a1 = __builtin_amdgcn_alignbyte(h0, l1, mis);
+            const uint32_t b1 = __builtin_amdgcn_alignbyte(h1, h0, mis);
+            w[i] = mis < 4 ? ((uint64_t)a1 << 32 | a0) : ((uint64_t)b1 << 32 | a1);
+        }
+    };
+    auto consume = [&](uint64_t (&w)[9], uint64_t t0) {
+        if constexpr (UNAL) realign(w);
 #pragma unroll
         for (int i = 0; i < 8; ++i) hhq_update(s, w[i]);
         if constexpr (COPY == 1) {
@@ -260,7 +302,7 @@ __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
         // batch x + DEPTH - 1 are issued before batch x is hashed.  Loads past
         // the last batch are clamped to it (inside the message) and unused.
         if (nb) {
-            uint64_t w[DEPTH][8];
+            uint64_t w[DEPTH][9];
 #pragma unroll
             for (int d = 0; d < DEPTH - 1; ++d) fetch(w[d], ((uint64_t)d < nb ? (uint64_t)d : nb - 1) * 8);
             uint64_t b = 0;
@@ -279,7 +321,7 @@ __global__ __launch_bounds__(256) void k_hh256_quad(const HashParams p) {
         }
     } else {
         for (; t + 8 <= packets; t += 8) {
-            uint64_t w[8];
+            uint64_t w[9];
             fetch(w, t);
             consume(w, t);
         }
@@ -1149,6 +1191,7 @@ const Tuning& tuning() {
         v.get_prio = num("RSG_DMA_PRIO", 2, 0, 3);
         v.decode_net = flag("RSG_DECODE_NET", true);
         v.net12_rd = num("RSG_NET12_RD", 2, 2, 4) == 4 ? 4 : 2;
+        v.hash_unal = flag("RSG_HASH_UNAL", true);
         v.get_cached = flag("RSG_GET_CACHED", true);
         return v;
     }();
@@ -1304,7 +1347,20 @@ hipError_t launch_hh256(const HashParams& p, hipStream_t stream) {
     const int depth = tuning().hash_depth;
     using HashKernel = void (*)(const HashParams);
     HashKernel k;
-    if (!copy) k = depth == 1 ? k_hh256_quad<0, 1> : depth == 2 ? k_hh256_quad<0, 2> : k_hh256_quad<0, 3>;
+    // messages at odd offsets (record pitch 174795 of RS(6,4) at 1 MiB
+    // blocks): aligned loads and a funnel shift, 1.005 -> 0.899 ms for the
+    // all-present GET; at even offsets (RS(10,4), RS(12,4): 2 mod 8) the
+    // hardware's unaligned loads are 4-5 % faster than the funnel
+    // (profiles/r04/o/).  Tuning::hash_unal, RSG_HASH_UNAL=0: always the loads.
+    bool even = true;
+    if (p.nbases) {
+        even = p.stripe_stride % 2 == 0;
+        for (uint32_t b = 0; b < p.nbases; ++b) even = even && (uintptr_t)p.base[b] % 2 == 0;
+    } else {
+        even = (uintptr_t)p.data % 2 == 0 && p.stripe_stride % 2 == 0 && p.shard_pitch % 2 == 0;
+    }
+    if (!copy && depth == 2 && !even && tuning().hash_unal) k = k_hh256_quad<0, 2, true>;
+    else if (!copy) k = depth == 1 ? k_hh256_quad<0, 1> : depth == 2 ? k_hh256_quad<0, 2> : k_hh256_quad<0, 3>;
     else if (direct_copy) k = depth == 1 ? k_hh256_quad<1, 1> : depth == 2 ? k_hh256_quad<1, 2> : k_hh256_quad<1, 3>;
     else k = depth == 1 ? k_hh256_quad<2, 1> : depth == 2 ? k_hh256_quad<2, 2> : k_hh256_quad<2, 3>;
     hipLaunchKernelGGL(k, dim3((uint32_t)blocks), dim3(256), 0, stream, p);
