@@ -261,8 +261,9 @@ static bool launch_net_if_listed(int heal, int k, int m, int nf, const uint8_t* 
                                                     launch_records_net12_part6, launch_records_net12_part7};
         return (k == 16 ? parts16 : parts12)[pid % RSG_NET_PARTS](pid, blocks, p, h, stream);
     }
-    if (k != 8) return false;
-    const int pid = records_net_pattern(heal, nf, (int)p.R, (int)p.n_store, coef);
+    if (k != 8 && k != 6) return false;
+    const int pid = k == 8 ? records_net_pattern(heal, nf, (int)p.R, (int)p.n_store, coef)
+                           : records_net6_pattern(heal, nf, (int)p.R, (int)p.n_store, coef);
     if (pid < 0) return false;
     GfApplyParams q = p;
     q.cached_stores = tuning().get_cached ? 1u : 0u;
@@ -272,7 +273,11 @@ static bool launch_net_if_listed(int heal, int k, int m, int nf, const uint8_t* 
                                               launch_records_net_part2, launch_records_net_part3,
                                               launch_records_net_part4, launch_records_net_part5,
                                               launch_records_net_part6, launch_records_net_part7};
-    return parts[pid % RSG_NET_PARTS](pid, blocks, q, h, stream);
+    static const Part parts6[RSG_NET_PARTS] = {launch_records_net6_part0, launch_records_net6_part1,
+                                               launch_records_net6_part2, launch_records_net6_part3,
+                                               launch_records_net6_part4, launch_records_net6_part5,
+                                               launch_records_net6_part6, launch_records_net6_part7};
+    return (k == 8 ? parts : parts6)[pid % RSG_NET_PARTS](pid, blocks, q, h, stream);
 }
 
 // The record files' layout the DMA ring can walk: LDS-DMA takes sources at

@@ -1,9 +1,12 @@
-// rs_decode_net.hip — the one-pass GET / heal kernel for RS(8,4) with its
+// rs_decode_net.hip — the one-pass GET / heal kernel for RS(8,4) and RS(6,4)
+// (the default geometry of a 10-drive set, storageclass.rs:24-31) with its
 // rows as a compile-time XOR network per erasure pattern
-// (k_decode_records_net<PID>; the networks in the generated
-// rs84_decode_nets.h, tools/gen_decode_nets.py).  Compiled RSG_NET_PARTS
-// times (Makefile), part RSG_NET_PART instantiating the patterns with
-// PID % RSG_NET_PARTS == RSG_NET_PART, so the 146 kernels build in parallel.
+// (k_decode_records_net<PID> / k_decode_records_net6<PID>; the networks in
+// the generated rs84_decode_nets.h / rs64_decode_nets.h,
+// tools/gen_decode_nets.py [--k 6]).  Compiled RSG_NET_PARTS times per
+// geometry (Makefile: RSG_NET_K = 8 or 6), part RSG_NET_PART instantiating
+// the patterns with PID % RSG_NET_PARTS == RSG_NET_PART, so the kernels
+// build in parallel.
 //
 // Same workgroup as k_decode_records_dma (rs_decode.hip): 8 stripes, NF
 // present record files DMA'd into a 3-slot LDS ring per 512-byte step,
@@ -13,7 +16,7 @@
 // coefficient, v_perm at half the XOR issue rate) become 2 network waves,
 // one per 4-stripe group (stripes 2g, 2g+1, 2g+4, 2g+5: 8 bytes of each per
 // lane, as the fused encoder's k_encode_hash_dma groups): each step the wave
-// bit-transposes the 8 survivor rows into 64 planes, runs the pattern's
+// bit-transposes the 8 (6) survivor rows into 64 (48) planes, runs the pattern's
 // network (all R rows at once: 173-244 three-input XORs), transposes the
 // rows back, stores the rebuilt rows (and heal's LDS row copies), compares
 // the surplus parity rows with the ring and copies GET's present data through.
@@ -34,10 +37,30 @@
 #ifndef RSG_NET_PART
 #error "RSG_NET_PART (0 .. RSG_NET_PARTS-1) is set by the Makefile"
 #endif
+#ifndef RSG_NET_K
+#define RSG_NET_K 8
+#endif
+
+#define RSG_NET_CAT2(a, b) a##b
+#define RSG_NET_CAT(a, b) RSG_NET_CAT2(a, b)
+#if RSG_NET_K == 8
+#define RSG_NET_TAG  // k_decode_records_net, launch_records_net_partN, records_net_pattern
+#elif RSG_NET_K == 6
+#define RSG_NET_TAG 6  // k_decode_records_net6, launch_records_net6_partN, records_net6_pattern
+#else
+#error "RSG_NET_K is 8 or 6"
+#endif
+#define RSG_NET_NAME(pre, post) RSG_NET_CAT(RSG_NET_CAT(pre, RSG_NET_TAG), post)
 
 namespace rsg {
 
+#if RSG_NET_K == 8
 #include "rs84_decode_nets.h"
+#else
+#include "rs64_decode_nets.h"
+namespace decnet = decnet6;
+#endif
+constexpr int kNetC = RSG_NET_K;  // survivors (data shards)
 
 // 8 output bytes per lane: plain (cached) stores by default — the L2 gathers
 // the walk's 512-byte rows before they reach HBM (RS(8,4), n = 4096, GET with
@@ -82,7 +105,7 @@ __device__ __forceinline__ void net_wave(const GfApplyParams& p, uint64_t n, uin
     using dma::PP;
     using L = NetShape<NF, TH>;
     constexpr decnet::Pattern pat = decnet::kPatterns[PID];
-    constexpr int C = 8, R = pat.R, NST = pat.n_store, SPW = L::SPW, HS = L::HS;
+    constexpr int C = kNetC, R = pat.R, NST = pat.n_store, SPW = L::SPW, HS = L::HS;
     static_assert(pat.nf == NF && (pat.heal ? NST : 0) == TH && R <= 4 && NST <= R, "pattern shape");
     if (p.wave_prio & kPrioGf) __builtin_amdgcn_s_setprio(2);
     const uint32_t lane = threadIdx.x & 63u;
@@ -192,7 +215,7 @@ __device__ __forceinline__ void net_wave(const GfApplyParams& p, uint64_t n, uin
 }
 
 template <int PID, int NF, int TH>
-__global__ __launch_bounds__((64 * NetShape<NF, TH>::WAVES)) void k_decode_records_net(const GfApplyParams p,
+__global__ __launch_bounds__((64 * NetShape<NF, TH>::WAVES)) void RSG_NET_NAME(k_decode_records_net, )(const GfApplyParams p,
                                                                                        const HashParams h) {
     using L = NetShape<NF, TH>;
     __shared__ __attribute__((aligned(16))) uint8_t ring[dma::D * L::DSLOT];
@@ -217,7 +240,7 @@ template <int PID>
 static void launch_net(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
     constexpr decnet::Pattern pat = decnet::kPatterns[PID];
     constexpr int NF = pat.nf, TH = pat.heal ? pat.n_store : 0;
-    hipLaunchKernelGGL((k_decode_records_net<PID, NF, TH>), dim3((uint32_t)blocks), dim3(64 * NetShape<NF, TH>::WAVES),
+    hipLaunchKernelGGL((RSG_NET_NAME(k_decode_records_net, )<PID, NF, TH>), dim3((uint32_t)blocks), dim3(64 * NetShape<NF, TH>::WAVES),
                        0, stream, p, h);
 }
 
@@ -234,28 +257,26 @@ constexpr std::array<NetLaunch, sizeof...(I)> net_table(std::index_sequence<I...
 
 static const std::array<NetLaunch, decnet::kCount> kNetPart = net_table(std::make_index_sequence<decnet::kCount>{});
 
-#define RSG_NET_CAT2(a, b) a##b
-#define RSG_NET_CAT(a, b) RSG_NET_CAT2(a, b)
-
 // This part's launcher: false if pattern `pid` is instantiated elsewhere.
-bool RSG_NET_CAT(launch_records_net_part, RSG_NET_PART)(int pid, uint64_t blocks, const GfApplyParams& p,
-                                                        const HashParams& h, hipStream_t stream) {
+bool RSG_NET_NAME(launch_records_net, RSG_NET_CAT(_part, RSG_NET_PART))(int pid, uint64_t blocks,
+                                                                        const GfApplyParams& p, const HashParams& h,
+                                                                        hipStream_t stream) {
     if (pid < 0 || pid >= decnet::kCount || !kNetPart[pid]) return false;
     kNetPart[pid](blocks, p, h, stream);
     return true;
 }
 
 #if RSG_NET_PART == 0
-// The pattern whose coefficient rows equal the launch's (R x 8, row-major),
+// The pattern whose coefficient rows equal the launch's (R x K, row-major),
 // or -1: matched byte for byte, so a network is only ever run on exactly the
 // matrix it was generated for.
-int records_net_pattern(int heal, int nf, int R, int n_store, const uint8_t* coef) {
+int RSG_NET_NAME(records_net, _pattern)(int heal, int nf, int R, int n_store, const uint8_t* coef) {
     for (int i = 0; i < decnet::kCount; ++i) {
         const decnet::Pattern& pt = decnet::kPatterns[i];
         if (pt.heal != heal || pt.nf != nf || pt.R != R || pt.n_store != n_store) continue;
         bool eq = true;
         for (int r = 0; r < R && eq; ++r)
-            for (int c = 0; c < 8 && eq; ++c) eq = pt.coef[r][c] == coef[r * 8 + c];
+            for (int c = 0; c < kNetC && eq; ++c) eq = pt.coef[r][c] == coef[r * kNetC + c];
         if (eq) return i;
     }
     return -1;

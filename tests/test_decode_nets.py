@@ -216,3 +216,46 @@ def test_rs12_decode_nets_rebuild_true_shards(oracle):
             acc = [a ^ b for a, b in zip(acc, part)]
         got = _bytes(acc, p["R"])
         assert np.array_equal(got, st[want_idx]), p["pid"]
+
+
+# ---------------------------------------------------------------- RS(6,4)
+HEADER6 = os.path.join(ROOT, "rustfs_amd", "csrc", "rs64_decode_nets.h")
+
+
+def test_rs6_decode_nets_rebuild_true_shards(oracle):
+    """RS(6,4), the default geometry of a 10-drive set (rs64_decode_nets.h,
+    k_decode_records_net6: rs_decode_net.hip over 6 survivors): every 1- and
+    2-shard loss (GET: a data shard lost; heal: every loss), one network per
+    pattern giving the true shards, its rows the oracle's decode matrix rows."""
+    k, t = 6, 10
+    src = open(HEADER6).read()
+    pats = []
+    for m in re.finditer(r"\{0x([0-9a-f]+), (\d), (\d+), (\d), (\d), \{(.*?)\}\},  // (\d+)", src):
+        rows = [[int(x) for x in r.split(",")] for r in re.findall(r"\{([0-9, ]+)\}", m.group(6))]
+        pats.append(dict(absent=int(m.group(1), 16), heal=int(m.group(2)), nf=int(m.group(3)), R=int(m.group(4)),
+                         nst=int(m.group(5)), coef=rows, pid=int(m.group(7))))
+    assert len(pats) == int(re.search(r"kCount = (\d+)", src).group(1))
+    assert sum(1 for p in pats if p["heal"]) == 10 + 45
+    assert sum(1 for p in pats if not p["heal"]) == 6 + 15 + 6 * 4
+    rng = np.random.default_rng(64)
+    gm = oracle.matrix(k, 4)
+    for p in pats:
+        lost = [i for i in range(t) if p["absent"] >> i & 1]
+        files = [i for i in range(t) if i not in lost]
+        store = lost if p["heal"] else [i for i in lost if i < k]
+        want_idx = store + files[k:]
+        assert p["R"] == len(want_idx) and p["nst"] == len(store) and p["nf"] == len(files)
+        inv = oracle.invert(gm[files[:k]])
+        for r, idx in enumerate(want_idx):
+            row = []
+            for c in range(k):
+                a = 0
+                for i in range(k):
+                    a ^= oracle.gf_mul(int(gm[idx][i]), int(inv[i][c]))
+                row.append(a)
+            assert row == p["coef"][r], (p["pid"], r)
+        st = np.zeros((t, 32), dtype=np.uint8)
+        st[:k] = rng.integers(0, 256, (k, 32), dtype=np.uint8)
+        oracle.encode(k, 4, st)
+        got = _bytes(_run(_program(src, p["pid"]), _planes(st[files[:k]])), p["R"])
+        assert np.array_equal(got, st[want_idx]), p["pid"]

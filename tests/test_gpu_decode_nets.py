@@ -300,6 +300,91 @@ def test_rs12_every_listed_pattern(gpu, oracle, records12, one_pass, heal, lost)
             assert np.array_equal(tgt2[i].cpu().numpy().reshape(N12, REC12)[keep], recs[i][keep]), f"shard {i}"
 
 
+# ---------------------------------------------------------------- RS(6,4)
+# the default geometry of a 10-drive set (storageclass.rs:24-31); S6 = 1001:
+# a ragged walk (one whole step and 489 bytes) with records at odd offsets
+K6, T6, N6, S6 = 6, 10, 11, 1001
+REC6 = 32 + S6
+LISTED6 = _listed("rs64_decode_nets.h", T6)
+
+
+@pytest.fixture(scope="module")
+def records6(gpu, oracle):
+    import torch
+    rng = np.random.default_rng(64)
+    shards = np.zeros((N6, T6, S6), dtype=np.uint8)
+    recs = np.zeros((T6, N6, REC6), dtype=np.uint8)
+    for s in range(N6):
+        shards[s, :K6] = rng.integers(0, 256, (K6, S6), dtype=np.uint8)
+        oracle.encode(K6, 4, shards[s])
+        for i in range(T6):
+            recs[i, s, :32] = np.frombuffer(oracle.hh256s(shards[s, i].tobytes()), dtype=np.uint8)
+            recs[i, s, 32:] = shards[s, i]
+    files = [torch.from_numpy(recs[i].reshape(-1).copy()).cuda() for i in range(T6)]
+    return shards, recs, files
+
+
+def test_rs6_table_lists_every_pattern():
+    """Every one- and two-shard loss of RS(6,4): 6 + 39 GET patterns (a data
+    shard among the lost) and 10 + 45 heal patterns."""
+    assert len([x for x in LISTED6 if not x[0]]) == 6 + 39
+    assert len([x for x in LISTED6 if x[0]]) == 10 + 45
+
+
+@pytest.mark.parametrize("heal,lost", LISTED6, ids=lambda x: str(x))
+def test_rs6_every_listed_pattern(gpu, oracle, records6, one_pass, heal, lost):
+    """k_decode_records_net6 (rs_decode_net.hip over 6 survivors) on a ragged
+    walk of records at odd offsets: GET in both forms and heal, bit-exact
+    against the oracle, with an altered surplus parity reported for its
+    stripe alone."""
+    import torch
+    from rustfs_amd import Erasure, _lib
+    shards, recs, files = records6
+    e = Erasure(K6, 4, K6 * S6)
+    present = [i for i in range(T6) if i not in lost]
+    sur = present[K6:]
+
+    def rehashed(f, stripe, pos):
+        bad = f.clone()
+        body = bad[stripe * REC6 + 32:(stripe + 1) * REC6].cpu().numpy().copy()
+        body[pos] ^= 0x40
+        bad[stripe * REC6 + 32:(stripe + 1) * REC6] = torch.from_numpy(body).cuda()
+        bad[stripe * REC6:stripe * REC6 + 32] = torch.from_numpy(
+            np.frombuffer(oracle.hh256s(body.tobytes()), dtype=np.uint8).copy()).cuda()
+        return bad
+
+    if not heal:
+        want = torch.from_numpy(shards[:, :K6].reshape(N6, K6 * S6).copy()).cuda()
+        f = [None if i in lost else files[i] for i in range(T6)]
+        for form in FORMS:
+            out, status = decode_get(e, f, S6, N6, form)
+            assert status == [0] * N6 and torch.equal(out, want), form
+        if sur:
+            stripe = sum(lost) % N6
+            bad = sur[sum(lost) % len(sur)]
+            f2 = list(f)
+            f2[bad] = rehashed(files[bad], stripe, 700 + sum(lost))
+            for form in FORMS:
+                out, status = decode_get(e, f2, S6, N6, form)
+                assert [i for i, x in enumerate(status) if x] == [stripe], form
+                assert status[stripe] == _lib.RSG_ERR_INCONSISTENT_SOURCES
+        return
+    src = [None if i in lost else files[i] for i in range(T6)]
+    tgt = [torch.zeros(N6 * REC6, dtype=torch.uint8, device="cuda") if i in lost else None for i in range(T6)]
+    assert e.heal_records_batch(src, tgt, S6, N6) == [0] * N6
+    for i in lost:
+        assert np.array_equal(tgt[i].cpu().numpy().reshape(N6, REC6), recs[i]), f"shard {i}"
+    if sur:
+        stripe = (3 * sum(lost) + 2) % N6
+        bad = sur[(sum(lost) + 1) % len(sur)]
+        src2 = list(src)
+        src2[bad] = rehashed(files[bad], stripe, 5 * sum(lost) % S6)
+        tgt2 = [torch.zeros(N6 * REC6, dtype=torch.uint8, device="cuda") if i in lost else None for i in range(T6)]
+        status = e.heal_records_batch(src2, tgt2, S6, N6)
+        assert [i for i, x in enumerate(status) if x] == [stripe]
+        assert status[stripe] == _lib.RSG_ERR_INCONSISTENT_SOURCES
+
+
 def test_rs16_heal_unlisted_pattern_falls_back(gpu, oracle, records16, one_pass):
     """A heal the network table does not list (three lost shards) takes the
     two-pass path even with the one-pass engine forced: still bit-exact."""

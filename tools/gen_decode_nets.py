@@ -23,6 +23,10 @@ rows) and one `net<PID>` specialisation per pattern.  The launcher matches a
 launch's coefficient rows against the table byte for byte, so a pattern not
 listed (or any disagreement) keeps the run-time-table kernel.
 
+RS(6,4) (`--k 6`, the default geometry of a 10-drive set) is generated like
+RS(8,4), one network over its 6 survivors (rs64_decode_nets.h, run by
+rs_decode_net.hip built with RSG_NET_K=6).
+
 RS(16,4) (`--k 16`) and RS(12,4) (`--k 12`, the default geometry of a
 16-drive set, storageclass.rs:24-31): the survivors' 128 / 96 planes do not
 fit one wave's registers beside the rows, so each pattern gets one network
@@ -221,7 +225,7 @@ def main():
     # RS(12,4): quarters 0-2 / 3-5 / 6-8 / 9-11 (four network waves, one per
     # SIMD, rs_decode_net12.hip)
     ka = 8
-    halves = {8: [(0, 8)], 16: [(0, 8), (8, 8)], 12: [(0, 3), (3, 3), (6, 3), (9, 3)]}[K]
+    halves = {6: [(0, 6)], 8: [(0, 8)], 16: [(0, 8), (8, 8)], 12: [(0, 3), (3, 3), (6, 3), (9, 3)]}[K]
     if quarters:
         halves = [(c0, K // 4) for c0 in range(0, K, K // 4)]
     tasks = [(p[5], seeds, c0, cn) for c0, cn in halves for p in pats]
@@ -231,14 +235,15 @@ def main():
     ops = [sum(n[i][0] for n in nets) for i in range(len(pats))]
     name = ("rs84q_decode_nets.h" if quarters else "rs84_decode_nets.h") if K == 8 else f"rs{K}{M}_decode_nets.h"
     space = f"decnet{'' if K == 8 and not quarters else K}{'q' if quarters else ''}"
+    single = K <= 8 and not quarters  # one network over all survivors (rs_decode_net.hip)
     hdr = [
         f"// {name} — GENERATED by tools/gen_decode_nets.py (do not edit).",
         f"// RS({K},{M}) one-pass GET / heal rows as compile-time three-input XOR networks,",
         f"// one per erasure pattern of one or two lost shards: {len(pats)} patterns,",
         f"// {min(ops)}-{max(ops)} ops each (mean {sum(ops) / len(ops):.0f}).  P[c*8+j] = bit plane j of",
-        f"// survivor c (the first {K} present shards{'' if K == 8 else ', in parts ' + ', '.join(f'{c0}-{c0 + cn - 1}' for c0, cn in halves)}), O[r*8+i] = bit plane i of row r",
+        f"// survivor c (the first {K} present shards{'' if single else ', in parts ' + ', '.join(f'{c0}-{c0 + cn - 1}' for c0, cn in halves)}), O[r*8+i] = bit plane i of row r",
         "// (rows [0, n_store) stored, the rest compared with the present",
-        f"// non-survivor parity in ascending order).  Included by {'rs_decode_net.hip' if K == 8 and not quarters else 'rs_decode_net16.hip' if K == 16 else 'rs_decode_netq.hip'}",
+        f"// non-survivor parity in ascending order).  Included by {'rs_decode_net.hip' if single else 'rs_decode_net16.hip' if K == 16 else 'rs_decode_netq.hip'}",
         "// inside namespace rsg, after x3().",
         "#pragma once",
         "",
@@ -261,7 +266,7 @@ def main():
         cs = ", ".join("{" + ", ".join(str(x) for x in r) + "}" for r in rr)
         hdr.append(f"    {{0x{mask:03x}, {heal}, {nf}, {R}, {nst}, {{{cs}}}}},  // {pid}")
     hdr += ["};", ""]
-    if K == 8 and not quarters:
+    if single:
         hdr += ["template <int PID>", "__device__ void net(const uint32_t (&P)[64], uint32_t (&O)[32]);", ""]
         for pid, pat in enumerate(pats):
             hdr += emit_net(pid, pat, nets[0][pid])
