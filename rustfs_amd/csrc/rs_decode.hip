@@ -245,9 +245,10 @@ static bool launch_net_if_listed(int heal, int k, int m, int nf, const uint8_t* 
                                  const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
     if (m != 4 || !coef || !tuning().decode_net || p.C != (uint32_t)k) return false;
     using Part = bool (*)(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
-    if (k == 16 || k == 12) {
-        const int pid = k == 16 ? records_net16_pattern(heal, nf, (int)p.R, (int)p.n_store, coef)
-                                : records_net12_pattern(heal, nf, (int)p.R, (int)p.n_store, coef);
+    if (k == 16 || k == 12 || k == 10) {
+        const int pid = k == 16   ? records_net16_pattern(heal, nf, (int)p.R, (int)p.n_store, coef)
+                        : k == 12 ? records_net12_pattern(heal, nf, (int)p.R, (int)p.n_store, coef)
+                                  : records_net10_pattern(heal, nf, (int)p.R, (int)p.n_store, coef);
         if (pid < 0) return false;
         const uint64_t blocks = (n_stripes + 3) / 4;
         if (blocks > 0x7fffffffull) return false;
@@ -259,7 +260,11 @@ static bool launch_net_if_listed(int heal, int k, int m, int nf, const uint8_t* 
                                                     launch_records_net12_part2, launch_records_net12_part3,
                                                     launch_records_net12_part4, launch_records_net12_part5,
                                                     launch_records_net12_part6, launch_records_net12_part7};
-        return (k == 16 ? parts16 : parts12)[pid % RSG_NET_PARTS](pid, blocks, p, h, stream);
+        static const Part parts10[RSG_NET_PARTS] = {launch_records_net10_part0, launch_records_net10_part1,
+                                                    launch_records_net10_part2, launch_records_net10_part3,
+                                                    launch_records_net10_part4, launch_records_net10_part5,
+                                                    launch_records_net10_part6, launch_records_net10_part7};
+        return (k == 16 ? parts16 : k == 12 ? parts12 : parts10)[pid % RSG_NET_PARTS](pid, blocks, p, h, stream);
     }
     if (k != 8 && k != 6) return false;
     const int pid = k == 8 ? records_net_pattern(heal, nf, (int)p.R, (int)p.n_store, coef)
@@ -287,7 +292,7 @@ static bool dma_records_walkable(const HashParams& h) { return 5 * h.stripe_stri
 
 bool heal_one_pass_shape(int k, int m, int nf, int targets, uint64_t shard_len) {
     return heal_dma_supported(k, m, nf, targets, shard_len) ||
-           ((k == 16 || k == 12) && m == 4 && tuning().decode_net && one_pass_geometry(k, m, shard_len) &&
+           ((k == 16 || k == 12 || k == 10) && m == 4 && tuning().decode_net && one_pass_geometry(k, m, shard_len) &&
             nf >= k && targets >= 1 && nf + targets <= k + m);
 }
 

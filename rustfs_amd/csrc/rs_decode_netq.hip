@@ -3,7 +3,10 @@
 // network waves (k_decode_records_net12<PID>): its rows as compile-time XOR
 // networks per erasure pattern in four parts of the survivors (generated
 // rs124_decode_nets.h, tools/gen_decode_nets.py --k 12).  Compiled
-// RSG_NET_PARTS times (Makefile, RSG_NETQ_K=12) like rs_decode_net.hip.
+// RSG_NET_PARTS times (Makefile, RSG_NETQ_K=12) like rs_decode_net.hip; and
+// again for RS(10,4), the 14-drive default (RSG_NETQ_K=10,
+// k_decode_records_net10, rs104_decode_nets.h: parts of 3, 3, 2, 2
+// survivors).
 //
 // At 1 MiB blocks RS(12,4)'s shards are 87382 bytes, so its record walks are
 // ragged (170 whole 512-byte steps and 342 bytes, rs_records.h walk_tail) and
@@ -49,27 +52,38 @@
 #error "RSG_NET_PART (0 .. RSG_NET_PARTS-1) is set by the Makefile"
 #endif
 #ifndef RSG_NETQ_K
-#error "RSG_NETQ_K (12 or 8) is set by the Makefile"
+#error "RSG_NETQ_K (12 or 10) is set by the Makefile"
 #endif
 
 #define RSG_NETQ_CAT2(a, b) a##b
 #define RSG_NETQ_CAT(a, b) RSG_NETQ_CAT2(a, b)
 #if RSG_NETQ_K == 12
 #define RSG_NETQ_TAG net12
+#elif RSG_NETQ_K == 10
+#define RSG_NETQ_TAG net10
 #else
-#error "RSG_NETQ_K is 12 (RS(8,4) in this form measured slower: see the header)"
+#error "RSG_NETQ_K is 12 or 10 (RS(8,4) in this form measured slower: see the header)"
 #endif
 // k_decode_records_net12, launch_records_net12_partN, records_net12_pattern
 #define RSG_NETQ_NAME(pre, post) RSG_NETQ_CAT(RSG_NETQ_CAT(pre, RSG_NETQ_TAG), post)
 
 namespace rsg {
 
+#if RSG_NETQ_K == 12
 #include "rs124_decode_nets.h"
 namespace decq = decnet12;
+#else
+#include "rs104_decode_nets.h"
+namespace decq = decnet10;
+#endif
 
 namespace {
 
-constexpr int kKQ = RSG_NETQ_K, kNQ = 4, kQC = kKQ / 4;  // data shards, network waves, survivors per wave
+constexpr int kKQ = RSG_NETQ_K, kNQ = 4;  // data shards, network waves
+// network wave q's survivors [kPartC0[q], kPartC0[q] + kPartN[q]): RS(12,4)
+// 3 + 3 + 3 + 3, RS(10,4) 3 + 3 + 2 + 2 (the generator's parts)
+constexpr int kPartC0[4] = {0, 3, 6, kKQ == 12 ? 9 : 8};
+constexpr int kPartN[4] = {3, 3, kKQ == 12 ? 3 : 2, kKQ == 12 ? 3 : 2};
 
 // ENC (the fused encode): the accumulators are also the target-row area —
 // a row's finisher writes its bytes over the accumulator it has just read and
@@ -111,7 +125,7 @@ __device__ __forceinline__ void netq_wave(const GfApplyParams& p, uint64_t n, ui
     constexpr decq::Pattern pat = decq::kPatterns[PID];
     constexpr int R = pat.R, NST = pat.n_store, NCMP = R - NST, SPW = L::SPW, HS = L::HS;
     static_assert(pat.nf == NF && (pat.heal ? NST : 0) == TH && R <= kNQ && NST <= R && HS == 2, "pattern shape");
-    constexpr int C0 = kQC * Q;             // this wave's survivors [C0, C0 + kQC)
+    constexpr int C0 = kPartC0[Q], NC = kPartN[Q];  // this wave's survivors [C0, C0 + NC)
     constexpr bool FIN = Q < R;             // it finishes row Q
     constexpr bool CMP = FIN && Q >= NST;   // ... a compared one (keeps surplus row Q - NST from the ring)
     if (p.wave_prio & kPrioGf) __builtin_amdgcn_s_setprio(2);
@@ -144,9 +158,9 @@ __device__ __forceinline__ void netq_wave(const GfApplyParams& p, uint64_t n, ui
     // the other rows' parts out to LDS; copy-through of its data survivors (GET)
     auto part = [&](uint32_t t) {
         const uint8_t* slot = ring + (t % D) * L::DSLOT + lane * 8u;
-        uint32_t P[64];  // planes [0, 24) only
+        uint32_t P[64];  // planes [0, 8 NC) only
 #pragma unroll
-        for (int c = 0; c < kQC; ++c) {
+        for (int c = 0; c < NC; ++c) {
             uint2 a[4];
             row4(slot + (C0 + c) * HS * IP, a);
             uint32_t w[8] = {a[0].x, a[0].y, a[1].x, a[1].y, a[2].x, a[2].y, a[3].x, a[3].y};
@@ -172,7 +186,7 @@ __device__ __forceinline__ void netq_wave(const GfApplyParams& p, uint64_t n, ui
         if (!TH && cmask) {  // GET: this wave's present data survivors copied through
             const bool ragged = t + 1 == steps && tail != CH;  // wave-uniform
 #pragma unroll
-            for (int c = 0; c < kQC; ++c) {
+            for (int c = 0; c < NC; ++c) {
                 if (!((cmask >> (C0 + c)) & 1u)) continue;  // wave-uniform
                 uint2 x[4];
                 row4(slot + (C0 + c) * HS * IP, x);
@@ -309,6 +323,9 @@ __global__ __launch_bounds__((64 * NetQShape<NF, TH>::WAVES)) void RSG_NETQ_NAME
     records_hash_wave<NF, 4, L::XB, L::RD, ENC>(h, p.wave_prio, ring, wave, steps, s0);
 }
 
+static_assert(NetQShape<13, 0, 2>::LDS <= 80 * 1024 && NetQShape<12, 2>::LDS <= 160 * 1024 &&
+                  NetQShape<13, 1>::LDS <= 160 * 1024,
+              "RS(10,4) GET (two workgroups per CU) and heal workgroups fit the LDS");
 #if RSG_NETQ_K == 12
 static_assert(NetQShape<15, 0>::LDS <= 160 * 1024 && NetQShape<14, 0>::LDS <= 160 * 1024 &&
                   NetQShape<15, 1>::LDS <= 160 * 1024 && NetQShape<14, 2>::LDS <= 160 * 1024,

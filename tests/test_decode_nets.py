@@ -218,6 +218,54 @@ def test_rs12_decode_nets_rebuild_true_shards(oracle):
         assert np.array_equal(got, st[want_idx]), p["pid"]
 
 
+# ---------------------------------------------------------------- RS(10,4)
+HEADER10 = os.path.join(ROOT, "rustfs_amd", "csrc", "rs104_decode_nets.h")
+
+
+def test_rs10_decode_nets_rebuild_true_shards(oracle):
+    """RS(10,4), the default geometry of a 14-drive set (rs104_decode_nets.h,
+    k_decode_records_net10: rs_decode_netq.hip's four network waves over
+    survivors 0-2, 3-5, 6-7, 8-9): per pattern the four part networks,
+    XOR-combined, give the true shards; every 1- and 2-shard loss is listed
+    and its rows are the oracle's decode matrix rows."""
+    k, t = 10, 14
+    parts = [(0, 3), (3, 3), (6, 2), (8, 2)]
+    src = open(HEADER10).read()
+    pats = []
+    for m in re.finditer(r"\{0x([0-9a-f]+), (\d), (\d+), (\d), (\d), \{(.*?)\}\},  // (\d+)", src):
+        rows = [[int(x) for x in r.split(",")] for r in re.findall(r"\{([0-9, ]+)\}", m.group(6))]
+        pats.append(dict(absent=int(m.group(1), 16), heal=int(m.group(2)), nf=int(m.group(3)), R=int(m.group(4)),
+                         nst=int(m.group(5)), coef=rows, pid=int(m.group(7))))
+    assert len(pats) == int(re.search(r"kCount = (\d+)", src).group(1))
+    assert sum(1 for p in pats if p["heal"]) == 14 + 91
+    assert sum(1 for p in pats if not p["heal"]) == 10 + 45 + 10 * 4
+    rng = np.random.default_rng(104)
+    gm = oracle.matrix(k, 4)
+    for p in pats:
+        lost = [i for i in range(t) if p["absent"] >> i & 1]
+        files = [i for i in range(t) if i not in lost]
+        store = lost if p["heal"] else [i for i in lost if i < k]
+        want_idx = store + files[k:]
+        assert p["R"] == len(want_idx) and p["nst"] == len(store) and p["nf"] == len(files)
+        inv = oracle.invert(gm[files[:k]])
+        for r, idx in enumerate(want_idx):
+            row = []
+            for c in range(k):
+                a = 0
+                for i in range(k):
+                    a ^= oracle.gf_mul(int(gm[idx][i]), int(inv[i][c]))
+                row.append(a)
+            assert row == p["coef"][r], (p["pid"], r)
+        st = np.zeros((t, 32), dtype=np.uint8)
+        st[:k] = rng.integers(0, 256, (k, 32), dtype=np.uint8)
+        oracle.encode(k, 4, st)
+        acc = [0] * 32
+        for q, (c0, cn) in enumerate(parts):
+            part = _run(_program(src, f"{p['pid']}, {q}", "net_q"), _planes(st[files[c0:c0 + cn]]))
+            acc = [a ^ b for a, b in zip(acc, part)]
+        assert np.array_equal(_bytes(acc, p["R"]), st[want_idx]), p["pid"]
+
+
 # ---------------------------------------------------------------- RS(6,4)
 HEADER6 = os.path.join(ROOT, "rustfs_amd", "csrc", "rs64_decode_nets.h")
 

@@ -300,89 +300,114 @@ def test_rs12_every_listed_pattern(gpu, oracle, records12, one_pass, heal, lost)
             assert np.array_equal(tgt2[i].cpu().numpy().reshape(N12, REC12)[keep], recs[i][keep]), f"shard {i}"
 
 
-# ---------------------------------------------------------------- RS(6,4)
-# the default geometry of a 10-drive set (storageclass.rs:24-31); S6 = 1001:
-# a ragged walk (one whole step and 489 bytes) with records at odd offsets
-K6, T6, N6, S6 = 6, 10, 11, 1001
-REC6 = 32 + S6
-LISTED6 = _listed("rs64_decode_nets.h", T6)
+# ------------------------------------------------------- RS(6,4), RS(10,4)
+# the default geometries of 10- and 14-drive sets (storageclass.rs:24-31) on
+# ragged walks: RS(6,4) with S = 1001 (records at odd offsets), RS(10,4) with
+# S = 1002 (records 2 mod 8, as at 1 MiB blocks)
+GEOS = {6: (11, 1001), 10: (9, 1002)}
+LISTED6 = _listed("rs64_decode_nets.h", 10)
+LISTED10 = _listed("rs104_decode_nets.h", 14)
+
+
+def _geo_records(oracle, k):
+    import torch
+    n, S = GEOS[k]
+    t, rec = k + 4, 32 + S
+    rng = np.random.default_rng(k * 7)
+    shards = np.zeros((n, t, S), dtype=np.uint8)
+    recs = np.zeros((t, n, rec), dtype=np.uint8)
+    for s in range(n):
+        shards[s, :k] = rng.integers(0, 256, (k, S), dtype=np.uint8)
+        oracle.encode(k, 4, shards[s])
+        for i in range(t):
+            recs[i, s, :32] = np.frombuffer(oracle.hh256s(shards[s, i].tobytes()), dtype=np.uint8)
+            recs[i, s, 32:] = shards[s, i]
+    return shards, recs, [torch.from_numpy(recs[i].reshape(-1).copy()).cuda() for i in range(t)]
 
 
 @pytest.fixture(scope="module")
 def records6(gpu, oracle):
-    import torch
-    rng = np.random.default_rng(64)
-    shards = np.zeros((N6, T6, S6), dtype=np.uint8)
-    recs = np.zeros((T6, N6, REC6), dtype=np.uint8)
-    for s in range(N6):
-        shards[s, :K6] = rng.integers(0, 256, (K6, S6), dtype=np.uint8)
-        oracle.encode(K6, 4, shards[s])
-        for i in range(T6):
-            recs[i, s, :32] = np.frombuffer(oracle.hh256s(shards[s, i].tobytes()), dtype=np.uint8)
-            recs[i, s, 32:] = shards[s, i]
-    files = [torch.from_numpy(recs[i].reshape(-1).copy()).cuda() for i in range(T6)]
-    return shards, recs, files
+    return _geo_records(oracle, 6)
 
 
-def test_rs6_table_lists_every_pattern():
-    """Every one- and two-shard loss of RS(6,4): 6 + 39 GET patterns (a data
-    shard among the lost) and 10 + 45 heal patterns."""
-    assert len([x for x in LISTED6 if not x[0]]) == 6 + 39
-    assert len([x for x in LISTED6 if x[0]]) == 10 + 45
+@pytest.fixture(scope="module")
+def records10(gpu, oracle):
+    return _geo_records(oracle, 10)
 
 
-@pytest.mark.parametrize("heal,lost", LISTED6, ids=lambda x: str(x))
-def test_rs6_every_listed_pattern(gpu, oracle, records6, one_pass, heal, lost):
-    """k_decode_records_net6 (rs_decode_net.hip over 6 survivors) on a ragged
-    walk of records at odd offsets: GET in both forms and heal, bit-exact
-    against the oracle, with an altered surplus parity reported for its
-    stripe alone."""
+def test_rs6_rs10_tables_list_every_pattern():
+    """Every one- and two-shard loss: RS(6,4) 6 + 39 GET patterns (a data
+    shard among the lost) and 10 + 45 heal patterns; RS(10,4) 10 + 85 and
+    14 + 91."""
+    assert len([x for x in LISTED6 if not x[0]]) == 6 + 39 and len([x for x in LISTED6 if x[0]]) == 10 + 45
+    assert len([x for x in LISTED10 if not x[0]]) == 10 + 85 and len([x for x in LISTED10 if x[0]]) == 14 + 91
+
+
+def _geo_case(oracle, k, data, heal, lost):
+    """GET in both forms and heal of one pattern, bit-exact against the
+    oracle, with an altered surplus parity reported for its stripe alone."""
     import torch
     from rustfs_amd import Erasure, _lib
-    shards, recs, files = records6
-    e = Erasure(K6, 4, K6 * S6)
-    present = [i for i in range(T6) if i not in lost]
-    sur = present[K6:]
+    n, S = GEOS[k]
+    t, rec = k + 4, 32 + S
+    shards, recs, files = data
+    e = Erasure(k, 4, k * S)
+    present = [i for i in range(t) if i not in lost]
+    sur = present[k:]
 
     def rehashed(f, stripe, pos):
         bad = f.clone()
-        body = bad[stripe * REC6 + 32:(stripe + 1) * REC6].cpu().numpy().copy()
+        body = bad[stripe * rec + 32:(stripe + 1) * rec].cpu().numpy().copy()
         body[pos] ^= 0x40
-        bad[stripe * REC6 + 32:(stripe + 1) * REC6] = torch.from_numpy(body).cuda()
-        bad[stripe * REC6:stripe * REC6 + 32] = torch.from_numpy(
+        bad[stripe * rec + 32:(stripe + 1) * rec] = torch.from_numpy(body).cuda()
+        bad[stripe * rec:stripe * rec + 32] = torch.from_numpy(
             np.frombuffer(oracle.hh256s(body.tobytes()), dtype=np.uint8).copy()).cuda()
         return bad
 
     if not heal:
-        want = torch.from_numpy(shards[:, :K6].reshape(N6, K6 * S6).copy()).cuda()
-        f = [None if i in lost else files[i] for i in range(T6)]
+        want = torch.from_numpy(shards[:, :k].reshape(n, k * S).copy()).cuda()
+        f = [None if i in lost else files[i] for i in range(t)]
         for form in FORMS:
-            out, status = decode_get(e, f, S6, N6, form)
-            assert status == [0] * N6 and torch.equal(out, want), form
+            out, status = decode_get(e, f, S, n, form)
+            assert status == [0] * n and torch.equal(out, want), form
         if sur:
-            stripe = sum(lost) % N6
+            stripe = sum(lost) % n
             bad = sur[sum(lost) % len(sur)]
             f2 = list(f)
             f2[bad] = rehashed(files[bad], stripe, 700 + sum(lost))
             for form in FORMS:
-                out, status = decode_get(e, f2, S6, N6, form)
+                out, status = decode_get(e, f2, S, n, form)
                 assert [i for i, x in enumerate(status) if x] == [stripe], form
                 assert status[stripe] == _lib.RSG_ERR_INCONSISTENT_SOURCES
         return
-    src = [None if i in lost else files[i] for i in range(T6)]
-    tgt = [torch.zeros(N6 * REC6, dtype=torch.uint8, device="cuda") if i in lost else None for i in range(T6)]
-    assert e.heal_records_batch(src, tgt, S6, N6) == [0] * N6
+    src = [None if i in lost else files[i] for i in range(t)]
+    tgt = [torch.zeros(n * rec, dtype=torch.uint8, device="cuda") if i in lost else None for i in range(t)]
+    assert e.heal_records_batch(src, tgt, S, n) == [0] * n
     for i in lost:
-        assert np.array_equal(tgt[i].cpu().numpy().reshape(N6, REC6), recs[i]), f"shard {i}"
+        assert np.array_equal(tgt[i].cpu().numpy().reshape(n, rec), recs[i]), f"shard {i}"
     if sur:
-        stripe = (3 * sum(lost) + 2) % N6
+        stripe = (3 * sum(lost) + 2) % n
         bad = sur[(sum(lost) + 1) % len(sur)]
         src2 = list(src)
-        src2[bad] = rehashed(files[bad], stripe, 5 * sum(lost) % S6)
-        tgt2 = [torch.zeros(N6 * REC6, dtype=torch.uint8, device="cuda") if i in lost else None for i in range(T6)]
-        status = e.heal_records_batch(src2, tgt2, S6, N6)
+        src2[bad] = rehashed(files[bad], stripe, 5 * sum(lost) % S)
+        tgt2 = [torch.zeros(n * rec, dtype=torch.uint8, device="cuda") if i in lost else None for i in range(t)]
+        status = e.heal_records_batch(src2, tgt2, S, n)
         assert [i for i, x in enumerate(status) if x] == [stripe]
         assert status[stripe] == _lib.RSG_ERR_INCONSISTENT_SOURCES
+
+
+@pytest.mark.parametrize("heal,lost", LISTED6, ids=lambda x: str(x))
+def test_rs6_every_listed_pattern(gpu, oracle, records6, one_pass, heal, lost):
+    """k_decode_records_net6 (rs_decode_net.hip over 6 survivors)."""
+    _geo_case(oracle, 6, records6, heal, lost)
+
+
+@pytest.mark.parametrize("heal,lost", LISTED10, ids=lambda x: str(x))
+def test_rs10_every_listed_pattern(gpu, oracle, records10, one_pass, heal, lost):
+    """k_decode_records_net10 (rs_decode_netq.hip, parts of 3, 3, 2, 2
+    survivors; GET on a 2-slot ring with two workgroups per CU, heal one
+    workgroup on a 4-slot ring)."""
+    _geo_case(oracle, 10, records10, heal, lost)
 
 
 def test_rs16_heal_unlisted_pattern_falls_back(gpu, oracle, records16, one_pass):
@@ -477,10 +502,13 @@ LONG = [(8, 19, 0, (0,)), (8, 19, 0, (0, 3)), (8, 19, 0, (2, 9)), (8, 19, 0, (6,
         (16, 11, 0, (3,)), (16, 11, 0, (2, 11)), (16, 11, 0, (4, 17)),
         (16, 11, 1, (17,)), (16, 11, 1, (1, 16)), (16, 11, 1, (0, 5)), (16, 11, 1, (7,))]
 # ragged walks at the production shard sizes: RS(12,4) at 1 MiB (S = 87382,
-# 170 steps + 342 bytes) and RS(8,4) with a ragged tail (S = 4100)
+# 170 steps + 342 bytes), RS(10,4) (104858) and RS(6,4) (174763, records at
+# odd offsets), and RS(8,4) with a ragged tail (S = 4100)
 LONG_RAGGED = [(12, 5, 0, (0,), 87382), (12, 5, 0, (2, 13), 87382), (12, 5, 1, (3, 14), 87382),
                (12, 5, 1, (15,), 87382), (12, 6, 0, (5, 7), 4100), (8, 9, 0, (0, 3), 4100), (8, 9, 1, (1, 8), 4100),
-               (8, 9, 0, (2,), 4100), (16, 5, 0, (4, 17), 65540), (16, 5, 1, (1, 16), 65540)]
+               (8, 9, 0, (2,), 4100), (16, 5, 0, (4, 17), 65540), (16, 5, 1, (1, 16), 65540),
+               (10, 5, 0, (0, 3), 104858), (10, 5, 1, (2, 11), 104858), (6, 5, 0, (1, 4), 174763),
+               (6, 5, 1, (0, 7), 174763)]
 
 
 @pytest.mark.parametrize("k,n,heal,lost,S", LONG_RAGGED, ids=str)

@@ -23,6 +23,10 @@ rows) and one `net<PID>` specialisation per pattern.  The launcher matches a
 launch's coefficient rows against the table byte for byte, so a pattern not
 listed (or any disagreement) keeps the run-time-table kernel.
 
+RS(10,4) (`--k 10`, the default geometry of a 14-drive set) gets four
+parts (survivors 0-2 / 3-5 / 6-7 / 8-9) like RS(12,4) (rs104_decode_nets.h,
+rs_decode_netq.hip built with RSG_NETQ_K=10).
+
 RS(6,4) (`--k 6`, the default geometry of a 10-drive set) is generated like
 RS(8,4), one network over its 6 survivors (rs64_decode_nets.h, run by
 rs_decode_net.hip built with RSG_NET_K=6).
@@ -225,7 +229,8 @@ def main():
     # RS(12,4): quarters 0-2 / 3-5 / 6-8 / 9-11 (four network waves, one per
     # SIMD, rs_decode_net12.hip)
     ka = 8
-    halves = {6: [(0, 6)], 8: [(0, 8)], 16: [(0, 8), (8, 8)], 12: [(0, 3), (3, 3), (6, 3), (9, 3)]}[K]
+    halves = {6: [(0, 6)], 8: [(0, 8)], 16: [(0, 8), (8, 8)], 12: [(0, 3), (3, 3), (6, 3), (9, 3)],
+              10: [(0, 3), (3, 3), (6, 2), (8, 2)]}[K]
     if quarters:
         halves = [(c0, K // 4) for c0 in range(0, K, K // 4)]
     tasks = [(p[5], seeds, c0, cn) for c0, cn in halves for p in pats]
@@ -271,9 +276,9 @@ def main():
         for pid, pat in enumerate(pats):
             hdr += emit_net(pid, pat, nets[0][pid])
             hdr.append("")
-    elif K == 12 or quarters:
-        qc = K // 4
-        hdr += [f"// net_q<PID, Q>: all rows over survivors {qc}Q-{qc}Q+{qc - 1} (planes P[0..{8 * qc}))",
+    elif K in (10, 12) or quarters:
+        parts = ", ".join(f"{c0}-{c0 + cn - 1}" for c0, cn in halves)
+        hdr += [f"// net_q<PID, Q>: all rows over part Q of the survivors ({parts}; its planes first in P)",
                 "template <int PID, int Q>", "__device__ void net_q(const uint32_t (&P)[64], uint32_t (&O)[32]);", ""]
         for pid, pat in enumerate(pats):
             for q, (c0, cn) in enumerate(halves):
