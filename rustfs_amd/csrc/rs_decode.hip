@@ -266,9 +266,10 @@ static bool launch_net_if_listed(int heal, int k, int m, int nf, const uint8_t* 
                                                     launch_records_net10_part6, launch_records_net10_part7};
         return (k == 16 ? parts16 : k == 12 ? parts12 : parts10)[pid % RSG_NET_PARTS](pid, blocks, p, h, stream);
     }
-    if (k != 8 && k != 6) return false;
-    const int pid = k == 8 ? records_net_pattern(heal, nf, (int)p.R, (int)p.n_store, coef)
-                           : records_net6_pattern(heal, nf, (int)p.R, (int)p.n_store, coef);
+    if (k != 8 && k != 6 && k != 4) return false;
+    const int pid = k == 8   ? records_net_pattern(heal, nf, (int)p.R, (int)p.n_store, coef)
+                    : k == 6 ? records_net6_pattern(heal, nf, (int)p.R, (int)p.n_store, coef)
+                             : records_net4_pattern(heal, nf, (int)p.R, (int)p.n_store, coef);
     if (pid < 0) return false;
     GfApplyParams q = p;
     q.cached_stores = tuning().get_cached ? 1u : 0u;
@@ -282,7 +283,11 @@ static bool launch_net_if_listed(int heal, int k, int m, int nf, const uint8_t* 
                                                launch_records_net6_part2, launch_records_net6_part3,
                                                launch_records_net6_part4, launch_records_net6_part5,
                                                launch_records_net6_part6, launch_records_net6_part7};
-    return (k == 8 ? parts : parts6)[pid % RSG_NET_PARTS](pid, blocks, q, h, stream);
+    static const Part parts4[RSG_NET_PARTS] = {launch_records_net4_part0, launch_records_net4_part1,
+                                               launch_records_net4_part2, launch_records_net4_part3,
+                                               launch_records_net4_part4, launch_records_net4_part5,
+                                               launch_records_net4_part6, launch_records_net4_part7};
+    return (k == 8 ? parts : k == 6 ? parts6 : parts4)[pid % RSG_NET_PARTS](pid, blocks, q, h, stream);
 }
 
 // The record files' layout the DMA ring can walk: LDS-DMA takes sources at

@@ -1,10 +1,11 @@
-// rs_decode_net.hip — the one-pass GET / heal kernel for RS(8,4) and RS(6,4)
-// (the default geometry of a 10-drive set, storageclass.rs:24-31) with its
-// rows as a compile-time XOR network per erasure pattern
-// (k_decode_records_net<PID> / k_decode_records_net6<PID>; the networks in
-// the generated rs84_decode_nets.h / rs64_decode_nets.h,
-// tools/gen_decode_nets.py [--k 6]).  Compiled RSG_NET_PARTS times per
-// geometry (Makefile: RSG_NET_K = 8 or 6), part RSG_NET_PART instantiating
+// rs_decode_net.hip — the one-pass GET / heal kernel for RS(8,4), RS(6,4)
+// and RS(4,4) (the default geometries of 12-, 10- and 8-drive sets,
+// storageclass.rs:24-31) with its rows as a compile-time XOR network per
+// erasure pattern (k_decode_records_net<PID> / _net6 / _net4; the networks
+// in the generated rs84_decode_nets.h / rs64_decode_nets.h /
+// rs44_decode_nets.h, tools/gen_decode_nets.py [--k 6|4]).  Compiled
+// RSG_NET_PARTS times per geometry (Makefile: RSG_NET_K = 8, 6 or 4), part
+// RSG_NET_PART instantiating
 // the patterns with PID % RSG_NET_PARTS == RSG_NET_PART, so the kernels
 // build in parallel.
 //
@@ -47,8 +48,10 @@
 #define RSG_NET_TAG  // k_decode_records_net, launch_records_net_partN, records_net_pattern
 #elif RSG_NET_K == 6
 #define RSG_NET_TAG 6  // k_decode_records_net6, launch_records_net6_partN, records_net6_pattern
+#elif RSG_NET_K == 4
+#define RSG_NET_TAG 4  // k_decode_records_net4, launch_records_net4_partN, records_net4_pattern
 #else
-#error "RSG_NET_K is 8 or 6"
+#error "RSG_NET_K is 8, 6 or 4"
 #endif
 #define RSG_NET_NAME(pre, post) RSG_NET_CAT(RSG_NET_CAT(pre, RSG_NET_TAG), post)
 
@@ -56,9 +59,12 @@ namespace rsg {
 
 #if RSG_NET_K == 8
 #include "rs84_decode_nets.h"
-#else
+#elif RSG_NET_K == 6
 #include "rs64_decode_nets.h"
 namespace decnet = decnet6;
+#else
+#include "rs44_decode_nets.h"
+namespace decnet = decnet4;
 #endif
 constexpr int kNetC = RSG_NET_K;  // survivors (data shards)
 

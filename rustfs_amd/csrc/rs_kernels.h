@@ -171,6 +171,20 @@ RSG_NET10_PART_DECL(5)
 RSG_NET10_PART_DECL(6)
 RSG_NET10_PART_DECL(7)
 #undef RSG_NET10_PART_DECL
+// RS(4,4) (rs_decode_net.hip built with RSG_NET_K=4, k_decode_records_net4): the same for R x 4 rows
+int records_net4_pattern(int heal, int nf, int R, int n_store, const uint8_t* coef);
+#define RSG_NET4_PART_DECL(i)                                                                                \
+    bool launch_records_net4_part##i(int pid, uint64_t blocks, const GfApplyParams& p, const HashParams& h, \
+                                     hipStream_t stream);
+RSG_NET4_PART_DECL(0)
+RSG_NET4_PART_DECL(1)
+RSG_NET4_PART_DECL(2)
+RSG_NET4_PART_DECL(3)
+RSG_NET4_PART_DECL(4)
+RSG_NET4_PART_DECL(5)
+RSG_NET4_PART_DECL(6)
+RSG_NET4_PART_DECL(7)
+#undef RSG_NET4_PART_DECL
 // RS(6,4) (rs_decode_net.hip built with RSG_NET_K=6, k_decode_records_net6): the same for R x 6 rows
 int records_net6_pattern(int heal, int nf, int R, int n_store, const uint8_t* coef);
 #define RSG_NET6_PART_DECL(i)                                                                                \

@@ -15,6 +15,7 @@ import os
 import re
 
 import numpy as np
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "rustfs_amd", "csrc", "rs84_decode_nets.h")
@@ -266,26 +267,25 @@ def test_rs10_decode_nets_rebuild_true_shards(oracle):
         assert np.array_equal(_bytes(acc, p["R"]), st[want_idx]), p["pid"]
 
 
-# ---------------------------------------------------------------- RS(6,4)
-HEADER6 = os.path.join(ROOT, "rustfs_amd", "csrc", "rs64_decode_nets.h")
-
-
-def test_rs6_decode_nets_rebuild_true_shards(oracle):
-    """RS(6,4), the default geometry of a 10-drive set (rs64_decode_nets.h,
-    k_decode_records_net6: rs_decode_net.hip over 6 survivors): every 1- and
-    2-shard loss (GET: a data shard lost; heal: every loss), one network per
-    pattern giving the true shards, its rows the oracle's decode matrix rows."""
-    k, t = 6, 10
-    src = open(HEADER6).read()
+# ------------------------------------------------------- RS(6,4), RS(4,4)
+@pytest.mark.parametrize("k", [6, 4])
+def test_rs6_rs4_decode_nets_rebuild_true_shards(oracle, k):
+    """RS(6,4) and RS(4,4), the default geometries of 10- and 8-drive sets
+    (rs64_decode_nets.h / rs44_decode_nets.h, k_decode_records_net6 / _net4:
+    rs_decode_net.hip over 6 / 4 survivors): every 1- and 2-shard loss (GET:
+    a data shard lost; heal: every loss), one network per pattern giving the
+    true shards, its rows the oracle's decode matrix rows."""
+    t = k + 4
+    src = open(os.path.join(ROOT, "rustfs_amd", "csrc", f"rs{k}4_decode_nets.h")).read()
     pats = []
     for m in re.finditer(r"\{0x([0-9a-f]+), (\d), (\d+), (\d), (\d), \{(.*?)\}\},  // (\d+)", src):
         rows = [[int(x) for x in r.split(",")] for r in re.findall(r"\{([0-9, ]+)\}", m.group(6))]
         pats.append(dict(absent=int(m.group(1), 16), heal=int(m.group(2)), nf=int(m.group(3)), R=int(m.group(4)),
                          nst=int(m.group(5)), coef=rows, pid=int(m.group(7))))
     assert len(pats) == int(re.search(r"kCount = (\d+)", src).group(1))
-    assert sum(1 for p in pats if p["heal"]) == 10 + 45
-    assert sum(1 for p in pats if not p["heal"]) == 6 + 15 + 6 * 4
-    rng = np.random.default_rng(64)
+    assert sum(1 for p in pats if p["heal"]) == t + t * (t - 1) // 2
+    assert sum(1 for p in pats if not p["heal"]) == k + k * (k - 1) // 2 + k * 4
+    rng = np.random.default_rng(k * 10 + 4)
     gm = oracle.matrix(k, 4)
     for p in pats:
         lost = [i for i in range(t) if p["absent"] >> i & 1]

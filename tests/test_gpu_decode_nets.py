@@ -304,7 +304,8 @@ def test_rs12_every_listed_pattern(gpu, oracle, records12, one_pass, heal, lost)
 # the default geometries of 10- and 14-drive sets (storageclass.rs:24-31) on
 # ragged walks: RS(6,4) with S = 1001 (records at odd offsets), RS(10,4) with
 # S = 1002 (records 2 mod 8, as at 1 MiB blocks)
-GEOS = {6: (11, 1001), 10: (9, 1002)}
+GEOS = {6: (11, 1001), 10: (9, 1002), 4: (13, 1003)}
+LISTED4 = _listed("rs44_decode_nets.h", 8)
 LISTED6 = _listed("rs64_decode_nets.h", 10)
 LISTED10 = _listed("rs104_decode_nets.h", 14)
 
@@ -335,12 +336,18 @@ def records10(gpu, oracle):
     return _geo_records(oracle, 10)
 
 
+@pytest.fixture(scope="module")
+def records4(gpu, oracle):
+    return _geo_records(oracle, 4)
+
+
 def test_rs6_rs10_tables_list_every_pattern():
     """Every one- and two-shard loss: RS(6,4) 6 + 39 GET patterns (a data
     shard among the lost) and 10 + 45 heal patterns; RS(10,4) 10 + 85 and
     14 + 91."""
     assert len([x for x in LISTED6 if not x[0]]) == 6 + 39 and len([x for x in LISTED6 if x[0]]) == 10 + 45
     assert len([x for x in LISTED10 if not x[0]]) == 10 + 85 and len([x for x in LISTED10 if x[0]]) == 14 + 91
+    assert len([x for x in LISTED4 if not x[0]]) == 4 + 22 and len([x for x in LISTED4 if x[0]]) == 8 + 28
 
 
 def _geo_case(oracle, k, data, heal, lost):
@@ -400,6 +407,12 @@ def _geo_case(oracle, k, data, heal, lost):
 def test_rs6_every_listed_pattern(gpu, oracle, records6, one_pass, heal, lost):
     """k_decode_records_net6 (rs_decode_net.hip over 6 survivors)."""
     _geo_case(oracle, 6, records6, heal, lost)
+
+
+@pytest.mark.parametrize("heal,lost", LISTED4, ids=lambda x: str(x))
+def test_rs4_every_listed_pattern(gpu, oracle, records4, one_pass, heal, lost):
+    """k_decode_records_net4 (rs_decode_net.hip over 4 survivors)."""
+    _geo_case(oracle, 4, records4, heal, lost)
 
 
 @pytest.mark.parametrize("heal,lost", LISTED10, ids=lambda x: str(x))
@@ -508,7 +521,7 @@ LONG_RAGGED = [(12, 5, 0, (0,), 87382), (12, 5, 0, (2, 13), 87382), (12, 5, 1, (
                (12, 5, 1, (15,), 87382), (12, 6, 0, (5, 7), 4100), (8, 9, 0, (0, 3), 4100), (8, 9, 1, (1, 8), 4100),
                (8, 9, 0, (2,), 4100), (16, 5, 0, (4, 17), 65540), (16, 5, 1, (1, 16), 65540),
                (10, 5, 0, (0, 3), 104858), (10, 5, 1, (2, 11), 104858), (6, 5, 0, (1, 4), 174763),
-               (6, 5, 1, (0, 7), 174763)]
+               (6, 5, 1, (0, 7), 174763), (4, 9, 0, (0, 5), 262144), (4, 9, 1, (2, 6), 262144)]
 
 
 @pytest.mark.parametrize("k,n,heal,lost,S", LONG_RAGGED, ids=str)
