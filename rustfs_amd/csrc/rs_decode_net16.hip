@@ -3,7 +3,7 @@
 // (k_decode_records_net16<PID>; networks in the generated rs164_decode_nets.h,
 // tools/gen_decode_nets.py --k 16).  Compiled RSG_NET_PARTS times (Makefile)
 // like rs_decode_net.hip.  RS(12,4) has its own four-wave form
-// (rs_decode_net12.hip).
+// (rs_decode_netq.hip).
 //
 // The table kernel's RS(16,4) workgroup (k_decode_records_dma<16,NF,4,TH>:
 // 4 stripes, NF present record files DMA'd into a 3-slot LDS ring per

@@ -119,7 +119,7 @@ hipError_t launch_copy_to_host(uint8_t* dst, const uint8_t* src, uint64_t n, hip
 // digest output [n][C+R][32].  C <= 16, R <= 4, any shard length.
 bool fused_supported(int C, int R, uint64_t shard_len);
 // RS(12,4): the fused encode as the one-pass network heal of every parity
-// shard (rs_decode_net12.hip, k_encode_hash_net12); its 4 x 12 coefficient
+// shard (rs_decode_netq.hip, k_encode_hash_net12); its 4 x 12 coefficient
 // rows, which the launch's tables must match.
 const uint8_t* encode_net12_coef();
 hipError_t launch_encode_hash_net12(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,

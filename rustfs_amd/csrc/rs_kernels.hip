@@ -1480,7 +1480,7 @@ static bool tables_match(const GfApplyParams& p, const uint8_t* coef, int C, int
 }
 
 // RS(12,4) encode in place over 1024+ stripes (256+ workgroups of 4):
-// k_encode_hash_net12 (rs_decode_net12.hip).
+// k_encode_hash_net12 (rs_decode_netq.hip).
 static bool net12_supported(const GfApplyParams& p, uint64_t n_stripes) {
     return p.C == 12 && p.R == 4 && p.mode == GF_MODE_STORE && !p.copy_mask && p.base == p.out_base &&
            p.stripe_stride == p.out_stripe_stride && n_stripes >= 1024 && 5 * p.stripe_stride < (1ull << 32) &&

@@ -112,7 +112,7 @@ def patterns():
     losses = [(a,) for a in range(T)] + [(a, b) for a in range(T) for b in range(a + 1, T)]
     # RS(12,4): also the heal of all four parity shards — rows = the encode
     # matrix over the data shards, which the fused encode + HH256S kernel
-    # (rs_decode_net12.hip, k_encode_hash_net12) runs as its network
+    # (rs_decode_netq.hip, k_encode_hash_net12) runs as its network
     every_parity = [tuple(range(K, T))] if K == 12 else []
     for heal in (0, 1):
         for lost in losses + (every_parity if heal else []):
@@ -228,7 +228,7 @@ def main():
         pats = [p for p in pats if f"{'heal' if p[1] else 'get'}:{','.join(str(i) for i in range(T) if p[0] >> i & 1)}" in only]
     # RS(16,4): survivors 0-7 / 8-15 (two network waves, rs_decode_net16.hip);
     # RS(12,4): quarters 0-2 / 3-5 / 6-8 / 9-11 (four network waves, one per
-    # SIMD, rs_decode_net12.hip)
+    # SIMD, rs_decode_netq.hip)
     ka = 8
     halves = {4: [(0, 4)], 6: [(0, 6)], 8: [(0, 8)], 16: [(0, 8), (8, 8)], 12: [(0, 3), (3, 3), (6, 3), (9, 3)],
               10: [(0, 3), (3, 3), (6, 2), (8, 2)]}[K]
