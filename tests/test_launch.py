@@ -155,3 +155,31 @@ def test_config5_plan(world):
         covered += list(range(s0, s0 + cnt))
     assert covered == list(range(total))
     assert max(p[1] for p in plans) - min(p[1] for p in plans) <= 1
+
+
+def test_pmc_traffic_covers_the_default_line():
+    """Every traffic entry the default bench line and the RS(12,4) lines look
+    up is in tools/pmc_traffic.json (shipped with the tree), and each is
+    within 3 % of the algorithmic bytes of its launch (no wasted re-reads)."""
+    import bench
+    k, m, S, n = 8, 4, 131072, 4096
+    t, rec = k + m, 32 + S
+    want = {
+        f"rs{k}{m}_S{S}_n{n}": n * (k + m) * S,
+        f"rs{k}{m}_S{S}_n{n}_hash": n * (k + m) * S,
+        "rs164_S65536_n4096": 4096 * 20 * 65536,
+        f"get_into0_rs{k}{m}_S{S}_n{n}": n * k * rec,
+        f"get_into2_rs{k}{m}_S{S}_n{n}": n * ((t - 2) * rec + 2 * S),
+        f"get_gather0_rs{k}{m}_S{S}_n{n}": n * (k * rec + k * S),
+        f"get_gather2_rs{k}{m}_S{S}_n{n}": n * ((t - 2) * rec + k * S),
+        f"heal_1d1p_rs{k}{m}_S{S}_n{n}": n * t * rec,
+        f"verify_all_rs{k}{m}_S{S}_n{n}": t * n * rec,
+        "rs124_S87382_n4096": 4096 * 16 * 87382,
+        "rs124_S87382_n4096_hash": 4096 * 16 * 87382,
+    }
+    for r in (1, 2, 3, 4):
+        want[f"reconstruct_e{r}_rs{k}{m}_S{S}_n{n}"] = n * (k + r) * S
+    for key, alg in want.items():
+        got = bench.pmc_lookup(key)
+        assert got is not None, key
+        assert abs(got / alg - 1) < 0.03, (key, got, alg)
