@@ -66,6 +66,8 @@ def parse(argv=None):
     ap.add_argument("--config4-batch", type=int, default=4096, help="config 4 extra: stripes per GPU")
     ap.add_argument("--config5-total", type=int, default=32768,
                     help="config 5 extra: RS(16,4) stripes split over all GPUs (one GPU: its 1/8 share)")
+    ap.add_argument("--no-rs12", action="store_true", help="skip the RS(12,4) (16-drive default) extras")
+    ap.add_argument("--rs12-batch", type=int, default=4096, help="RS(12,4) extras: stripes")
     ap.add_argument("--record-engine", choices=["auto", "one-pass", "two-pass"], default="auto",
                     help="GET/heal engine path for the engine extras (rsg_set_record_engine)")
     return ap.parse_args(argv)
@@ -264,7 +266,7 @@ def pmc_traffic(k, m, S, n, digests):
     return pmc_lookup(f"rs{k}{m}_S{S}_n{n}{'_hash' if digests else ''}")
 
 
-def time_encode(e, stripes, digests, stream, reps, warm=3, warm_seconds=0.3):
+def time_encode(e, stripes, digests, stream, reps, warm=3, warm_seconds=0.5):
     """Average device time (ms) of one rsg_encode_batch_dev over `reps`
     launches: HIP events on the launch stream around each, after `warm`
     untimed launches continued until the device has been busy with this
@@ -340,7 +342,7 @@ def config_extras(a, e_main, stripes, k, m, dev, stream, rank, world=1):
     def timed_ranks(name, e, st, dig, kk, mm, S, n, total):
         torch.cuda.synchronize()
         t_w = time.perf_counter()  # untimed warm-up (clock ramp after the previous extras)
-        while time.perf_counter() - t_w < 0.3:
+        while time.perf_counter() - t_w < 0.5:
             for _ in range(4):
                 e.encode_batch(st, dig, stream=stream)
             torch.cuda.synchronize()
@@ -392,17 +394,59 @@ def config_extras(a, e_main, stripes, k, m, dev, stream, rank, world=1):
     return out
 
 
-def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto"):
+ENGINE_WARM_S = 0.5  # each engine loop: back-to-back calls until the device has been busy this long
+ENGINE_REPS = 20     # then this many timed calls (kernel median / min / max from the in-call hook)
+
+
+def engine_plan(k, m, S, n, full=True):
+    """The engine extras one geometry's line carries: (name, algorithmic bytes
+    per call, PMC lookup key or None).  Algorithmic bytes are what the call's
+    contract moves at minimum: every record it must verify read once (t - e
+    present files of 32 + S bytes per stripe), every output byte written once.
+    full (the RS(8,4) headline's geometry): also the asynchronous GET / heal."""
+    t, rec = k + m, 32 + S
+    g = f"rs{k}{m}_S{S}_n{n}"
+    plan = [("get_all_present", n * k * rec, f"get_into0_{g}"),
+            ("get_2_data_lost", n * ((t - 2) * rec + 2 * S), f"get_into2_{g}"),
+            ("heal_1data_1parity", n * ((t - 2) * rec + 2 * rec), f"heal_1d1p_{g}"),
+            ("bitrot_verify_all_files", t * n * rec, f"verify_all_{g}")]
+    if full:
+        plan += [("get_2_data_lost_async", n * ((t - 2) * rec + 2 * S), None),
+                 ("heal_1data_1parity_async", n * ((t - 2) * rec + 2 * rec), None)]
+    return plan
+
+
+def steady_loop(fn, warm_s):
+    """Back-to-back calls of fn until the device has been busy for warm_s
+    (the clock the chip holds under this load, not the first calls after an
+    idle or a different kernel); returns the last result."""
+    import torch
+    r = fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < warm_s:
+        for _ in range(4):
+            r = fn()
+        torch.cuda.synchronize()
+    return r
+
+
+def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto", full=True, reps=ENGINE_REPS,
+                  warm_s=ENGINE_WARM_S):
     """SURVEY §8(f) engines on the same device-resident batch, as BitrotWriter
     record files ([HH256S][S bytes] per block): GET all present, GET with two
-    data disks lost, heal of one data + one parity disk, whole-file
-    bitrot_verify.  The calls are synchronous (per-stripe status to the host);
-    each is timed with HIP events on the stream around the whole call, and its
-    HBM roofline is priced on the bytes its contract moves at minimum:
-    every record it must verify is read once, every output byte written once."""
+    data disks lost (in place, reconstruct_into's contract), heal of one data
+    + one parity disk, whole-file bitrot_verify (engine_plan).  Every entry is
+    timed in steady state, the headline's protocol: warm-up calls until the
+    device has been busy for warm_s, then `reps` calls; the kernel time of each
+    comes from HIP events recorded inside the call (rsg_set_kernel_timing) —
+    median, min and max — and the whole calls' time from HIP events on the
+    stream around all of them.  The roofline is priced on engine_plan's
+    algorithmic bytes."""
     import torch
     from rustfs_amd.bitrot import HashAlgorithm, bitrot_verify_batch
     t, rec = k + m, 32 + S
+    plan = {name: (alg, key) for name, alg, key in engine_plan(k, m, S, n, full)}
     dig = torch.empty((n, t, 32), dtype=torch.uint8, device=stripes.device)
     e.encode_batch(stripes, dig, stream=stream)
     files = []
@@ -412,7 +456,6 @@ def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto"):
         f[:, 32:] = stripes[:, i]
         files.append(f.reshape(-1))
     del dig
-    out = torch.empty((n, k * S), dtype=torch.uint8, device=stripes.device)
     want_last = stripes[n - 1, :k].reshape(-1).clone()
     res = {}
 
@@ -420,60 +463,46 @@ def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto"):
     from rustfs_amd import _lib
     L, ctx = _lib.load(), _lib.context(stripes.device.index or 0).handle
 
-    def timed(name, fn, alg, check, reps=5, traffic_key=None):
-        fn()
-        torch.cuda.synchronize()
-        # each loop starts from an idle GPU: after ~20 back-to-back one-pass
-        # calls the clock drops (a power transient: the hooked loop right
-        # after the plain one ran 1.62 ms per call against 1.38 ms,
-        # profiles/r04/h/bench.json), which would set the two loops apart
-        time.sleep(0.5)
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        ev[0].record(stream)
-        for _ in range(reps):
-            r = fn()
-        ev[1].record(stream)
-        torch.cuda.synchronize()
-        ms = ev[0].elapsed_time(ev[1]) / reps
-        check(r)
-        res[name] = {"call_ms": round(ms, 4), "GiB_s_payload": round(n * k * S / (ms * 1e-3) / GiB, 1),
-                     "alg_bytes": alg, "achieved_GB_s": round(alg / (ms * 1e-3) / 1e9, 1),
-                     "frac_call": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                     "traffic": pmc_lookup(traffic_key) if traffic_key else None}
-        # the engine's kernels alone (HIP events around its launches inside
-        # the call, rsg_set_kernel_timing), the median of `reps` more calls
+    def timed(name, fn, check):
+        alg, key = plan[name]
+        steady_loop(fn, warm_s)
         kms = []
-        time.sleep(0.5)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         _lib.check(L.rsg_set_kernel_timing(ctx, 1))
         try:
             ev[0].record(stream)
             for _ in range(reps):
-                fn()
+                r = fn()
                 v = ctypes.c_float(-1)
                 _lib.check(L.rsg_last_kernel_ms(ctx, ctypes.byref(v)))
                 kms.append(v.value)
             ev[1].record(stream)
             torch.cuda.synchronize()
-            # the same calls' whole time with the hook on (against call_ms:
-            # whether the hook's events change the calls themselves)
-            res[name]["call_ms_hooked"] = round(ev[0].elapsed_time(ev[1]) / reps, 4)
         finally:
             _lib.check(L.rsg_set_kernel_timing(ctx, 0))
+        check(r)
+        ms = ev[0].elapsed_time(ev[1]) / reps
+        res[name] = {"call_ms": round(ms, 4), "calls": reps, "warm_s": warm_s,
+                     "GiB_s_payload": round(n * k * S / (ms * 1e-3) / GiB, 1),
+                     "alg_bytes": alg, "achieved_GB_s": round(alg / (ms * 1e-3) / 1e9, 1),
+                     "frac_call": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "traffic": pmc_lookup(key) if key else None}
         if kms and min(kms) > 0:
-            km = sorted(kms)[len(kms) // 2]  # the median (one call's outlier does not move it)
-            res[name].update({"kernel_ms": round(km, 4), "kernel_ms_each": [round(x, 4) for x in kms],
+            km = sorted(kms)[len(kms) // 2]  # the median
+            res[name].update({"kernel_ms": round(km, 4), "kernel_ms_min": round(min(kms), 4),
+                              "kernel_ms_max": round(max(kms), 4), "max_over_min": round(max(kms) / min(kms), 3),
+                              "kernel_ms_each": [round(x, 4) for x in kms],
                               "frac": round(alg / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
         else:
             res[name]["frac"] = res[name]["frac_call"]
 
-    def timed_pipelined(name, submit, alg, check, reps=8):
+    def timed_pipelined(name, submit, check):
         """`reps` calls, each submitted before the previous one is waited on
-        (the asynchronous ABI), timed with HIP events on the stream around
-        all of them: the device never idles while the host reads a batch's
-        verdicts, so the per-call time approaches the kernel time."""
-        submit().wait()
-        torch.cuda.synchronize()
-        time.sleep(0.5)  # from an idle GPU, as timed()
+        (the asynchronous ABI), after the same steady-state warm-up, timed
+        with HIP events on the stream around all of them: the device never
+        idles while the host reads a batch's verdicts."""
+        alg, _ = plan[name]
+        steady_loop(lambda: submit().wait(), warm_s)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record(stream)
         tk = submit()
@@ -486,17 +515,16 @@ def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto"):
         torch.cuda.synchronize()
         ms = ev[0].elapsed_time(ev[1]) / reps
         check(r)
-        res[name] = {"call_ms": round(ms, 4), "calls": reps, "GiB_s_payload": round(n * k * S / (ms * 1e-3) / GiB, 1),
+        res[name] = {"call_ms": round(ms, 4), "calls": reps, "warm_s": warm_s,
+                     "GiB_s_payload": round(n * k * S / (ms * 1e-3) / GiB, 1),
                      "alg_bytes": alg, "frac_call": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
     _lib.check(L.rsg_set_record_engine(ctx, {"auto": _lib.RSG_RECORD_ENGINE_AUTO,
                                               "one-pass": _lib.RSG_RECORD_ENGINE_ONE_PASS,
                                               "two-pass": _lib.RSG_RECORD_ENGINE_TWO_PASS}[record_engine]))
     res["record_engine"] = record_engine
-
-    def ok_get(r):
-        o, status = r
-        assert all(x == 0 for x in status) and torch.equal(o[n - 1], want_last)
+    res["protocol"] = (f"steady state: back-to-back calls until the device has been busy {warm_s} s, then "
+                       f"{reps} timed calls; kernel_ms = median of the in-call HIP-event kernel times")
 
     # GET, in-place form (rsg_decode_records_into_dev, reconstruct_into's
     # contract, bridge.rs:274-307): present data served from the verified
@@ -517,19 +545,13 @@ def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto"):
 
     lost = [None if i in (0, 3) else files[i] for i in range(t)]
     timed("get_all_present", lambda: e.decode_records_into_batch(files, S, n, targets=slots, stream=stream),
-          n * k * rec, ok_into(()), traffic_key=f"get_into0_rs{k}{m}_S{S}_n{n}")
+          ok_into(()))
     timed("get_2_data_lost", lambda: e.decode_records_into_batch(lost, S, n, targets=slots, stream=stream),
-          n * ((t - 2) * rec + 2 * S), ok_into((0, 3)), traffic_key=f"get_into2_rs{k}{m}_S{S}_n{n}")
-    # the same GETs submitted back to back (rsg_decode_records_submit): each
-    # batch's status handling overlaps the next batch's kernels
-    timed_pipelined("get_2_data_lost_async",
-                    lambda: e.decode_records_submit(lost, S, n, targets=slots, inplace=True, stream=stream),
-                    n * ((t - 2) * rec + 2 * S), ok_into((0, 3)))
-    # gather form (rsg_decode_records_dev: every data shard copied to one block buffer)
-    timed("get_all_present_gather", lambda: e.decode_records_batch(files, S, n, out=out, stream=stream),
-          n * (k * rec + k * S), ok_get, traffic_key=f"get_gather0_rs{k}{m}_S{S}_n{n}")
-    timed("get_2_data_lost_gather", lambda: e.decode_records_batch(lost, S, n, out=out, stream=stream),
-          n * ((t - 2) * rec + k * S), ok_get, traffic_key=f"get_gather2_rs{k}{m}_S{S}_n{n}")
+          ok_into((0, 3)))
+    if full:  # the same GETs submitted back to back (rsg_decode_records_submit)
+        timed_pipelined("get_2_data_lost_async",
+                        lambda: e.decode_records_submit(lost, S, n, targets=slots, inplace=True, stream=stream),
+                        ok_into((0, 3)))
     tg = [torch.empty(n * rec, dtype=torch.uint8, device=stripes.device) if i in (1, k) else None for i in range(t)]
     src = [None if i in (1, k) else files[i] for i in range(t)]
 
@@ -539,16 +561,40 @@ def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto"):
     def ok_verify(status):
         assert status == [0] * t
 
-    timed("heal_1data_1parity", lambda: e.heal_records_batch(src, tg, S, n, stream=stream),
-          n * ((t - 2) * rec + 2 * rec), ok_heal, traffic_key=f"heal_1d1p_rs{k}{m}_S{S}_n{n}")
-    timed_pipelined("heal_1data_1parity_async", lambda: e.heal_records_submit(src, tg, S, n, stream=stream),
-                    n * ((t - 2) * rec + 2 * rec), ok_heal)
+    timed("heal_1data_1parity", lambda: e.heal_records_batch(src, tg, S, n, stream=stream), ok_heal)
+    if full:
+        timed_pipelined("heal_1data_1parity_async", lambda: e.heal_records_submit(src, tg, S, n, stream=stream),
+                        ok_heal)
     timed("bitrot_verify_all_files",
           lambda: bitrot_verify_batch(files, n * rec, n * S, HashAlgorithm.HighwayHash256S, S, stream=stream),
-          t * n * rec, ok_verify, traffic_key=f"verify_all_rs{k}{m}_S{S}_n{n}")
-    del files, lost, tg, src, out, slots
+          ok_verify)
+    del files, lost, tg, src, slots
     torch.cuda.empty_cache()
     return res
+
+
+def rs12_4_extras(a, dev, stream):
+    """rustfs's 16-drive default, RS(12,4) (storageclass.rs:24-31), at 1 MiB
+    blocks (S = 87382: ragged walks, records at 2 mod 8) on the driver's line:
+    encode, encode + fused HH256S (the PUT path's kernel), and the engines of
+    engine_plan(12, 4, ...) — each with kernel_ms, frac and traffic."""
+    import torch
+    from rustfs_amd import Erasure
+    k, m, n = 12, 4, a.rs12_batch
+    S = -(-(1 << 20) // k)
+    st = random_stripes(dev, k, m, S, n, 4000)
+    e = Erasure(k, m, 1 << 20, device=dev.index)
+    out = {"workload": f"RS(12,4), 1 MiB blocks (S={S}), {n} stripes (16-drive default set, storageclass.rs:24-31)"}
+    reps = max(10, a.steps)
+    out["encode"] = encode_extra(f"RS(12,4) encode, S={S}, n={n}", e, st, None, k, m, S, n, stream, reps)
+    dig = torch.empty((n, k + m, 32), dtype=torch.uint8, device=dev)
+    out["encode_fused_hh256s"] = encode_extra(f"RS(12,4) encode + fused HH256S, S={S}, n={n}", e, st, dig,
+                                              k, m, S, n, stream, reps)
+    del dig
+    out["engines"] = engine_extras(e, st, k, m, S, n, stream, full=False)
+    del st
+    torch.cuda.empty_cache()
+    return out
 
 
 def main(argv=None):
@@ -664,6 +710,8 @@ def main(argv=None):
         extras["verify_all_ok_after_reconstruct"] = bool(ok.all().item())
         if not a.no_engines and world == 1 and not a.digests:
             extras["engines"] = engine_extras(e, stripes, k, m, S, n, stream, a.record_engine)
+        if not a.no_engines and not a.no_rs12 and world == 1 and (k, m) != (12, 4):
+            extras["rs12_4"] = rs12_4_extras(a, dev, stream)
         if not a.no_config_extras:
             extras.update(config_extras(a, e, stripes, k, m, dev, stream, rank, world))
 

@@ -183,3 +183,29 @@ def test_pmc_traffic_covers_the_default_line():
         got = bench.pmc_lookup(key)
         assert got is not None, key
         assert abs(got / alg - 1) < 0.03, (key, got, alg)
+
+
+def test_engine_plan_rs12_4():
+    """The RS(12,4) extras of the driver's line (the 16-drive default set,
+    storageclass.rs:24-31): in-place GET with 0 and 2 data lost, heal of one
+    data + one parity disk and the whole-file bitrot_verify, priced on the
+    contract's minimum bytes at S = ceil(1 MiB / 12) = 87382, n = 4096; the
+    RS(8,4) line adds the asynchronous GET / heal."""
+    import bench
+    k, m, n = 12, 4, 4096
+    S = -(-(1 << 20) // k)
+    assert S == 87382
+    t, rec = k + m, 32 + S
+    plan = {name: (alg, key) for name, alg, key in bench.engine_plan(k, m, S, n, full=False)}
+    assert plan == {
+        "get_all_present": (n * k * rec, "get_into0_rs124_S87382_n4096"),
+        "get_2_data_lost": (n * (14 * rec + 2 * S), "get_into2_rs124_S87382_n4096"),
+        "heal_1data_1parity": (n * t * rec, "heal_1d1p_rs124_S87382_n4096"),
+        "bitrot_verify_all_files": (t * n * rec, "verify_all_rs124_S87382_n4096"),
+    }
+    full = [name for name, _, _ in bench.engine_plan(8, 4, 131072, 4096)]
+    assert full[-2:] == ["get_2_data_lost_async", "heal_1data_1parity_async"]
+    # the engine loops time at least 20 calls after a >= 0.5 s busy warm-up
+    assert bench.ENGINE_REPS >= 20 and bench.ENGINE_WARM_S >= 0.5
+    a = bench.parse([])
+    assert a.rs12_batch == 4096 and not a.no_rs12

@@ -2,9 +2,12 @@
 two data disks lost, or heal, RS(8,4) 1 MiB stripes, n = 4096 records.
 get* = the gather form (rsg_decode_records_dev), into* = the in-place form
 (rsg_decode_records_into_dev).
-Usage: python tools/engine_prof.py get2|get2_01|get1|get0|into2|into1|into0|heal [reps]"""
+Usage: python tools/engine_prof.py get2|get2_01|get1|get0|into2|into1|into0|heal [reps]
+EP_LOOPS=L EP_SLEEP=s: L loops of `reps` calls, each after s seconds idle (the
+bench's engine protocol of round 4, for the per-dispatch clock table)."""
 import os
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -41,7 +44,12 @@ def main():
         files[10].view(n, rec)[:, 32:] ^= 0x5A
     if not early:
         out = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
-    for _ in range(reps):
+    loops = int(os.environ.get("EP_LOOPS", "1"))
+    idle = float(os.environ.get("EP_SLEEP", "0"))
+    for _ in range(loops * reps):
+        if idle and _ % reps == 0:
+            torch.cuda.synchronize()
+            time.sleep(idle)
         if what == "heal":
             tg = [torch.empty(n * rec, dtype=torch.uint8, device="cuda") if i in (1, k) else None for i in range(t)]
             e.heal_records_batch([None if i in (1, k) else files[i] for i in range(t)], tg, S, n)
