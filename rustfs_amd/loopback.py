@@ -7,7 +7,8 @@ what exercises the codec path:
 
 * PUT: split the object into `block_size` blocks, encode every block
   (Erasure::encode_data), write each shard as interleaved `[HH256S][block]`
-  records (BitrotWriter::write, bitrot.rs:464-510) to `<dir_i>/<object>/part.1`.
+  records (BitrotWriter::write, bitrot.rs:464-510) to
+  `<dir_i>/<object>/<version>/part.1`.
   Full blocks go through one batched call (rsg_encode_batch_host) that returns
   parity and all bitrot digests in the same pass (the encode_batched dispatch
   point, encode.rs:795-919); the short tail block through encode_data.
@@ -16,21 +17,26 @@ what exercises the codec path:
   missing for the block), reconstruct missing data shards
   (decode_data_with_reconstruction_verification, erasure.rs:935-973), and
   return the first `size` bytes.  Full blocks go through the GPU GET engine
-  (rsg_decode_records_dev).
+  (rsg_decode_records_into_dev, in place: only the rebuilt shards are written).
 * HEAL: rebuild the shard files of replaced disks (Erasure::heal,
   heal.rs:112-206) — full blocks in one rsg_heal_records_dev call, the tail
   block through decode_data_and_parity — byte-identical to what PUT wrote.
 * VERIFY: deep-scan every shard file (bitrot_verify, bitrot.rs:616-655) with
   one rsg_bitrot_verify_dev call.
 
-Commit: a PUT writes every shard file under a temporary name and renames the
-written ones into place only once the write quorum holds, then writes each
-disk's meta.json (tagged with the PUT's version id); a disk whose writer was
-dropped loses its previous version's part and meta (heal rebuilds them), and a
-PUT that fails leaves the previous version untouched — the reference stages
-through a temporary directory and renames on commit (rename_data).  GET and
-heal pick the metadata version held by the most disks and read only the shard
-files of disks holding it (the reference's quorum choice of FileInfo).
+Commit: a PUT writes every shard file into a directory of its own version id
+(the reference's per-version data_dir, which xl.meta points to), and only once
+the write quorum holds replaces each disk's meta.json (naming that version and
+its modification time) — one atomic rename switches a disk's part and
+metadata together — then removes the disk's other version directories.  A
+crash or an interleaved PUT can leave a disk on either version, never with one
+version's part under another's metadata.  A disk whose writer was dropped
+loses its previous version (heal rebuilds it), and a PUT that fails leaves the
+previous version untouched (rename_data).  GET and heal pick the metadata
+version held by at least k disks (read quorum; the most disks, then the newest
+modification time) and read only the shard files of disks holding it (the
+reference's quorum choice of FileInfo); no version with k disks is a read-quorum
+error.
 
 Shard placement is identity (shard i on disk i); the reference's key-hash
 distribution, xl.meta, quorum and locking are out of scope.
@@ -39,7 +45,9 @@ from __future__ import annotations
 
 import json
 import os
+import shutil
 import threading
+import time
 import uuid
 from typing import Iterator, List, Optional
 
@@ -77,8 +85,18 @@ class LocalErasureSet:
     def m(self) -> int:
         return self.erasure.parity_shards
 
-    def _path(self, i: int, name: str) -> str:
-        return os.path.join(self.dirs[i], name, "part.1")
+    def _path(self, i: int, name: str, version: str) -> str:
+        """Disk i's part file of `version` (the version's own data dir)."""
+        return os.path.join(self.dirs[i], name, version, "part.1")
+
+    def part_file(self, i: int, name: str) -> Optional[str]:
+        """Disk i's part file of the version its meta.json names (None: the
+        disk holds no committed version of `name`)."""
+        try:
+            with open(os.path.join(self.dirs[i], name, "meta.json")) as f:
+                return self._path(i, name, json.load(f)["version"])
+        except (OSError, ValueError, KeyError):
+            return None
 
     # ------------------------------------------------------------------ PUT
     def put_object(self, name: str, data) -> dict:
@@ -119,9 +137,6 @@ class LocalErasureSet:
                 self._stage_lock.release()
         return self._commit(name, int(data.size), version)
 
-    def _tmp(self, i: int, name: str, version: str) -> str:
-        return self._path(i, name) + ".tmp-" + version
-
     def _write_records(self, name: str, records: List[list], tail, version: str) -> None:
         e, t = self.erasure, self.k + self.m
         if tail is not None:
@@ -129,8 +144,8 @@ class LocalErasureSet:
             for i in range(t):
                 records[i] += [self.algo.hash_encode(shards[i]), shards[i]]
         for i in range(t):
-            os.makedirs(os.path.dirname(self._path(i, name)), exist_ok=True)
-            fd = os.open(self._tmp(i, name, version), os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+            os.makedirs(os.path.dirname(self._path(i, name, version)), exist_ok=True)
+            fd = os.open(self._path(i, name, version), os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
             try:
                 for c0 in range(0, len(records[i]), 512):  # IOV_MAX is 1024 on Linux
                     chunk = records[i][c0:c0 + 512]
@@ -160,8 +175,8 @@ class LocalErasureSet:
         try:
             for i in range(t):
                 try:  # a disk that cannot take the part has no writer (DiskNotFound)
-                    os.makedirs(os.path.dirname(self._path(i, name)), exist_ok=True)
-                    fds.append(os.open(self._tmp(i, name, version), os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644))
+                    os.makedirs(os.path.dirname(self._path(i, name, version)), exist_ok=True)
+                    fds.append(os.open(self._path(i, name, version), os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644))
                 except OSError:
                     fds.append(None)
             info = put_stream(e, reader, size, fds, self.algo, batch_blocks, inflight_batches,
@@ -188,29 +203,40 @@ class LocalErasureSet:
 
     def _discard(self, name: str, version: str) -> None:
         for i in range(self.k + self.m):
-            try:
-                os.unlink(self._tmp(i, name, version))
-            except OSError:
-                pass
+            shutil.rmtree(os.path.join(self.dirs[i], name, version), ignore_errors=True)
+
+    def _drop_other_versions(self, i: int, name: str, keep: Optional[str]) -> None:
+        """Remove disk i's version directories other than `keep` (after its
+        meta.json switched: nothing reads them any more)."""
+        base = os.path.join(self.dirs[i], name)
+        try:
+            entries = os.listdir(base)
+        except OSError:
+            return
+        for d in entries:
+            if d != keep and os.path.isdir(os.path.join(base, d)):
+                shutil.rmtree(os.path.join(base, d), ignore_errors=True)
 
     def _commit(self, name: str, size: int, version: str, skip=()) -> dict:
-        """Rename the written shard files into place and write each disk's
-        meta.json; a skipped (dropped) disk keeps nothing of the previous
-        version, so no GET or heal reads a stale part or size from it."""
+        """Switch each disk to the new version: its meta.json is replaced in
+        one rename (the part file already sits in the version's directory),
+        then the disk's other versions are removed.  A skipped (dropped) disk
+        keeps nothing of the previous version, so no GET or heal reads a stale
+        part or size from it."""
         e = self.erasure
         meta = {"size": int(size), "data_blocks": self.k, "parity_blocks": self.m, "block_size": e.block_size,
-                "shard_size": e.shard_size(), "algorithm": self.algo.name, "version": version}
+                "shard_size": e.shard_size(), "algorithm": self.algo.name, "version": version,
+                "mod_time": time.time_ns()}
         for i in range(self.k + self.m):
             if i in skip:
-                for p in (self._tmp(i, name, version), self._path(i, name),
-                          os.path.join(self.dirs[i], name, "meta.json")):
-                    try:
-                        os.unlink(p)
-                    except OSError:
-                        pass
+                try:
+                    os.unlink(os.path.join(self.dirs[i], name, "meta.json"))
+                except OSError:
+                    pass
+                self._drop_other_versions(i, name, None)
                 continue
-            os.replace(self._tmp(i, name, version), self._path(i, name))
             self._write_meta_file(i, name, meta)
+            self._drop_other_versions(i, name, version)
         return meta
 
     def _write_meta_file(self, i: int, name: str, meta: dict) -> None:
@@ -221,8 +247,11 @@ class LocalErasureSet:
 
     # ------------------------------------------------------------------ GET
     def _meta(self, name: str) -> dict:
-        """The metadata version held by the most disks (ties: the lowest disk
-        index holding one), with "disks": the disks that hold it."""
+        """The metadata version the set serves, with "disks": the disks that
+        hold it.  Only a version on at least k disks can be read (read quorum,
+        the reference's quorum choice of FileInfo); among those, the one held
+        by the most disks, then the newest modification time.  No version
+        with k disks: a read-quorum error."""
         votes: dict = {}
         for i in range(self.k + self.m):
             try:
@@ -234,10 +263,13 @@ class LocalErasureSet:
             votes.setdefault(key, (meta, []))[1].append(i)
         if not votes:
             raise FileNotFoundError(name)
-        meta, disks = max(votes.values(), key=lambda v: (len(v[1]), -v[1][0]))
+        quorum = [v for v in votes.values() if len(v[1]) >= self.k]
+        if not quorum:
+            raise _lib.RsgError(_lib.RSG_ERR_TOO_FEW_SHARDS, f"{name}: no metadata version reaches read quorum")
+        meta, disks = max(quorum, key=lambda v: (len(v[1]), v[0].get("mod_time", 0), -v[1][0]))
         return dict(meta, disks=disks)
 
-    def _open_shards(self, name: str, size: int, disks=None) -> List[Optional[int]]:
+    def _open_shards(self, name: str, size: int, version: str, disks=None) -> List[Optional[int]]:
         """Shard file descriptors; a missing or wrong-length file, or a disk
         not holding the chosen metadata version, is None (the reader for that
         disk is unavailable)."""
@@ -249,7 +281,7 @@ class LocalErasureSet:
                 fds.append(None)
                 continue
             try:
-                fd = os.open(self._path(i, name), os.O_RDONLY)
+                fd = os.open(self._path(i, name, version), os.O_RDONLY)
             except OSError:
                 fds.append(None)
                 continue
@@ -270,7 +302,7 @@ class LocalErasureSet:
         get_object_range does."""
         meta = self._meta(name)
         size = meta["size"]
-        fds = self._open_shards(name, size, meta["disks"])
+        fds = self._open_shards(name, size, meta["version"], meta["disks"])
         try:
             yield from get_stream(self.erasure, fds, size, offset, length, self.algo, batch_blocks, self._get_stage)
         finally:
@@ -298,7 +330,7 @@ class LocalErasureSet:
             raw = None
             if i not in targets and i in meta["disks"]:
                 try:
-                    with open(self._path(i, name), "rb") as f:
+                    with open(self._path(i, name, meta["version"]), "rb") as f:
                         raw = f.read()
                 except OSError:
                     raw = None
@@ -340,13 +372,15 @@ class LocalErasureSet:
             for i in targets:
                 out[i] += self.algo.hash_encode(bytes(shards[i])) + bytes(shards[i])
         meta = {key: v for key, v in meta.items() if key != "disks"}
-        for i in targets:
-            os.makedirs(os.path.dirname(self._path(i, name)), exist_ok=True)
-            tmp = self._path(i, name) + ".heal-tmp"
+        for i in targets:  # the healed part in the version's directory, then the disk's meta switches to it
+            path = self._path(i, name, meta["version"])
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            tmp = path + ".heal-tmp"
             with open(tmp, "wb") as f:
                 f.write(bytes(out[i]))
-            os.replace(tmp, self._path(i, name))
+            os.replace(tmp, path)
             self._write_meta_file(i, name, meta)
+            self._drop_other_versions(i, name, meta["version"])
 
     # --------------------------------------------------------------- VERIFY
     def verify_object(self, name: str) -> List[int]:
@@ -361,7 +395,7 @@ class LocalErasureSet:
         files = []
         for i in range(t):
             try:
-                with open(self._path(i, name), "rb") as f:
+                with open(self._path(i, name, meta["version"]), "rb") as f:
                     raw = f.read()
                 files.append(torch.frombuffer(bytearray(raw), dtype=torch.uint8).to("cuda") if raw
                              else torch.empty(0, dtype=torch.uint8, device="cuda"))

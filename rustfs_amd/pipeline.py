@@ -20,7 +20,7 @@ GET — ``get_stream`` mirrors ``Erasure::decode_inner``
 (crates/ecstore/src/erasure/coding/decode.rs:1702-1968) for a byte range:
 the blocks covering [offset, offset + length) are read from the shard files B
 blocks at a time (a read-ahead thread fetches batch i+1 while batch i is
-verified and decoded on the GPU by ``rsg_decode_records_dev``), and the
+verified and decoded on the GPU by ``rsg_decode_records_into_dev``), and the
 requested bytes of each block are yielded in order (the block geometry of
 decode.rs:1767-1781).  A short last block goes through the host codec path.
 """

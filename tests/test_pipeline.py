@@ -63,8 +63,8 @@ def _set(tmp_path, k, m, bs=BS):
     return LocalErasureSet(dirs, k, m, block_size=bs), dirs
 
 
-def _files(dirs, name):
-    return [open(os.path.join(d, name, "part.1"), "rb").read() for d in dirs]
+def _files(es, name):
+    return [open(es.part_file(i, name), "rb").read() for i in range(len(es.dirs))]
 
 
 def _reader(kind, data, tmp_path):
@@ -92,7 +92,7 @@ def test_put_stream_writes_put_object_files(gpu, oracle, tmp_path, kind, k, m, n
     if kind == "file":
         assert r.read() == b"TRAILER"  # left positioned after the body
     es.put_object("b/o", data)
-    got, want = _files(dirs, "b/s"), _files(dirs, "b/o")
+    got, want = _files(es, "b/s"), _files(es, "b/o")
     assert got == want
     # oracle: block by block [HH256S][shard] records
     if size:
@@ -127,7 +127,7 @@ def test_range_get(gpu, tmp_path, k, m, lost):
     data = np.random.default_rng(5).integers(0, 256, size, dtype=np.uint8).tobytes()
     es.put_object_stream("b/o", io.BytesIO(data), size, batch_blocks=4)
     for i in lost:
-        os.remove(os.path.join(dirs[i], "b/o", "part.1"))
+        os.remove(es.part_file(i, "b/o"))
     for off, ln in _ranges(size, BS):
         got = b"".join(es.get_object_stream("b/o", off, ln, batch_blocks=3))
         assert got == data[off:off + ln], (off, ln)
@@ -145,7 +145,7 @@ def test_range_get_drops_corrupted_records(gpu, tmp_path):
     rec = 32 + BS // 4
 
     def flip(i, off):
-        p = os.path.join(dirs[i], "b/o", "part.1")
+        p = es.part_file(i, "b/o")
         raw = bytearray(open(p, "rb").read())
         raw[off] ^= 0x40
         open(p, "wb").write(bytes(raw))
@@ -196,10 +196,11 @@ class _BreakWriters(io.BytesIO):
         return n
 
     def _fd_of(self, i):
-        want = os.path.realpath(os.path.join(self.es.dirs[i], self.name, "part.1"))
+        base = os.path.realpath(os.path.join(self.es.dirs[i], self.name)) + os.sep
         for fd in os.listdir("/proc/self/fd"):
-            try:  # the PUT writes part.1 under a temporary name until it commits
-                if os.path.realpath(f"/proc/self/fd/{fd}").startswith(want + ".tmp-"):
+            try:  # the PUT writes <name>/<its version>/part.1 (nothing else is open there)
+                p = os.path.realpath(f"/proc/self/fd/{fd}")
+                if p.startswith(base) and p.endswith(os.sep + "part.1"):
                     return int(fd)
             except OSError:
                 pass
@@ -226,13 +227,12 @@ def test_put_stream_write_quorum(gpu, tmp_path, k, m, broken, ok):
         return
     es.put_object_stream("b/o", r, size, batch_blocks=2, inflight_batches=1)
     assert es.last_put["failed_shards"] == sorted(broken)
-    for i in broken:
-        assert not os.path.exists(os.path.join(dirs[i], "b/o", "part.1"))
-        assert not os.path.exists(os.path.join(dirs[i], "b/o", "meta.json"))
+    for i in broken:  # neither a meta.json nor any version's part
+        assert es.part_file(i, "b/o") is None and os.listdir(os.path.join(dirs[i], "b/o")) == []
     assert es.get_object("b/o") == data
     es.put_object("b/ref", data)
     es.heal_object("b/o", list(broken))
-    assert _files(dirs, "b/o") == _files(dirs, "b/ref")
+    assert _files(es, "b/o") == _files(es, "b/ref")
 
 
 @pytest.mark.gpu
@@ -278,8 +278,7 @@ def test_overwrite_with_dropped_writer(gpu, tmp_path, old_size, new_size):
     es.put_object_stream("b/o", _BreakWriters(new, BS, es, "b/o", (0,)), new_size, batch_blocks=2,
                          inflight_batches=1)
     assert es.last_put["failed_shards"] == [0]
-    assert not os.path.exists(os.path.join(dirs[0], "b/o", "meta.json"))
-    assert not os.path.exists(os.path.join(dirs[0], "b/o", "part.1"))
+    assert es.part_file(0, "b/o") is None and os.listdir(os.path.join(dirs[0], "b/o")) == []
     assert es.get_object("b/o") == new
     es.heal_object("b/o", [0])
     assert es.get_object("b/o") == new
@@ -288,7 +287,9 @@ def test_overwrite_with_dropped_writer(gpu, tmp_path, old_size, new_size):
         es.put_object_stream("b/o", _BreakWriters(old, BS, es, "b/o", (0, 1, 2)), old_size, batch_blocks=2,
                              inflight_batches=1)
     assert es.get_object("b/o") == new
-    assert not [f for d in dirs for f in os.listdir(os.path.join(d, "b/o")) if ".tmp" in f]
+    # every disk holds its meta.json and the committed version's directory, nothing else
+    ver = es._meta("b/o")["version"]
+    assert all(sorted(os.listdir(os.path.join(d, "b/o"))) == sorted(["meta.json", ver]) for d in dirs)
 
 
 @pytest.mark.gpu
@@ -301,9 +302,11 @@ def test_meta_by_quorum(gpu, tmp_path):
     a = np.random.default_rng(3).integers(0, 256, 2 * BS + 5, dtype=np.uint8).tobytes()
     b = np.random.default_rng(4).integers(0, 256, 2 * BS + 9, dtype=np.uint8).tobytes()
     es.put_object("b/o", a)
-    stale = [open(os.path.join(dirs[3], "b/o", f), "rb").read() for f in ("meta.json", "part.1")]
+    old_part = es.part_file(3, "b/o")
+    stale = [open(p, "rb").read() for p in (os.path.join(dirs[3], "b/o", "meta.json"), old_part)]
     es.put_object("b/o", b)
-    for f, raw in zip(("meta.json", "part.1"), stale):  # disk 3 rolled back to the old version
-        open(os.path.join(dirs[3], "b/o", f), "wb").write(raw)
+    os.makedirs(os.path.dirname(old_part), exist_ok=True)  # disk 3 rolled back to the old version
+    for p, raw in zip((os.path.join(dirs[3], "b/o", "meta.json"), old_part), stale):
+        open(p, "wb").write(raw)
     assert json.load(open(os.path.join(dirs[3], "b/o", "meta.json")))["size"] == len(a)
     assert es.get_object("b/o") == b

@@ -148,7 +148,7 @@ def main():
         get_rate("get")  # warm (stage allocation, page cache of the shard files)
         get_rate("get")
         for i in (0, 1):
-            os.remove(os.path.join(root, f"d{i}", "b/o", "part.1"))
+            os.remove(es.part_file(i, "b/o"))
         get_rate("get_2_data_lost")
         res["pcie_h2d_d2h_ceiling_GBps"] = 57.0
         res["note"] = ("put/get: whole-object wall-clock rate in object bytes/s; the PUT moves "
