@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define RSG_ABI_VERSION 5
+#define RSG_ABI_VERSION 6
 #define RSG_MAX_TOTAL_SHARDS 256 /* galois_8::Field::ORDER, erasure.rs:72 */
 #define RSG_DIGEST_BYTES 32      /* HighwayHash-256 */
 
@@ -112,6 +112,27 @@ typedef enum rsg_record_engine {
 } rsg_record_engine;
 int rsg_set_record_engine(rsg_ctx *ctx, int engine);
 
+/* Kernel-choice knobs (no reference counterpart; ABI 6: tests and A/B runs).
+ * The library runs its defaults; nothing in the process environment changes
+ * them (the RSG_* variables are read only by measurement builds compiled with
+ * RSG_MEASUREMENT_BUILD).  rsg_set_tuning(name, value) sets one knob for the
+ * whole process (every context): value NULL = that knob's default, name NULL
+ * = every knob's default; an unknown name or a value the knob does not take is
+ * RSG_ERR_INVALID_ARG and changes nothing.  Launches already queued keep the
+ * setting they were made with.  Every setting produces identical bytes and
+ * statuses; only the kernel (and its speed) differs.  rsg_get_tuning writes
+ * the knob's current value (NUL-terminated, at most cap bytes).  Knobs (value
+ * syntax): RSG_FUSED, RSG_LOST_DISK_FAST, RSG_ZERO_COPY, RSG_ROLLED,
+ * RSG_HASH_COPY, RSG_FUSED_SPW1, RSG_DECODE_NET, RSG_HASH_UNAL, RSG_GET_CACHED
+ * (0|1); RSG_VEC_BLOCK (0|64|256); RSG_VEC_OCC (-1..8); RSG_HASH_DEPTH (1..3);
+ * RSG_FUSED_KIND (auto|packed|ring|dma|wide2|wide4|split2|split4);
+ * RSG_ENC_PRIO, RSG_DMA_PRIO, RSG_DMA_NT (0..3); RSG_DMA_EW (2|4);
+ * RSG_DMA_SPW (4|8); RSG_NET12_RD (2; 4 only in measurement builds, whose
+ * library carries that A/B kernel form).  INTEGRATION.md lists what each
+ * selects. */
+int rsg_set_tuning(const char *name, const char *value);
+int rsg_get_tuning(const char *name, char *out, size_t cap);
+
 /* Fault injection, tests only (no reference counterpart; ABI 5): sub-batch
  * `index` of every later rsg_encode_batch_host_submit on this context fails
  * to enqueue with RSG_ERR_DEVICE (-1, the default: never).  Lets the tests
@@ -175,7 +196,13 @@ int rsg_verify_batch_dev(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t n,
 int rsg_hash_batch_dev(rsg_ctx *ctx, int algo, const uint8_t *d_data, size_t len, size_t stride,
                        size_t n, uint8_t *d_out, void *stream);
 
-/* GET-side engine, batched (RustfsCodecDecodeEngine::reconstruct_into,
+/* DEPRECATED since ABI 6 (kept so ABI-4 bindings stay valid; nothing in this
+ * repository calls it): use rsg_decode_records_into_dev, the form the
+ * reference's GET has — write_data_blocks writes from the per-shard buffers
+ * (decode.rs:1390), so copying every present data shard into one block buffer
+ * is work the reference does not do, and at RS(12,4) this form runs at a third
+ * of the HBM roofline (records 2 mod 8 copied to 8-aligned rows).
+ * GET-side engine, batched, gather form (RustfsCodecDecodeEngine::reconstruct_into,
  * bridge.rs:274-307, with BitrotReader's verify-before-use, bitrot.rs:227-247).
  * Shard i of n stripes is resident on the device in BitrotWriter layout:
  * record s at d_files[i] + s*(32+shard_len) = [32-byte digest][shard_len bytes]
@@ -204,8 +231,10 @@ int rsg_decode_records_dev(rsg_ctx *ctx, int k, int m, size_t shard_len, size_t 
  * d_targets: k device slots, one per data shard, each at least
  * (n-1)*target_stride + shard_len bytes (target_stride >= shard_len;
  * target_stride = k*shard_len with d_targets[i] = base + i*shard_len gives the
- * contiguous block layout); a slot range overlapping a source record file is
- * RSG_ERR_INVALID_ARG.  With every data file present the call only verifies
+ * contiguous block layout); a slot range overlapping a source record file, or
+ * two slots with a stripe window in common (some s, s' with
+ * [d_targets[i] + s*target_stride, +shard_len) and [d_targets[j] +
+ * s'*target_stride, +shard_len) sharing a byte), is RSG_ERR_INVALID_ARG.  With every data file present the call only verifies
  * the k data records of each stripe (parity is read for a stripe only if one of
  * its data records is rotten).  h_src (host, optional, k*n bytes, [shard][stripe]):
  * 1 where data shard i of stripe s is served from its record, 0 where it was
@@ -215,8 +244,9 @@ int rsg_decode_records_into_dev(rsg_ctx *ctx, int k, int m, size_t shard_len, si
                                 uint8_t *const *d_targets, size_t target_stride, uint8_t *h_src,
                                 int *h_status, void *stream);
 
-/* Asynchronous GET (ABI 5): either form — d_out (gather) or d_targets +
- * target_stride (in place), exactly one non-NULL — queued on `stream` with a
+/* Asynchronous GET (ABI 5): either form — d_out (gather, deprecated as
+ * rsg_decode_records_dev) or d_targets + target_stride (in place), exactly one
+ * non-NULL — queued on `stream` with a
  * ticket returned at once, so a caller decoding many batches (decode.rs's
  * pipeline, decode.rs:1702-1968) overlaps one batch's status handling with the
  * next batch's kernels.  rsg_poll / rsg_wait complete it (the same tickets as

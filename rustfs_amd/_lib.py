@@ -63,8 +63,18 @@ EXPORTED = (
     "rsg_decode_records_dev", "rsg_heal_records_dev", "rsg_bitrot_verify_dev",
     "rsg_encode_batch_host_submit", "rsg_poll", "rsg_wait", "rsg_set_kernel_timing", "rsg_last_kernel_ms",
     "rsg_set_record_engine", "rsg_decode_records_into_dev", "rsg_decode_records_submit",
-    "rsg_heal_records_submit", "rsg_test_fail_subbatch",
+    "rsg_heal_records_submit", "rsg_test_fail_subbatch", "rsg_set_tuning", "rsg_get_tuning",
 )
+
+# Kernel-choice knobs (rsg_set_tuning, include/rsgpu.h) and their defaults:
+# set only through the ABI (the production library ignores RSG_* variables).
+TUNING_DEFAULTS = {
+    "RSG_FUSED": "1", "RSG_LOST_DISK_FAST": "1", "RSG_ZERO_COPY": "1", "RSG_VEC_BLOCK": "0",
+    "RSG_VEC_OCC": "-1", "RSG_ROLLED": "0", "RSG_HASH_COPY": "0", "RSG_HASH_DEPTH": "2",
+    "RSG_FUSED_KIND": "auto", "RSG_FUSED_SPW1": "0", "RSG_ENC_PRIO": "0", "RSG_DMA_EW": "2",
+    "RSG_DMA_NT": "3", "RSG_DMA_SPW": "8", "RSG_DMA_PRIO": "2", "RSG_DECODE_NET": "1",
+    "RSG_NET12_RD": "2", "RSG_HASH_UNAL": "1", "RSG_GET_CACHED": "1",
+}
 
 
 class RsgError(IOError):
@@ -130,6 +140,8 @@ def load():
         L.rsg_last_kernel_ms.argtypes = [P, ctypes.POINTER(ctypes.c_float)]
         L.rsg_set_record_engine.argtypes = [P, I]
         L.rsg_test_fail_subbatch.argtypes = [P, I]
+        L.rsg_set_tuning.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        L.rsg_get_tuning.argtypes = [ctypes.c_char_p, ctypes.c_char_p, S]
         _lib = L
         return L
 
@@ -151,6 +163,41 @@ def check(code: int, context: str = "") -> None:
     if code in (RSG_ERR_INCONSISTENT_SOURCES, RSG_ERR_BITROT_MISMATCH):
         raise InvalidDataError(code, context)
     raise RsgError(code, context)
+
+
+def get_tuning(name: str) -> str:
+    """A kernel-choice knob's current value (rsg_get_tuning)."""
+    buf = ctypes.create_string_buffer(32)
+    check(load().rsg_get_tuning(name.encode(), buf, len(buf)), f"rsg_get_tuning({name})")
+    return buf.value.decode()
+
+
+def set_tuning(name: str | None, value: str | None) -> None:
+    """Set one knob process-wide (value None: its default; name None: every
+    knob's default) through rsg_set_tuning."""
+    check(load().rsg_set_tuning(name.encode() if name is not None else None,
+                                str(value).encode() if value is not None else None),
+          f"rsg_set_tuning({name}={value})")
+
+
+class tuned:
+    """`with tuned(RSG_DECODE_NET="0"): ...` — knobs set for the block, every
+    one of them back to its previous value afterwards (tests, A/B runs)."""
+
+    def __init__(self, **knobs):
+        self.knobs = knobs
+        self.saved = {}
+
+    def __enter__(self):
+        for k, v in self.knobs.items():
+            self.saved[k] = get_tuning(k)
+            set_tuning(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.saved.items():
+            set_tuning(k, v)
+        return False
 
 
 class Context:

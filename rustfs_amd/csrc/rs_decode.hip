@@ -1,7 +1,9 @@
-// rs_decode.hip — the one-pass GET / heal kernel (k_decode_records_dma) and
-// its launchers, in its own translation unit so its instantiations (four
-// survivor counts x present-file counts x heal targets) compile in parallel
-// with rs_kernels.hip.
+// rs_decode.hip — the one-pass GET / heal kernel with run-time coefficient
+// tables (k_decode_records_dma) and its launchers.  Compiled once per survivor
+// count C = 1..16 with RSG_DECODE_C=C (Makefile: that part instantiates the
+// C-survivor kernels, every present-file count and heal target count, and
+// exports launch_get_tab_C), and once without it (the dispatch below), so the
+// instantiations build in parallel.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -13,7 +15,7 @@ namespace rsg {
 
 // ---------------------------------------------------------------------------
 // One-pass degraded GET (rsg_decode_records_dev, a data disk lost) for
-// RS(k, m) with k in {2, 4, 8, 16} and m <= 4: every present record of G
+// RS(k, m) with k <= 16 and m <= 4: every present record of G
 // stripes is verified, the missing data shards rebuilt from the first C = k
 // present (survivors), the present data shards copied through and the
 // surplus parity compared with its re-derived value — reading each present
@@ -44,7 +46,7 @@ namespace rsg {
 // of the latency-bound hash chains instead of queueing behind them (RS(8,4),
 // n = 4096: GET 2 lost 2.44 -> 2.18 ms, heal 1.92 -> 1.69 ms;
 // profiles/r02/ab_prio/).  Tuning::get_prio overrides it for A/B runs.
-static uint32_t dma_prio() { return (uint32_t)tuning().get_prio; }
+[[maybe_unused]] static uint32_t dma_prio() { return (uint32_t)tuning().get_prio; }
 
 template <int NF, int G, int TH = 0>
 struct GetShape : RecRing<NF, G, TH> {
@@ -65,6 +67,7 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_re
     __shared__ __attribute__((aligned(16))) uint8_t ring[D * L::DSLOT];
     __shared__ __attribute__((aligned(16))) uint8_t tabs[C * RM * 32];
     __shared__ __attribute__((aligned(16))) uint8_t trow[TH ? 2 * L::TSLOT : 16];
+    static_assert(D * L::DSLOT + C * RM * 32 + (TH ? 2 * L::TSLOT : 16) <= 160 * 1024, "the ring fits the LDS");
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     const uint64_t n = h.n;
     const uint32_t steps = p.units;
@@ -160,10 +163,6 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_re
     records_hash_wave<NF, G>(h, p.wave_prio, ring, wave, steps, s0);
 }
 
-static_assert(dma::D * (get_group(16) / 2) * 19 * dma::IP + 16 * 4 * 32 + 2 * 4 * 4 * dma::PP <= 160 * 1024,
-              "RS(16,4) one-pass ring fits the LDS");
-static_assert(dma::D * (get_group(8) / 2) * 11 * dma::IP + 8 * 4 * 32 <= 160 * 1024, "RS(8,4) ring fits the LDS");
-
 template <int C, int NF, int G, int TH = 0>
 static void launch_get(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
     hipLaunchKernelGGL((k_decode_records_dma<C, NF, G, TH>), dim3((uint32_t)blocks),
@@ -185,12 +184,17 @@ static bool launch_get_nf(int nf, uint64_t n_stripes, const GfApplyParams& p, co
     }
 }
 
-template <int C, int G>
-static bool launch_get_th(int nf, int th, uint64_t n_stripes, const GfApplyParams& p, const HashParams& h,
-                          hipStream_t stream) {
-    if constexpr (C > 8) {  // no one-pass heal above 8 survivors (heal_dma_supported)
-        return th == 0 && launch_get_nf<C, G, 0, C>(nf, n_stripes, p, h, stream);
-    }
+using TabLaunch = bool (*)(int nf, int th, uint64_t n_stripes, const GfApplyParams& p, const HashParams& h,
+                           hipStream_t stream);
+
+#define RSG_DEC_CAT2(a, b) a##b
+#define RSG_DEC_CAT(a, b) RSG_DEC_CAT2(a, b)
+
+#ifdef RSG_DECODE_C
+// This part's survivor count: GET (th = 0) and heal (th = 1..4 targets).
+bool RSG_DEC_CAT(launch_get_tab_, RSG_DECODE_C)(int nf, int th, uint64_t n_stripes, const GfApplyParams& p,
+                                                const HashParams& h, hipStream_t stream) {
+    constexpr int C = RSG_DECODE_C, G = get_group(C);
     switch (th) {
         case 0: return launch_get_nf<C, G, 0, C>(nf, n_stripes, p, h, stream);
         case 1: return launch_get_nf<C, G, 1, C>(nf, n_stripes, p, h, stream);
@@ -200,62 +204,76 @@ static bool launch_get_th(int nf, int th, uint64_t n_stripes, const GfApplyParam
     }
     return false;
 }
+#else
+bool launch_get_tab_1(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_get_tab_2(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_get_tab_3(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_get_tab_4(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_get_tab_5(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_get_tab_6(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_get_tab_7(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_get_tab_8(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_get_tab_9(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_get_tab_10(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_get_tab_11(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_get_tab_12(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_get_tab_13(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_get_tab_14(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_get_tab_15(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_get_tab_16(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
 
 static bool launch_get_any(int k, int nf, int th, uint64_t n_stripes, const GfApplyParams& p, const HashParams& h,
                            hipStream_t stream) {
-    switch (k) {
-        case 2: return launch_get_th<2, get_group(2)>(nf, th, n_stripes, p, h, stream);
-        case 4: return launch_get_th<4, get_group(4)>(nf, th, n_stripes, p, h, stream);
-        case 6: return launch_get_th<6, get_group(6)>(nf, th, n_stripes, p, h, stream);
-        case 8: return launch_get_th<8, get_group(8)>(nf, th, n_stripes, p, h, stream);
-        case 10: return launch_get_th<10, get_group(10)>(nf, th, n_stripes, p, h, stream);
-        case 12: return launch_get_th<12, get_group(12)>(nf, th, n_stripes, p, h, stream);
-        case 16: return launch_get_th<16, get_group(16)>(nf, th, n_stripes, p, h, stream);
-    }
-    return false;
+    static const TabLaunch parts[16] = {launch_get_tab_1,  launch_get_tab_2,  launch_get_tab_3,  launch_get_tab_4,
+                                        launch_get_tab_5,  launch_get_tab_6,  launch_get_tab_7,  launch_get_tab_8,
+                                        launch_get_tab_9,  launch_get_tab_10, launch_get_tab_11, launch_get_tab_12,
+                                        launch_get_tab_13, launch_get_tab_14, launch_get_tab_15, launch_get_tab_16};
+    if (k < 1 || k > 16 || th < 0 || th > 4) return false;
+    return parts[k - 1](nf, th, n_stripes, p, h, stream);
 }
 
-// Geometries with a one-pass kernel: the data-shard counts of rustfs's
-// default sets and the powers of two (k in {2, 4, 6, 8, 10, 12, 16}: 4- to
-// 20-drive sets, storageclass.rs:24-31), m <= 4, any shard length (a ragged
-// last step, rs_records.h walk_tail).
+// Geometries with a one-pass kernel: every k <= 16 with m <= 4 — every set
+// of 2 to 16 drives (disks_layout.rs:25, MAX_ERASURE_SHARDS = 16 in
+// fileinfo.rs:38) at its default parity (storageclass.rs:24-31), the reduced-
+// redundancy class's one parity shard (storageclass.rs:99, 326-331) and
+// explicit EC:1..4 — any shard length (a ragged last step, rs_records.h
+// walk_tail).
 static bool one_pass_geometry(int k, int m, uint64_t shard_len) {
-    return (k == 2 || k == 4 || k == 6 || k == 8 || k == 10 || k == 12 || k == 16) && m >= 1 && m <= 4 &&
-           shard_len >= 1 && (shard_len + dma::CH - 1) / dma::CH <= 0xffffffffull;
+    return k >= 1 && k <= 16 && m >= 1 && m <= 4 && shard_len >= 1 &&
+           (shard_len + dma::CH - 1) / dma::CH <= 0xffffffffull;
 }
 
 bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len) {
     return one_pass_geometry(k, m, shard_len) && nf >= k && nf < k + m;
 }
 
-// One-pass heal for k <= 8: at RS(16,4) its four GF waves per workgroup (16
-// survivors x 4 rows each) set the pace and the two-pass path is faster
-// (n = 4096, one data + one parity disk: 2.14 ms one-pass, 1.98 ms two-pass;
-// profiles/r03/eng_ab/).
 bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len) {
-    return one_pass_geometry(k, m, shard_len) && k <= 8 && nf >= k && targets >= 1 && nf + targets <= k + m;
+    return one_pass_geometry(k, m, shard_len) && nf >= k && targets >= 1 && nf + targets <= k + m;
 }
 
-// RS(8,4) patterns with a compile-time XOR network (rs_decode_net.hip): the
-// launch's coefficient rows are matched byte for byte against the generated
-// table; a listed pattern runs k_decode_records_net, anything else the
-// run-time-table kernel above.  Tuning::decode_net = false (RSG_DECODE_NET=0)
+// The table kernel's heal against the two-pass path (GF pass, then verify +
+// target digests): one pass for k <= 8; above 8 survivors the workgroup holds
+// 4 stripes and its GF waves (k survivors x up to 4 rows each) set the pace —
+// at RS(16,4) two-pass is faster (n = 4096, one data + one parity disk: 2.14
+// ms one-pass, 1.98 ms two-pass; profiles/r03/eng_ab/).
+bool heal_table_preferred(int k) { return k <= 8; }
+
+// Patterns with a compile-time XOR network (RS(4,4), RS(6,4), RS(8,4):
+// rs_decode_net.hip; RS(10,4), RS(12,4): rs_decode_netq.hip): the launch's
+// coefficient rows are matched byte for byte against the generated table; a
+// listed pattern runs its network kernel, anything else the run-time-table
+// kernel above.  Tuning::decode_net = false (RSG_DECODE_NET=0)
 // keeps the table kernel for A/B runs.
 static bool launch_net_if_listed(int heal, int k, int m, int nf, const uint8_t* coef, uint64_t n_stripes,
                                  const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
     if (m != 4 || !coef || !tuning().decode_net || p.C != (uint32_t)k) return false;
     using Part = bool (*)(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
-    if (k == 16 || k == 12 || k == 10) {
-        const int pid = k == 16   ? records_net16_pattern(heal, nf, (int)p.R, (int)p.n_store, coef)
-                        : k == 12 ? records_net12_pattern(heal, nf, (int)p.R, (int)p.n_store, coef)
-                                  : records_net10_pattern(heal, nf, (int)p.R, (int)p.n_store, coef);
+    if (k == 12 || k == 10) {
+        const int pid = k == 12 ? records_net12_pattern(heal, nf, (int)p.R, (int)p.n_store, coef)
+                                : records_net10_pattern(heal, nf, (int)p.R, (int)p.n_store, coef);
         if (pid < 0) return false;
         const uint64_t blocks = (n_stripes + 3) / 4;
         if (blocks > 0x7fffffffull) return false;
-        static const Part parts16[RSG_NET_PARTS] = {launch_records_net16_part0, launch_records_net16_part1,
-                                                    launch_records_net16_part2, launch_records_net16_part3,
-                                                    launch_records_net16_part4, launch_records_net16_part5,
-                                                    launch_records_net16_part6, launch_records_net16_part7};
         static const Part parts12[RSG_NET_PARTS] = {launch_records_net12_part0, launch_records_net12_part1,
                                                     launch_records_net12_part2, launch_records_net12_part3,
                                                     launch_records_net12_part4, launch_records_net12_part5,
@@ -264,7 +282,7 @@ static bool launch_net_if_listed(int heal, int k, int m, int nf, const uint8_t* 
                                                     launch_records_net10_part2, launch_records_net10_part3,
                                                     launch_records_net10_part4, launch_records_net10_part5,
                                                     launch_records_net10_part6, launch_records_net10_part7};
-        return (k == 16 ? parts16 : k == 12 ? parts12 : parts10)[pid % RSG_NET_PARTS](pid, blocks, p, h, stream);
+        return (k == 12 ? parts12 : parts10)[pid % RSG_NET_PARTS](pid, blocks, p, h, stream);
     }
     if (k != 8 && k != 6 && k != 4) return false;
     const int pid = k == 8   ? records_net_pattern(heal, nf, (int)p.R, (int)p.n_store, coef)
@@ -296,15 +314,14 @@ static bool launch_net_if_listed(int heal, int k, int m, int nf, const uint8_t* 
 static bool dma_records_walkable(const HashParams& h) { return 5 * h.stripe_stride < (1ull << 32); }
 
 bool heal_one_pass_shape(int k, int m, int nf, int targets, uint64_t shard_len) {
-    return heal_dma_supported(k, m, nf, targets, shard_len) ||
-           ((k == 16 || k == 12 || k == 10) && m == 4 && tuning().decode_net && one_pass_geometry(k, m, shard_len) &&
-            nf >= k && targets >= 1 && nf + targets <= k + m);
+    return heal_dma_supported(k, m, nf, targets, shard_len);
 }
 
-// hipErrorNotSupported: no one-pass kernel for this pattern (RS(16,4) heal
-// not in the network table) — the caller takes the two-pass path.
+// hipErrorNotSupported: no network for this pattern and the table heal is not
+// wanted (neither forced nor preferred for k) — the caller takes the two-pass path.
 hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, int nf, int targets,
-                                   uint64_t shard_len, uint64_t n_stripes, const uint8_t* coef, hipStream_t stream) {
+                                   uint64_t shard_len, uint64_t n_stripes, const uint8_t* coef, bool any_table,
+                                   hipStream_t stream) {
     p.wave_prio = dma_prio();
     if (!heal_one_pass_shape(k, m, nf, targets, shard_len) || (int)p.C != k || n_stripes == 0 || p.R > 4 ||
         p.n_store != (uint32_t)targets || p.copy_mask || !dma_records_walkable(h) ||
@@ -314,7 +331,7 @@ hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, 
     p.byte_end = shard_len;
     h.n = n_stripes;
     if (launch_net_if_listed(1, k, m, nf, coef, n_stripes, p, h, stream)) return hipGetLastError();
-    if (!heal_dma_supported(k, m, nf, targets, shard_len)) return hipErrorNotSupported;
+    if (!any_table && !heal_table_preferred(k)) return hipErrorNotSupported;
     if (!launch_get_any(k, nf, targets, n_stripes, p, h, stream)) return hipErrorInvalidValue;
     return hipGetLastError();
 }
@@ -332,5 +349,6 @@ hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int k, int m
     if (!launch_get_any(k, nf, 0, n_stripes, p, h, stream)) return hipErrorInvalidValue;
     return hipGetLastError();
 }
+#endif  // RSG_DECODE_C
 
 }  // namespace rsg

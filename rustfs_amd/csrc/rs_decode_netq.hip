@@ -345,12 +345,14 @@ void launch_netq(uint64_t blocks, const GfApplyParams& p, const HashParams& h, h
     // 4-slot form); heal: its target rows do not fit two workgroups' LDS
     const dim3 block(64 * NetQShape<NF, TH>::WAVES);
     if constexpr (TH == 0) {
-        if (tuning().net12_rd == 2)
+        if (!RSG_MEASUREMENT_BUILD || tuning().net12_rd == 2)
             hipLaunchKernelGGL((RSG_NETQ_NAME(k_decode_records_, )<PID, NF, TH, false, 2>), dim3((uint32_t)blocks),
                                block, 0, stream, p, h);
+#if RSG_MEASUREMENT_BUILD  // the 4-slot A/B form
         else
             hipLaunchKernelGGL((RSG_NETQ_NAME(k_decode_records_, )<PID, NF, TH>), dim3((uint32_t)blocks), block, 0,
                                stream, p, h);
+#endif
     } else {
         hipLaunchKernelGGL((RSG_NETQ_NAME(k_decode_records_, )<PID, NF, TH>), dim3((uint32_t)blocks), block, 0,
                            stream, p, h);
@@ -423,13 +425,15 @@ hipError_t launch_encode_hash_net12(GfApplyParams p, HashParams h, uint64_t shar
     h.stripe_stride = p.stripe_stride;
     h.nbases = 12;
     for (int c = 0; c < 12; ++c) h.base[c] = p.base + p.in_off[c];
-    // two workgroups per CU on a 2-slot ring (RSG_NET12_RD=4: one, 4 slots)
-    if (tuning().net12_rd == 2)
+    // two workgroups per CU on a 2-slot ring (RSG_NET12_RD=4, measurement builds: one, 4 slots)
+    if (!RSG_MEASUREMENT_BUILD || tuning().net12_rd == 2)
         hipLaunchKernelGGL((k_decode_records_net12<kEncodePid, 12, 4, true, 2>),
                            dim3((uint32_t)((n_stripes + L::SPW - 1) / L::SPW)), dim3(64 * L::WAVES), 0, stream, p, h);
+#if RSG_MEASUREMENT_BUILD
     else
         hipLaunchKernelGGL((k_decode_records_net12<kEncodePid, 12, 4, true, 4>),
                            dim3((uint32_t)((n_stripes + L::SPW - 1) / L::SPW)), dim3(64 * L::WAVES), 0, stream, p, h);
+#endif
     return hipGetLastError();
 }
 

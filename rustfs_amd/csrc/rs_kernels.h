@@ -23,6 +23,13 @@ enum GfMode : uint32_t {
 // the environment (rsg::tuning(), first use: rsg_create) — never read per
 // call.  Production runs leave every variable unset and get the defaults
 // below, which are the measured-best shapes (DESIGN.md cites the A/B runs).
+// Measurement builds (`make MEASURE=1`, tools/ A/B runs): the RSG_* environment
+// variables select kernels, and the A/B-only kernel variants are compiled in.
+// The shipped library is built with 0.
+#ifndef RSG_MEASUREMENT_BUILD
+#define RSG_MEASUREMENT_BUILD 0
+#endif
+
 struct Tuning {
     bool fused = true;            // RSG_FUSED=0: encode, then a separate hash launch
     bool lost_disk_fast = true;   // RSG_LOST_DISK_FAST=0: general GET/heal order
@@ -40,7 +47,8 @@ struct Tuning {
     int dma_spw = 8;              // RSG_DMA_SPW=4: four stripes per fused DMA workgroup
     int get_prio = 2;             // RSG_DMA_PRIO=<0..3>: wave priorities of the one-pass GET/heal
     bool decode_net = true;       // RSG_DECODE_NET=0: run-time-table GF waves for every one-pass pattern
-    int net12_rd = 2;             // RSG_NET12_RD=4: RS(12,4) GET ring of 4 slots, one workgroup per CU (A/B)
+    int net12_rd = 2;             // RSG_NET12_RD=4: RS(12,4) / RS(10,4) GET ring of 4 slots, one workgroup per CU
+                                  // (A/B; its kernels exist in measurement builds only)
     bool hash_unal = true;        // RSG_HASH_UNAL=0: unaligned 8-byte loads for unaligned messages (A/B)
     bool get_cached = true;       // RSG_GET_CACHED=0: non-temporal output stores in the network GET/heal kernel
 };
@@ -133,11 +141,16 @@ bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len);
 hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int k, int m, int nf, uint64_t shard_len,
                                      uint64_t n_stripes, const uint8_t* coef, hipStream_t stream);
 // One-pass heal (k_decode_records_dma with target hashing), the same
-// geometries with k <= 8: nf present source files, `targets` absent target
-// files written with digests (nf + targets <= k + m).
+// geometries: nf present source files, `targets` absent target files written
+// with digests (nf + targets <= k + m).  A pattern with a compile-time network
+// runs it; otherwise the table kernel runs if `any_table` (a forced one-pass
+// engine) or the table heal is the faster path for k (heal_table_preferred),
+// else hipErrorNotSupported: the caller takes the two-pass path.
 bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len);
+bool heal_table_preferred(int k);
 hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, int nf, int targets,
-                                   uint64_t shard_len, uint64_t n_stripes, const uint8_t* coef, hipStream_t stream);
+                                   uint64_t shard_len, uint64_t n_stripes, const uint8_t* coef, bool any_table,
+                                   hipStream_t stream);
 
 // The one-pass GET/heal kernel with compile-time XOR networks
 // (rs_decode_net.hip, k_decode_records_net): RS(8,4) patterns of one or two
@@ -199,37 +212,22 @@ RSG_NET6_PART_DECL(5)
 RSG_NET6_PART_DECL(6)
 RSG_NET6_PART_DECL(7)
 #undef RSG_NET6_PART_DECL
-// RS(16,4) (rs_decode_net16.hip, k_decode_records_net16): the same for R x 16 rows
-int records_net16_pattern(int heal, int nf, int R, int n_store, const uint8_t* coef);
-#define RSG_NET16_PART_DECL(i)                                                                                 \
-    bool launch_records_net16_part##i(int pid, uint64_t blocks, const GfApplyParams& p, const HashParams& h, \
-                                      hipStream_t stream);
-RSG_NET16_PART_DECL(0)
-RSG_NET16_PART_DECL(1)
-RSG_NET16_PART_DECL(2)
-RSG_NET16_PART_DECL(3)
-RSG_NET16_PART_DECL(4)
-RSG_NET16_PART_DECL(5)
-RSG_NET16_PART_DECL(6)
-RSG_NET16_PART_DECL(7)
 // RS(12,4) (rs_decode_netq.hip, k_decode_records_net12): the same for R x 12 rows
 int records_net12_pattern(int heal, int nf, int R, int n_store, const uint8_t* coef);
-#define RSG_NET16_PART_DECL12(i)                                                                               \
+#define RSG_NET12_PART_DECL(i)                                                                               \
     bool launch_records_net12_part##i(int pid, uint64_t blocks, const GfApplyParams& p, const HashParams& h, \
                                       hipStream_t stream);
-RSG_NET16_PART_DECL12(0)
-RSG_NET16_PART_DECL12(1)
-RSG_NET16_PART_DECL12(2)
-RSG_NET16_PART_DECL12(3)
-RSG_NET16_PART_DECL12(4)
-RSG_NET16_PART_DECL12(5)
-RSG_NET16_PART_DECL12(6)
-RSG_NET16_PART_DECL12(7)
-#undef RSG_NET16_PART_DECL12
-#undef RSG_NET16_PART_DECL
-// One-pass heal possible for this shape: the table kernel (k <= 8) or, for
-// RS(16,4), a listed network pattern (decided at launch: RSG_ERR_UNSUPPORTED
-// from the launcher then means "use the two-pass path").
+RSG_NET12_PART_DECL(0)
+RSG_NET12_PART_DECL(1)
+RSG_NET12_PART_DECL(2)
+RSG_NET12_PART_DECL(3)
+RSG_NET12_PART_DECL(4)
+RSG_NET12_PART_DECL(5)
+RSG_NET12_PART_DECL(6)
+RSG_NET12_PART_DECL(7)
+#undef RSG_NET12_PART_DECL
+// One-pass heal possible for this shape (the table kernel takes every k <=
+// 16, m <= 4; which kernel runs is decided at launch).
 bool heal_one_pass_shape(int k, int m, int nf, int targets, uint64_t shard_len);
 hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                     hipStream_t stream);

@@ -21,9 +21,13 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <atomic>
+#include <deque>
+#include <mutex>
 #include <string>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "rs_device.h"
 #include "gf_bitslice.h"
@@ -384,9 +388,6 @@ constexpr int fused_spw() {
 // stripe's first digest words, bit 4 raises the hasher waves' issue priority
 // (s_setprio 1), bit 5 the encoder waves'.  In the shipped library every
 // ablation bit compiles to 0.
-#ifndef RSG_MEASUREMENT_BUILD
-#define RSG_MEASUREMENT_BUILD 0
-#endif
 template <int C, int R, int SPW, int ABLATE_ = 0>
 __global__ __launch_bounds__(64 * (SPW + (SPW * (C + R) + 15) / 16))
 __attribute__((amdgpu_waves_per_eu(R == 1 ? 4 : C <= 8 ? 7 : C <= 12 ? 5 : 4)))
@@ -1156,46 +1157,165 @@ void k_encode_hash_ring(const GfApplyParams p, const HashParams h, const uint32_
 // ---------------------------------------------------------------------------
 // Launchers.
 
-const Tuning& tuning() {
-    static const Tuning t = [] {
-        Tuning v;
-        auto num = [](const char* name, int def, int lo, int hi) {
-            const char* e = getenv(name);
-            if (!e || !*e) return def;
-            const int x = atoi(e);
-            return (x < lo || x > hi) ? def : x;
-        };
-        auto flag = [](const char* name, bool def) {
-            const char* e = getenv(name);
-            return (e && *e) ? e[0] != '0' : def;
-        };
-        v.fused = flag("RSG_FUSED", true);
-        v.lost_disk_fast = flag("RSG_LOST_DISK_FAST", true);
-        v.zero_copy = flag("RSG_ZERO_COPY", true);
-        v.vec_block = num("RSG_VEC_BLOCK", 0, 64, 256);
-        if (v.vec_block != 0 && v.vec_block != 256) v.vec_block = 64;
-        v.vec_occ = num("RSG_VEC_OCC", -1, 0, 8);
-        v.rolled = flag("RSG_ROLLED", false);
-        v.hash_direct_copy = flag("RSG_HASH_COPY", false);
-        v.hash_depth = num("RSG_HASH_DEPTH", 2, 1, 3);
-        if (const char* e = getenv("RSG_FUSED_KIND")) {
-            const std::string k(e);
-            v.fused_kind = k == "packed" ? 1 : k == "ring" ? 2 : k == "dma" ? 3 : k == "wide2" ? 4 : k == "wide4" ? 5 :
-                          k == "split2" ? 6 : k == "split4" ? 7 : 0;
-        }
-        v.fused_spw1 = flag("RSG_FUSED_SPW1", false);
-        v.enc_prio = num("RSG_ENC_PRIO", 0, 0, 3);
-        v.dma_ew = num("RSG_DMA_EW", 2, 2, 4) == 4 ? 4 : 2;
-        v.dma_nt = num("RSG_DMA_NT", 3, 0, 3);
-        v.dma_spw = num("RSG_DMA_SPW", 8, 4, 8) == 4 ? 4 : 8;
-        v.get_prio = num("RSG_DMA_PRIO", 2, 0, 3);
-        v.decode_net = flag("RSG_DECODE_NET", true);
-        v.net12_rd = num("RSG_NET12_RD", 2, 2, 4) == 4 ? 4 : 2;
-        v.hash_unal = flag("RSG_HASH_UNAL", true);
-        v.get_cached = flag("RSG_GET_CACHED", true);
-        return v;
-    }();
+// Kernel-choice knobs (Tuning, rs_kernels.h).  The library runs the
+// defaults; a knob changes only through rsg_set_tuning (tests and A/B runs,
+// set_tuning below) or — in measurement builds only (RSG_MEASUREMENT_BUILD) —
+// from its RSG_* environment variable, read once.  A production process's
+// environment cannot change which kernels run.  Every setting is published as
+// a new immutable snapshot (launches in flight keep reading the one they
+// loaded); snapshots live for the process.
+namespace {
+
+// name -> the knob's field; false for an unknown name or a value out of range
+bool set_knob(Tuning& v, const std::string& name, const char* value) {
+    if (!value || !*value) return false;
+    const std::string s(value);
+    char* endp = nullptr;
+    const long x = strtol(value, &endp, 10);
+    const bool is_num = endp && *endp == '\0';
+    auto flag = [&](bool& f) {
+        if (s != "0" && s != "1") return false;
+        f = s == "1";
+        return true;
+    };
+    auto num = [&](int& f, int lo, int hi) {
+        if (!is_num || x < lo || x > hi) return false;
+        f = (int)x;
+        return true;
+    };
+    auto one_of = [&](int& f, int a, int b, int c = -1000) {
+        if (!is_num || (x != a && x != b && x != c)) return false;
+        f = (int)x;
+        return true;
+    };
+    if (name == "RSG_FUSED") return flag(v.fused);
+    if (name == "RSG_LOST_DISK_FAST") return flag(v.lost_disk_fast);
+    if (name == "RSG_ZERO_COPY") return flag(v.zero_copy);
+    if (name == "RSG_VEC_BLOCK") return one_of(v.vec_block, 0, 64, 256);
+    if (name == "RSG_VEC_OCC") return num(v.vec_occ, -1, 8);
+    if (name == "RSG_ROLLED") return flag(v.rolled);
+    if (name == "RSG_HASH_COPY") return flag(v.hash_direct_copy);
+    if (name == "RSG_HASH_DEPTH") return num(v.hash_depth, 1, 3);
+    if (name == "RSG_FUSED_KIND") {
+        static const char* const kinds[] = {"auto", "packed", "ring", "dma", "wide2", "wide4", "split2", "split4"};
+        for (int i = 0; i < 8; ++i)
+            if (s == kinds[i]) {
+                v.fused_kind = i;
+                return true;
+            }
+        return false;
+    }
+    if (name == "RSG_FUSED_SPW1") return flag(v.fused_spw1);
+    if (name == "RSG_ENC_PRIO") return num(v.enc_prio, 0, 3);
+    if (name == "RSG_DMA_EW") return one_of(v.dma_ew, 2, 4);
+    if (name == "RSG_DMA_NT") return num(v.dma_nt, 0, 3);
+    if (name == "RSG_DMA_SPW") return one_of(v.dma_spw, 4, 8);
+    if (name == "RSG_DMA_PRIO") return num(v.get_prio, 0, 3);
+    if (name == "RSG_DECODE_NET") return flag(v.decode_net);
+    if (name == "RSG_NET12_RD") return RSG_MEASUREMENT_BUILD ? one_of(v.net12_rd, 2, 4) : one_of(v.net12_rd, 2, 2);
+    if (name == "RSG_HASH_UNAL") return flag(v.hash_unal);
+    if (name == "RSG_GET_CACHED") return flag(v.get_cached);
+    return false;
+}
+
+// the knob's current setting in set_knob's syntax; false for an unknown name
+bool knob_value(const Tuning& v, const std::string& name, std::string& out) {
+    auto b = [&](bool f) { out = f ? "1" : "0"; return true; };
+    auto i = [&](int x) { out = std::to_string(x); return true; };
+    if (name == "RSG_FUSED") return b(v.fused);
+    if (name == "RSG_LOST_DISK_FAST") return b(v.lost_disk_fast);
+    if (name == "RSG_ZERO_COPY") return b(v.zero_copy);
+    if (name == "RSG_VEC_BLOCK") return i(v.vec_block);
+    if (name == "RSG_VEC_OCC") return i(v.vec_occ);
+    if (name == "RSG_ROLLED") return b(v.rolled);
+    if (name == "RSG_HASH_COPY") return b(v.hash_direct_copy);
+    if (name == "RSG_HASH_DEPTH") return i(v.hash_depth);
+    if (name == "RSG_FUSED_KIND") {
+        static const char* const kinds[] = {"auto", "packed", "ring", "dma", "wide2", "wide4", "split2", "split4"};
+        out = kinds[v.fused_kind >= 0 && v.fused_kind < 8 ? v.fused_kind : 0];
+        return true;
+    }
+    if (name == "RSG_FUSED_SPW1") return b(v.fused_spw1);
+    if (name == "RSG_ENC_PRIO") return i(v.enc_prio);
+    if (name == "RSG_DMA_EW") return i(v.dma_ew);
+    if (name == "RSG_DMA_NT") return i(v.dma_nt);
+    if (name == "RSG_DMA_SPW") return i(v.dma_spw);
+    if (name == "RSG_DMA_PRIO") return i(v.get_prio);
+    if (name == "RSG_DECODE_NET") return b(v.decode_net);
+    if (name == "RSG_NET12_RD") return i(v.net12_rd);
+    if (name == "RSG_HASH_UNAL") return b(v.hash_unal);
+    if (name == "RSG_GET_CACHED") return b(v.get_cached);
+    return false;
+}
+
+#if RSG_MEASUREMENT_BUILD
+const char* const kKnobs[] = {"RSG_FUSED", "RSG_LOST_DISK_FAST", "RSG_ZERO_COPY", "RSG_VEC_BLOCK", "RSG_VEC_OCC",
+                              "RSG_ROLLED", "RSG_HASH_COPY", "RSG_HASH_DEPTH", "RSG_FUSED_KIND", "RSG_FUSED_SPW1",
+                              "RSG_ENC_PRIO", "RSG_DMA_EW", "RSG_DMA_NT", "RSG_DMA_SPW", "RSG_DMA_PRIO",
+                              "RSG_DECODE_NET", "RSG_NET12_RD", "RSG_HASH_UNAL", "RSG_GET_CACHED"};
+#endif
+
+std::mutex g_tuning_mu;
+std::atomic<const Tuning*> g_tuning{nullptr};
+std::deque<Tuning>& tuning_store() {
+    static std::deque<Tuning> d;  // every published snapshot (a deque never moves its elements)
+    return d;
+}
+
+const Tuning* publish(const Tuning& v) {  // under g_tuning_mu
+    tuning_store().push_back(v);
+    const Tuning* t = &tuning_store().back();
+    g_tuning.store(t, std::memory_order_release);
     return t;
+}
+
+Tuning initial_tuning() {
+    Tuning v;  // the defaults (rs_kernels.h)
+#if RSG_MEASUREMENT_BUILD
+    for (const char* name : kKnobs)
+        if (const char* e = getenv(name)) (void)set_knob(v, name, e);  // an invalid value keeps the default
+#endif
+    return v;
+}
+
+}  // namespace
+
+const Tuning& tuning() {
+    if (const Tuning* t = g_tuning.load(std::memory_order_acquire)) return *t;
+    std::lock_guard<std::mutex> lk(g_tuning_mu);
+    if (const Tuning* t = g_tuning.load(std::memory_order_acquire)) return *t;
+    return *publish(initial_tuning());
+}
+
+// rsg_set_tuning: name NULL = every knob back to its default; value NULL =
+// this knob back to its default.  RSG_ERR_INVALID_ARG (1) for an unknown
+// name or a value the knob does not take; nothing changes then.
+int set_tuning(const char* name, const char* value) {
+    (void)tuning();
+    std::lock_guard<std::mutex> lk(g_tuning_mu);
+    if (!name) {
+        publish(Tuning{});
+        return 0;
+    }
+    const std::string nm(name);
+    Tuning v = *g_tuning.load(std::memory_order_acquire);
+    if (!value) {  // this knob's default
+        std::string d;
+        if (!knob_value(Tuning{}, nm, d) || !set_knob(v, nm, d.c_str())) return 1;
+        publish(v);
+        return 0;
+    }
+    if (!set_knob(v, nm, value)) return 1;
+    publish(v);
+    return 0;
+}
+
+// rsg_get_tuning: the knob's current setting (NUL-terminated in out[cap]).
+int get_tuning(const char* name, char* out, size_t cap) {
+    std::string v;
+    if (!name || !out || !knob_value(tuning(), name, v) || v.size() + 1 > cap) return 1;
+    memcpy(out, v.c_str(), v.size() + 1);
+    return 0;
 }
 
 using GfKernel = void (*)(const GfApplyParams);

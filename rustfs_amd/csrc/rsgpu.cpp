@@ -25,6 +25,11 @@
 #include "../../include/rsgpu.h"
 #include "rs_kernels.h"
 
+namespace rsg {  // the kernel-choice knobs (rs_kernels.hip): 0 = ok, 1 = unknown name / bad value
+int set_tuning(const char* name, const char* value);
+int get_tuning(const char* name, char* out, size_t cap);
+}  // namespace rsg
+
 namespace {
 
 // --------------------------------------------------------------------------
@@ -757,7 +762,6 @@ int rsg_create(int device, rsg_ctx** out) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return RSG_ERR_NO_DEVICE;
     if (hipSetDevice(device) != hipSuccess) return RSG_ERR_NO_DEVICE;
-    (void)rsg::tuning();  // A/B knobs resolved once, before any launch
     auto* c = new rsg_ctx();
     c->device = device;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -1699,8 +1703,9 @@ int launch_heal_one_pass(RecJob& j, const std::vector<int>& files, const std::ve
         h.flag_base[f] = j.d_flags() + (size_t)files[f] * j.n;
     }
     j.sc->tmark(j.s);  // the timing hook opens after the host-side preparation
+    const bool any_table = j.ctx->record_engine.load() == RSG_RECORD_ENGINE_ONE_PASS;  // forced: the table heal too
     const hipError_t e = rsg::launch_heal_records_dma(p, h, k, j.m, (int)files.size(), (int)targets.size(), j.S,
-                                                      j.n, coef.data(), j.s);
+                                                      j.n, coef.data(), any_table, j.s);
     if (e == hipErrorNotSupported) j.sc->tunmark();
     return e == hipErrorNotSupported ? RSG_ERR_UNSUPPORTED : hip_status(e);  // unsupported: nothing launched
 }
@@ -1793,7 +1798,7 @@ int heal_begin(RecJob& j) {
     for (int i : tg_idx) one_pass = one_pass && !j.files[i];
     if (one_pass) {
         st = launch_heal_one_pass(j, all_idx, tg_idx);  // opens the timing mark when it launches
-        if (st == RSG_ERR_UNSUPPORTED) {  // RS(16,4) pattern without a network: the two-pass path
+        if (st == RSG_ERR_UNSUPPORTED) {  // no network, table heal not preferred for k: the two-pass path
             one_pass = false;
             j.any_verify = false;
         } else if (st) {
@@ -1925,6 +1930,23 @@ bool spans_overlap(const uint8_t* a, uint64_t la, const uint8_t* b, uint64_t lb)
     return (uintptr_t)a < (uintptr_t)b + lb && (uintptr_t)b < (uintptr_t)a + la;
 }
 
+// Slots a and b of the in-place GET, stripes at a + s*ts and b + s'*ts (s, s'
+// < n), each shard_len bytes: true if some pair of their stripe windows shares
+// a byte (two rebuilt shards would be written over each other).  The block
+// layout (slot i = base + i*shard_len, ts = k*shard_len) interleaves the
+// slots without a collision.
+bool slot_windows_collide(const uint8_t* a, const uint8_t* b, uint64_t ts, uint64_t shard_len, uint64_t n) {
+    const __int128 d = (__int128)(uintptr_t)b - (__int128)(uintptr_t)a;
+    const __int128 t = (__int128)ts;
+    __int128 q = d / t;
+    if (d % t != 0 && d < 0) q -= 1;  // floor
+    for (__int128 c = q; c <= q + 1; ++c) {  // the two stripe offsets nearest to d
+        const __int128 diff = d - c * t;
+        if ((diff < 0 ? -diff : diff) < (__int128)shard_len && (c < 0 ? -c : c) <= (__int128)n - 1) return true;
+    }
+    return false;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1952,6 +1974,11 @@ int rsg_decode_records_submit(rsg_ctx* ctx, int k, int m, size_t shard_len, size
             if (!d_targets[i]) return RSG_ERR_INVALID_ARG;
             for (int f = 0; f < k + m && span; ++f)
                 if (d_files[f] && spans_overlap(d_targets[i], span, d_files[f], (uint64_t)n * rec))
+                    return RSG_ERR_INVALID_ARG;
+            // two slots whose stripe windows share bytes (one buffer passed
+            // as several slots): rebuilt shards would overwrite each other
+            for (int j = 0; j < i && n && shard_len; ++j)
+                if (slot_windows_collide(d_targets[j], d_targets[i], target_stride, shard_len, n))
                     return RSG_ERR_INVALID_ARG;
         }
     }
@@ -2018,6 +2045,14 @@ int rsg_test_fail_subbatch(rsg_ctx* ctx, int index) {
     if (!ctx || index < -1) return RSG_ERR_INVALID_ARG;
     ctx->fail_subbatch.store(index);
     return RSG_OK;
+}
+
+int rsg_set_tuning(const char* name, const char* value) {
+    return rsg::set_tuning(name, value) ? RSG_ERR_INVALID_ARG : RSG_OK;
+}
+
+int rsg_get_tuning(const char* name, char* out, size_t cap) {
+    return rsg::get_tuning(name, out, cap) ? RSG_ERR_INVALID_ARG : RSG_OK;
 }
 
 int rsg_set_record_engine(rsg_ctx* ctx, int engine) {

@@ -400,8 +400,9 @@ class Erasure:
 
     def decode_records_batch(self, files: Sequence, shard_len: int, n: int, verify_surplus: bool = True,
                              algo: int = _lib.RSG_HASH_HIGHWAY256S, out=None, stream=None):
-        """GET engine, gather form (rsg_decode_records_dev): `files[i]` is a cuda
-        uint8 tensor holding shard i's n BitrotWriter records ([32-byte
+        """GET engine, gather form (rsg_decode_records_dev, deprecated since ABI
+        6: decode_records_into_batch is the reference's form): `files[i]` is a
+        cuda uint8 tensor holding shard i's n BitrotWriter records ([32-byte
         digest][shard_len]) or None.  Returns (data (n, k*shard_len) tensor,
         per-stripe status list)."""
         import torch

@@ -33,7 +33,7 @@ def test_exported_symbols_have_c_linkage():
 
 
 def test_abi_version(rsgpu_lib):
-    assert rsgpu_lib.rsg_abi_version() == 5
+    assert rsgpu_lib.rsg_abi_version() == 6
 
 
 @pytest.mark.parametrize("k,m", [(1, 1), (2, 2), (3, 1), (4, 2), (6, 3), (8, 4), (12, 4), (16, 4), (10, 10),
@@ -78,3 +78,52 @@ def test_null_args_rejected_without_device(rsgpu_lib):
     assert rsgpu_lib.rsg_encode(None, 4, 2, 16, None) == _lib.RSG_ERR_INVALID_ARG
     assert rsgpu_lib.rsg_device_count(None) == _lib.RSG_ERR_INVALID_ARG
     rsgpu_lib.rsg_destroy(None)  # no-op
+
+
+def test_tuning_knobs_default_and_settable(rsgpu_lib):
+    """rsg_get_tuning reports every knob's default; rsg_set_tuning changes one
+    knob, refuses unknown names and values out of range without changing
+    anything, and NULL value / NULL name restore the defaults (no GPU)."""
+    from rustfs_amd import _lib
+    for k, v in _lib.TUNING_DEFAULTS.items():
+        assert _lib.get_tuning(k) == v, k
+    with _lib.tuned(RSG_DECODE_NET="0", RSG_FUSED_KIND="dma", RSG_HASH_DEPTH="3"):
+        assert (_lib.get_tuning("RSG_DECODE_NET"), _lib.get_tuning("RSG_FUSED_KIND"),
+                _lib.get_tuning("RSG_HASH_DEPTH")) == ("0", "dma", "3")
+    assert _lib.get_tuning("RSG_DECODE_NET") == "1" and _lib.get_tuning("RSG_FUSED_KIND") == "auto"
+    # RSG_NET12_RD=4: its kernels are compiled into measurement builds only
+    for name, bad in (("RSG_NET12_RD", b"3"), ("RSG_NET12_RD", b"4"), ("RSG_DECODE_NET", b"yes"), ("RSG_HASH_DEPTH", b"4"),
+                      ("RSG_FUSED_KIND", b"fast"), ("RSG_NO_SUCH_KNOB", b"1")):
+        assert rsgpu_lib.rsg_set_tuning(name.encode(), bad) == _lib.RSG_ERR_INVALID_ARG
+    assert _lib.get_tuning("RSG_HASH_DEPTH") == "2"
+    _lib.set_tuning("RSG_HASH_DEPTH", "3")
+    _lib.set_tuning("RSG_HASH_DEPTH", None)
+    assert _lib.get_tuning("RSG_HASH_DEPTH") == "2"
+    _lib.set_tuning("RSG_VEC_OCC", "4")
+    _lib.set_tuning(None, None)
+    assert _lib.get_tuning("RSG_VEC_OCC") == "-1"
+    buf = ctypes.create_string_buffer(2)
+    assert rsgpu_lib.rsg_get_tuning(b"RSG_FUSED_KIND", buf, 2) == _lib.RSG_ERR_INVALID_ARG
+
+
+def test_environment_changes_no_kernel_choice():
+    """The production library ignores the RSG_* environment variables (only
+    measurement builds read them): a process with every knob set to a
+    non-default value in its environment still sees the defaults."""
+    import subprocess
+    import sys
+    from rustfs_amd import _lib
+    env = dict(os.environ)
+    nondefault = {"RSG_FUSED": "0", "RSG_LOST_DISK_FAST": "0", "RSG_ZERO_COPY": "0", "RSG_VEC_BLOCK": "256",
+                  "RSG_VEC_OCC": "3", "RSG_ROLLED": "1", "RSG_HASH_COPY": "1", "RSG_HASH_DEPTH": "3",
+                  "RSG_FUSED_KIND": "dma", "RSG_FUSED_SPW1": "1", "RSG_ENC_PRIO": "3", "RSG_DMA_EW": "4",
+                  "RSG_DMA_NT": "0", "RSG_DMA_SPW": "4", "RSG_DMA_PRIO": "0", "RSG_DECODE_NET": "0",
+                  "RSG_NET12_RD": "4", "RSG_HASH_UNAL": "0", "RSG_GET_CACHED": "0"}
+    assert set(nondefault) == set(_lib.TUNING_DEFAULTS)
+    env.update(nondefault)
+    code = ("import json, sys; sys.path.insert(0, %r); from rustfs_amd import _lib; "
+            "print(json.dumps({k: _lib.get_tuning(k) for k in _lib.TUNING_DEFAULTS}))" % ROOT)
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    import json
+    assert json.loads(out.stdout.strip().splitlines()[-1]) == _lib.TUNING_DEFAULTS

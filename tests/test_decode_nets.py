@@ -121,52 +121,6 @@ def test_decode_nets_rebuild_true_shards(oracle):
             assert np.array_equal(got, st[want_idx]), (p["pid"], trial)
 
 
-# ---------------------------------------------------------------- RS(16,4)
-HEADER16 = os.path.join(ROOT, "rustfs_amd", "csrc", "rs164_decode_nets.h")
-
-
-def test_rs16_decode_nets_rebuild_true_shards(oracle):
-    """RS(16,4) (rs164_decode_nets.h, k_decode_records_net16): per pattern a
-    network over survivors 0-7 and one over survivors 8-15, XOR-combined,
-    must give the true shards; the table is every 1- and 2-shard loss
-    (GET: a data shard lost; heal: every loss) and its rows are the oracle's
-    decode matrix rows."""
-    k, t = 16, 20
-    src = open(HEADER16).read()
-    pats = []
-    for m in re.finditer(r"\{0x([0-9a-f]+), (\d), (\d+), (\d), (\d), \{(.*?)\}\},  // (\d+)", src):
-        rows = [[int(x) for x in r.split(",")] for r in re.findall(r"\{([0-9, ]+)\}", m.group(6))]
-        pats.append(dict(absent=int(m.group(1), 16), heal=int(m.group(2)), nf=int(m.group(3)), R=int(m.group(4)),
-                         nst=int(m.group(5)), coef=rows, pid=int(m.group(7))))
-    assert len(pats) == int(re.search(r"kCount = (\d+)", src).group(1))
-    assert sum(1 for p in pats if p["heal"]) == 20 + 190
-    assert sum(1 for p in pats if not p["heal"]) == 16 + 120 + 16 * 4
-    rng = np.random.default_rng(164)
-    gm = oracle.matrix(k, 4)
-    for p in pats:
-        lost = [i for i in range(t) if p["absent"] >> i & 1]
-        files = [i for i in range(t) if i not in lost]
-        store = lost if p["heal"] else [i for i in lost if i < k]
-        want_idx = store + files[k:]
-        assert p["R"] == len(want_idx) and p["nst"] == len(store) and p["nf"] == len(files)
-        inv = oracle.invert(gm[files[:k]])
-        for r, idx in enumerate(want_idx):
-            row = []
-            for c in range(k):
-                a = 0
-                for i in range(k):
-                    a ^= oracle.gf_mul(int(gm[idx][i]), int(inv[i][c]))
-                row.append(a)
-            assert row == p["coef"][r], (p["pid"], r)
-        st = np.zeros((t, 32), dtype=np.uint8)
-        st[:k] = rng.integers(0, 256, (k, 32), dtype=np.uint8)
-        oracle.encode(k, 4, st)
-        lo = _run(_program(src, p["pid"], "net_lo"), _planes(st[files[:8]]))
-        hi = _run(_program(src, p["pid"], "net_hi"), _planes(st[files[8:16]]))
-        got = _bytes([a ^ b for a, b in zip(lo, hi)], p["R"])
-        assert np.array_equal(got, st[want_idx]), p["pid"]
-
-
 # ---------------------------------------------------------------- RS(12,4)
 HEADER12 = os.path.join(ROOT, "rustfs_amd", "csrc", "rs124_decode_nets.h")
 

@@ -99,3 +99,84 @@ def test_four_threads_decode_and_heal(gpu, oracle):
     for t in ths:
         t.join()
     assert not errors, errors[0]
+
+
+def _rot(torch, f, stripe, S, pos):
+    """The record's body altered, its digest left: a bitrot mismatch."""
+    bad = f.clone()
+    off = stripe * (32 + S) + 32 + pos
+    bad[off] = bad[off] ^ 0x10
+    return bad
+
+
+def test_rotten_records_redone_async(gpu, oracle):
+    """a submitted GET and heal that each meet a rotten record
+    (verify-before-use, bitrot.rs:227-247: the record counts as missing for its
+    stripe, which the finishing step redoes) with a second job queued behind
+    them on the same stream, waited out of order; then the same calls again,
+    reusing the returned scratch.  Outputs, h_src and statuses bit-exact."""
+    import torch
+    from rustfs_amd import Erasure, _lib
+    S, n = 1024, 1100  # >= 1024 stripes: the one-pass kernels, as the engine picks at scale
+    shards, recs, files = _oracle_records(torch, oracle, S, n, seed=3)
+    e = Erasure(K, M, K * S)
+    rec = 32 + S
+    want = torch.from_numpy(shards[:, :K].reshape(n, K * S).copy()).cuda()
+    get_src = [None if i in (1, 6) else files[i] for i in range(T)]
+    get_src[3] = _rot(torch, files[3], 5, S, 77)            # stripe 5: data shard 3 rotten too
+    heal_src = [None if i in (1, 8) else files[i] for i in range(T)]
+    heal_src[4] = _rot(torch, files[4], 1099, S, S - 1)      # stripe 1099: data shard 4 rotten
+    stream = torch.cuda.Stream()
+    for rnd in range(2):
+        with torch.cuda.stream(stream):
+            tg = [torch.zeros(n * rec, dtype=torch.uint8, device="cuda") if i in (1, 8) else None for i in range(T)]
+            t_get = e.decode_records_submit(get_src, S, n, inplace=True, stream=stream)
+            t_heal = e.heal_records_submit(heal_src, tg, S, n, stream=stream)
+            t_after = e.decode_records_submit(files, S, n, stream=stream)  # queued behind both
+        out, status = t_after.wait()
+        assert status == [0] * n and torch.equal(out, want), rnd
+        assert t_heal.wait() == [0] * n, rnd
+        for i in (1, 8):
+            assert np.array_equal(tg[i].cpu().numpy().reshape(n, rec), recs[i]), (rnd, i)
+        slots, src, status = t_get.wait()
+        assert status == [0] * n, rnd
+        assert not src[1].any() and not src[6].any()
+        assert not src[3][5] and src[3][:5].all() and src[3][6:].all(), rnd
+        got = slots.view(n, K, S)
+        for i in (1, 6):
+            assert torch.equal(got[:, i], want.view(n, K, S)[:, i]), (rnd, i)
+        assert torch.equal(got[5, 3], want.view(n, K, S)[5, 3]), rnd  # the rotten record's shard, rebuilt
+    assert _lib.load().rsg_sync(gpu.handle, stream.cuda_stream) == 0
+
+
+def test_in_place_slots_must_not_alias(gpu, oracle):
+    """one buffer passed as two slots whose stripe windows collide
+    (target_stride == S, slot j = slot i + S: stripe s of slot j is stripe s+1
+    of slot i) is refused — two rebuilt shards would overwrite each other; the
+    documented block layout (slot i = base + i*S, stride k*S) is accepted."""
+    import ctypes
+    import torch
+    from rustfs_amd import _lib
+    S, n = 1024, 4
+    shards, recs, files = _oracle_records(torch, oracle, S, n, seed=4)
+    L = _lib.load()
+    buf = torch.zeros((n + K) * S, dtype=torch.uint8, device="cuda")
+    ptrs = (ctypes.c_void_p * T)(*[None if i in (0, 1) else files[i].data_ptr() for i in range(T)])
+    status = (ctypes.c_int * n)()
+    src = (ctypes.c_uint8 * (K * n))()
+
+    def call(slots, stride):
+        tg = (ctypes.c_void_p * K)(*slots)
+        return L.rsg_decode_records_into_dev(gpu.handle, K, M, S, n, ptrs, _lib.RSG_HASH_HIGHWAY256S, 1, tg, stride,
+                                             src, status, None)
+    base = buf.data_ptr()
+    alias = [base + i * S for i in range(K)]  # stride S: every slot's stripe s is slot 0's stripe s+i
+    assert call(alias, S) == _lib.RSG_ERR_INVALID_ARG
+    same = [base] * K
+    assert call(same, K * S) == _lib.RSG_ERR_INVALID_ARG
+    block = torch.zeros(n * K * S, dtype=torch.uint8, device="cuda")
+    assert call([block.data_ptr() + i * S for i in range(K)], K * S) == 0
+    torch.cuda.synchronize()
+    assert list(status) == [0] * n
+    got = block.view(n, K, S).cpu().numpy()
+    assert np.array_equal(got[:, 0], shards[:, 0]) and np.array_equal(got[:, 1], shards[:, 1])

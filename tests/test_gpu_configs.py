@@ -172,19 +172,16 @@ print("ok")
 @pytest.mark.parametrize("env", [{"RSG_DMA_SPW": "4"}, {"RSG_DMA_EW": "4"}, {"RSG_DMA_NT": "0"},
                                  {"RSG_ENC_PRIO": "3"}])
 def test_dma_kernel_ab_variants(gpu, oracle, env):
-    """The fused DMA kernel's A/B knobs (read once per process, so each runs
-    in its own process): four stripes per workgroup, the two-wave encoder,
-    cached loads/stores, raised priorities — parity and digests vs the oracle
-    on a ragged batch (n = 2051) and a 4-aligned one."""
+    """The fused DMA kernel's A/B knobs, set through rsg_set_tuning for this
+    test alone: four stripes per workgroup, the two-wave encoder, cached
+    loads/stores, raised priorities — parity and digests vs the oracle on a
+    ragged batch (n = 2051) and a 4-aligned one."""
     import os
-    import subprocess
-    import sys
+    from rustfs_amd import _lib
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    for n in (2051, 2052):
-        r = subprocess.run([sys.executable, "-c", _VARIANT_SNIPPET.format(root=root, n=n)],
-                           env={**os.environ, **env, "RSG_FUSED_KIND": "dma"}, capture_output=True, text=True,
-                           timeout=150)
-        assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (env, n, r.stdout[-500:], r.stderr[-2000:])
+    with _lib.tuned(RSG_FUSED_KIND="dma", **env):
+        for n in (2051, 2052):
+            exec(_VARIANT_SNIPPET.format(root=root, n=n), {})
 
 
 _WIDE_SNIPPET = r"""
@@ -217,12 +214,10 @@ def test_wide_kernel_ragged_batches(gpu, oracle, kind):
     per workgroup, 1 KiB steps, XOR-network encoder on 16 B per lane of a
     stripe pair): parity and all 12 digests vs the oracle on ragged batches
     (dead stripes in the last workgroup), a single step and many steps.
-    Forced with RSG_FUSED_KIND (read once per process: own process each)."""
+    Forced with the RSG_FUSED_KIND knob (rsg_set_tuning)."""
     import os
-    import subprocess
-    import sys
+    from rustfs_amd import _lib
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    for n, S in ((1, 1024), (3, 4096), (5, 2048), (6, 65536), (1027, 8192)):
-        r = subprocess.run([sys.executable, "-c", _WIDE_SNIPPET.format(root=root, n=n, S=S)],
-                           env={**os.environ, "RSG_FUSED_KIND": kind}, capture_output=True, text=True, timeout=150)
-        assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (kind, n, S, r.stdout[-500:], r.stderr[-2000:])
+    with _lib.tuned(RSG_FUSED_KIND=kind):
+        for n, S in ((1, 1024), (3, 4096), (5, 2048), (6, 65536), (1027, 8192)):
+            exec(_WIDE_SNIPPET.format(root=root, n=n, S=S), {})

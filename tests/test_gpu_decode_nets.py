@@ -1,13 +1,16 @@
-"""Every erasure pattern with a compile-time XOR network through the one-pass
-GET / heal kernels (k_decode_records_net for RS(8,4): every pattern of one or
-two lost shards, one kernel per pattern, rs84_decode_nets.h;
-k_decode_records_net16 for RS(16,4), rs164_decode_nets.h — the patterns are
-read from the generated tables): GET (a data shard lost) and heal (every
-lost shard a target), on oracle-built BitrotWriter records, over a ragged
-batch (RS(8,4): 19 stripes = two full 8-stripe workgroups and a partial
-one, so every 4-stripe network group meets live and dead stripes; RS(16,4):
-11 stripes = two full 4-stripe workgroups and a partial one), bit-exact
-against the oracle's shards and digests; then the same pattern with one
+"""Every erasure pattern of one or two lost shards through the one-pass GET /
+heal kernels: the compile-time XOR-network kernels (k_decode_records_net for
+RS(8,4), one kernel per pattern, rs84_decode_nets.h; RS(4,4), RS(6,4),
+RS(10,4), RS(12,4) likewise — the patterns read from the generated tables)
+and the run-time-table kernel k_decode_records_dma for every other k <= 16
+(RS(16,4), and the odd data counts of 5-, 9-, 15-drive sets and the reduced-
+redundancy class: RS(5,4), RS(11,4), RS(15,1), ...; the patterns generated
+here): GET (a data shard lost) and heal (every lost shard a target), on
+oracle-built BitrotWriter records, over a ragged batch (RS(8,4): 19 stripes
+= two full 8-stripe workgroups and a partial one, so every 4-stripe network
+group meets live and dead stripes; RS(16,4): 11 stripes = two full 4-stripe
+workgroups and a partial one), bit-exact against the oracle's shards and
+digests; then the same pattern with one
 surplus parity record of one stripe altered and re-hashed must report
 "inconsistent sources" for that stripe only (erasure.rs:935-973,
 heal.rs:179-197).  The CPU test test_decode_nets.py pins the networks
@@ -137,9 +140,20 @@ def test_heal_every_pattern(gpu, oracle, records, one_pass, lost):
             assert np.array_equal(got[keep], recs[i][keep]), f"shard {i}"
 
 
+def _every_pattern(k, m):
+    """(heal, lost) of every one- and two-shard loss: GET needs a data shard
+    among the lost (else nothing is rebuilt), heal takes every loss."""
+    t = k + m
+    losses = [(i,) for i in range(t)] + (list(itertools.combinations(range(t), 2)) if m >= 2 else [])
+    return [(0, lost) for lost in losses if min(lost) < k] + [(1, lost) for lost in losses]
+
+
 # ---------------------------------------------------------------- RS(16,4)
+# no networks since round 5 (rustfs cannot store 20 shards, fileinfo.rs:38):
+# GET on the table kernel, heal on the two-pass path (or the table kernel
+# with the one-pass engine forced, as here)
 K16, T16, N16 = 16, 20, 11
-LISTED16 = _listed("rs164_decode_nets.h", T16)
+LISTED16 = _every_pattern(16, 4)
 
 
 @pytest.fixture(scope="module")
@@ -304,22 +318,28 @@ def test_rs12_every_listed_pattern(gpu, oracle, records12, one_pass, heal, lost)
 # the default geometries of 10- and 14-drive sets (storageclass.rs:24-31) on
 # ragged walks: RS(6,4) with S = 1001 (records at odd offsets), RS(10,4) with
 # S = 1002 (records 2 mod 8, as at 1 MiB blocks)
-GEOS = {6: (11, 1001), 10: (9, 1002), 4: (13, 1003)}
+GEOS = {(6, 4): (11, 1001), (10, 4): (9, 1002), (4, 4): (13, 1003),
+        # the table kernel at odd k (round 5): RS(5,4) 9 drives, RS(11,4) 15
+        # drives, RS(15,1) the reduced-redundancy class of 16 drives, RS(3,2),
+        # RS(7,1), RS(13,3), RS(1,1) (2 drives) — ragged S, records at every
+        # alignment mod 8
+        (5, 4): (19, 1005), (11, 4): (9, 1006), (15, 1): (11, 1007), (3, 2): (17, 999), (7, 1): (19, 1011),
+        (13, 3): (5, 1013), (1, 1): (9, 997), (9, 4): (7, 1019)}
 LISTED4 = _listed("rs44_decode_nets.h", 8)
 LISTED6 = _listed("rs64_decode_nets.h", 10)
 LISTED10 = _listed("rs104_decode_nets.h", 14)
 
 
-def _geo_records(oracle, k):
+def _geo_records(oracle, k, m=4):
     import torch
-    n, S = GEOS[k]
-    t, rec = k + 4, 32 + S
-    rng = np.random.default_rng(k * 7)
+    n, S = GEOS[(k, m)]
+    t, rec = k + m, 32 + S
+    rng = np.random.default_rng(k * 7 + m)
     shards = np.zeros((n, t, S), dtype=np.uint8)
     recs = np.zeros((t, n, rec), dtype=np.uint8)
     for s in range(n):
         shards[s, :k] = rng.integers(0, 256, (k, S), dtype=np.uint8)
-        oracle.encode(k, 4, shards[s])
+        oracle.encode(k, m, shards[s])
         for i in range(t):
             recs[i, s, :32] = np.frombuffer(oracle.hh256s(shards[s, i].tobytes()), dtype=np.uint8)
             recs[i, s, 32:] = shards[s, i]
@@ -328,17 +348,17 @@ def _geo_records(oracle, k):
 
 @pytest.fixture(scope="module")
 def records6(gpu, oracle):
-    return _geo_records(oracle, 6)
+    return _geo_records(oracle, 6, 4)
 
 
 @pytest.fixture(scope="module")
 def records10(gpu, oracle):
-    return _geo_records(oracle, 10)
+    return _geo_records(oracle, 10, 4)
 
 
 @pytest.fixture(scope="module")
 def records4(gpu, oracle):
-    return _geo_records(oracle, 4)
+    return _geo_records(oracle, 4, 4)
 
 
 def test_rs6_rs10_tables_list_every_pattern():
@@ -350,15 +370,15 @@ def test_rs6_rs10_tables_list_every_pattern():
     assert len([x for x in LISTED4 if not x[0]]) == 4 + 22 and len([x for x in LISTED4 if x[0]]) == 8 + 28
 
 
-def _geo_case(oracle, k, data, heal, lost):
+def _geo_case(oracle, k, data, heal, lost, m=4):
     """GET in both forms and heal of one pattern, bit-exact against the
     oracle, with an altered surplus parity reported for its stripe alone."""
     import torch
     from rustfs_amd import Erasure, _lib
-    n, S = GEOS[k]
-    t, rec = k + 4, 32 + S
+    n, S = GEOS[(k, m)]
+    t, rec = k + m, 32 + S
     shards, recs, files = data
-    e = Erasure(k, 4, k * S)
+    e = Erasure(k, m, k * S)
     present = [i for i in range(t) if i not in lost]
     sur = present[k:]
 
@@ -406,13 +426,13 @@ def _geo_case(oracle, k, data, heal, lost):
 @pytest.mark.parametrize("heal,lost", LISTED6, ids=lambda x: str(x))
 def test_rs6_every_listed_pattern(gpu, oracle, records6, one_pass, heal, lost):
     """k_decode_records_net6 (rs_decode_net.hip over 6 survivors)."""
-    _geo_case(oracle, 6, records6, heal, lost)
+    _geo_case(oracle, 6, records6, heal, lost, 4)
 
 
 @pytest.mark.parametrize("heal,lost", LISTED4, ids=lambda x: str(x))
 def test_rs4_every_listed_pattern(gpu, oracle, records4, one_pass, heal, lost):
     """k_decode_records_net4 (rs_decode_net.hip over 4 survivors)."""
-    _geo_case(oracle, 4, records4, heal, lost)
+    _geo_case(oracle, 4, records4, heal, lost, 4)
 
 
 @pytest.mark.parametrize("heal,lost", LISTED10, ids=lambda x: str(x))
@@ -420,12 +440,46 @@ def test_rs10_every_listed_pattern(gpu, oracle, records10, one_pass, heal, lost)
     """k_decode_records_net10 (rs_decode_netq.hip, parts of 3, 3, 2, 2
     survivors; GET on a 2-slot ring with two workgroups per CU, heal one
     workgroup on a 4-slot ring)."""
-    _geo_case(oracle, 10, records10, heal, lost)
+    _geo_case(oracle, 10, records10, heal, lost, 4)
 
 
-def test_rs16_heal_unlisted_pattern_falls_back(gpu, oracle, records16, one_pass):
-    """A heal the network table does not list (three lost shards) takes the
-    two-pass path even with the one-pass engine forced: still bit-exact."""
+TABLE_GEOS = [(5, 4), (11, 4), (15, 1), (3, 2), (7, 1), (13, 3), (1, 1), (9, 4)]
+TABLE_CASES = [(k, m, heal, lost) for k, m in TABLE_GEOS for heal, lost in _every_pattern(k, m)]
+
+
+@pytest.fixture(scope="module")
+def table_records(gpu, oracle):
+    cache = {}
+
+    def get(k, m):
+        if (k, m) not in cache:
+            cache[(k, m)] = _geo_records(oracle, k, m)
+        return cache[(k, m)]
+    return get
+
+
+def test_table_patterns_cover_every_loss():
+    """RS(5,4): 5 + 5*8 + 10 GET and 9 + 36 heal patterns; RS(15,1): 15 GET and
+    16 heal (one parity shard: one loss at most); RS(11,4) 11 + 11*4 + 55 and
+    15 + 105."""
+    def count(k, m, heal):
+        return len([x for x in _every_pattern(k, m) if x[0] == heal])
+    assert (count(5, 4, 0), count(5, 4, 1)) == (5 + 40 + 10, 9 + 36)
+    assert (count(15, 1, 0), count(15, 1, 1)) == (15, 16)
+    assert (count(11, 4, 0), count(11, 4, 1)) == (11 + 44 + 55, 15 + 105)
+
+
+@pytest.mark.parametrize("k,m,heal,lost", TABLE_CASES, ids=str)
+def test_table_kernel_every_pattern(gpu, oracle, table_records, one_pass, k, m, heal, lost):
+    """The run-time-table one-pass kernel (k_decode_records_dma, one part per
+    survivor count) at the data counts without networks: every one- and
+    two-shard loss, GET in both forms and heal, ragged S."""
+    _geo_case(oracle, k, table_records(k, m), heal, lost, m)
+
+
+def test_rs16_heal_three_lost(gpu, oracle, records16, one_pass):
+    """A heal of three lost shards (the table kernel's widest target set at
+    RS(16,4) with the one-pass engine forced): bit-exact."""
     import torch
     from rustfs_amd import Erasure
     shards, recs, files = records16
@@ -474,20 +528,20 @@ print("ok")
 """
 
 
-@pytest.mark.parametrize("env", [{"RSG_DECODE_NET": "0"}, {"RSG_GET_CACHED": "0"}, {"RSG_NET12_RD": "4"}])
-def test_network_knobs_in_own_process(gpu, oracle, env):
-    """The A/B knobs of the network GET/heal path (read once per process, so
-    each in its own process): RSG_DECODE_NET=0 sends listed RS(8,4) patterns
-    to the run-time-table one-pass kernel and RS(16,4) heal to the two-pass
-    path; RSG_GET_CACHED=0 makes the RS(8,4) network kernel's stores
-    non-temporal; RSG_NET12_RD=4 runs RS(12,4)'s GET on a 4-slot ring, one
-    workgroup per CU.  Bit-exact against the oracle either way."""
-    import subprocess
-    import sys
+@pytest.mark.parametrize("env", [{"RSG_DECODE_NET": "0"}, {"RSG_GET_CACHED": "0"}])
+def test_network_knobs(gpu, oracle, env):
+    """The A/B knobs of the network GET/heal path, set through rsg_set_tuning
+    for this test alone: RSG_DECODE_NET=0 sends listed RS(8,4) / RS(12,4)
+    patterns to the run-time-table one-pass kernel; RSG_GET_CACHED=0 makes the
+    RS(8,4) network kernel's stores non-temporal.  Bit-exact against the
+    oracle either way.  (RSG_NET12_RD=4 exists in measurement builds only.)"""
+    from rustfs_amd import _lib
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-c", _TABLE_SNIPPET.format(root=root)], env={**os.environ, **env},
-                       capture_output=True, text=True, timeout=150)
-    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (env, r.stdout[-500:], r.stderr[-2000:])
+    try:
+        with _lib.tuned(**env):
+            exec(_TABLE_SNIPPET.format(root=root), {})
+    finally:  # the snippet forces the one-pass engine on the shared context
+        _lib.check(_lib.load().rsg_set_record_engine(gpu.handle, _lib.RSG_RECORD_ENGINE_AUTO))
 
 
 # ------------------------------------------------- long shards (the ring wraps)
