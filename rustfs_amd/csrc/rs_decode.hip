@@ -126,6 +126,13 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_re
                             __builtin_amdgcn_perm(t4.w, t4.z, s1b), __builtin_amdgcn_perm(t2, t2, s2b));
                 }
             }
+            if constexpr (C & 1) {  // an odd survivor count leaves its last coefficient's third term pending
+#pragma unroll
+                for (int r = 0; r < RM; ++r) {
+                    acc[r][0] ^= pend[r][0];
+                    acc[r][1] ^= pend[r][1];
+                }
+            }
             const bool part = s + 1 == steps && tail != CH;  // wave-uniform
             const uint64_t keep = part ? part_mask8(lane * 8u, tail) : ~0ull;
 #pragma unroll
