@@ -85,22 +85,34 @@ constexpr int kKQ = RSG_NETQ_K, kNQ = 4;  // data shards, network waves
 constexpr int kPartC0[4] = {0, 3, 6, kKQ == 12 ? 9 : 8};
 constexpr int kPartN[4] = {3, 3, kKQ == 12 ? 3 : 2, kKQ == 12 ? 3 : 2};
 
-// ENC (the fused encode): the accumulators are also the target-row area —
-// a row's finisher writes its bytes over the accumulator it has just read and
-// the target hasher clears it after hashing it, so three slots (the hasher
-// trails two steps) replace two slots plus the double-buffered row area.
+// TR (target rows in their accumulators): the fused encode (ENC, all four
+// parity rows) and a heal on a 2-slot ring (its TH target rows).  A target
+// row's finisher writes its bytes over the accumulator it has just read and
+// the target hasher clears it after hashing it, so the target rows take three
+// accumulator slots (the hasher trails two steps) instead of two plus the
+// double-buffered row area — what lets RS(12,4)'s and RS(10,4)'s heal fit two
+// workgroups (two hash chains and two network waves per SIMD) in the LDS.
 template <int NF, int TH, int RDX = 4, bool ENC = false>
 struct NetQShape : RecRing<NF, 4, TH> {
-    static constexpr int WAVES = RecRing<NF, 4, TH>::HW + kNQ + RecRing<NF, 4, TH>::TW;
-    // one row's accumulator: 8 planes, lane-major dwords (2 KiB); ENC: also
-    // the row's 4 stripes at the target hasher's pitch
-    static constexpr uint32_t XROW = ENC ? 4 * dma::PP : 8 * 64 * 4;
-    static constexpr uint32_t XSLOT = 4 * XROW;    // a step's exchange (8-8.5 KiB)
-    static constexpr int NXB = ENC ? 3 : 2;        // exchange slots
+    static constexpr bool TR = ENC || (TH > 0 && RDX == 2);
+    // a TR heal whose last hash wave's idle quads cover the target streams
+    // hashes its targets there (records_hash_target_wave): one wave fewer
+    static constexpr bool MERGE =
+        TR && !ENC && TH > 0 && 2 * (8 - RecRing<NF, 4, TH>::LAST) >= 4 * TH;
+    static constexpr int WAVES = RecRing<NF, 4, TH>::HW + kNQ + (MERGE ? 0 : RecRing<NF, 4, TH>::TW);
+    static constexpr int NT = TR ? (ENC ? 4 : TH) : 0;  // rows [0, NT) have a target area
+    static constexpr uint32_t XROW_T = 4 * dma::PP;    // target row: accumulator, then its 4 stripes' bytes
+    static constexpr uint32_t XROW_C = 8 * 64 * 4;     // accumulator: 8 planes, lane-major dwords (2 KiB)
+    static constexpr int NTS = 3, NCS = 2;             // slots: target rows, the other rows
+    static constexpr uint32_t TSLOTX = NT * XROW_T, CSLOTX = (4 - NT) * XROW_C;
+    static constexpr uint32_t XBYTES = NTS * TSLOTX + NCS * CSLOTX;  // the exchange area
     static constexpr int XB = TH ? 1 : 0;          // extra barrier: heal's target hashers trail by 2 steps
     static constexpr int RD = RDX;                 // ring slots (RD - 1 steps of DMA in flight)
-    static constexpr uint32_t LDS = RD * RecRing<NF, 4, TH>::DSLOT + NXB * XSLOT +
-                                    (TH && !ENC ? 2 * RecRing<NF, 4, TH>::TSLOT : 16) + 32;
+    static constexpr uint32_t LDS = RD * RecRing<NF, 4, TH>::DSLOT + XBYTES +
+                                    (TH && !TR ? 2 * RecRing<NF, 4, TH>::TSLOT : 16) + 32;
+    // waves per SIMD with two workgroups per CU on the 2-slot ring (the
+    // register budget the compiler must meet)
+    static constexpr int WPE = RDX == 2 ? (2 * WAVES + 3) / 4 : 1;
 };
 
 __device__ __forceinline__ void put8_q(uint8_t* p, const uint2& v) { st64_any(p, u64_of(v)); }  // any alignment
@@ -150,10 +162,12 @@ __device__ __forceinline__ void netq_wave(const GfApplyParams& p, uint64_t n, ui
     const uint32_t tail = walk_tail(p.byte_end, steps);  // a ragged walk's last step: first tail bytes only
     uint32_t keep[8];   // step t-1's part of row Q, held across B(t)
     uint2 cmp[4];       // CMP: step t-1's surplus row, held across B(t)
-    // row r's accumulator of step t, lane-major
-    auto xb_at = [&](int r, uint32_t t) {
-        return (uint32_t*)(xbuf + (t % L::NXB) * L::XSLOT + r * L::XROW) + lane;
+    // row r's accumulator of step t, lane-major (target rows: NTS slots, the rest NCS)
+    auto xrow = [&](int r, uint32_t t) -> uint8_t* {
+        return r < L::NT ? xbuf + (t % L::NTS) * L::TSLOTX + r * L::XROW_T
+                         : xbuf + L::NTS * L::TSLOTX + (t % L::NCS) * L::CSLOTX + (r - L::NT) * L::XROW_C;
     };
+    auto xb_at = [&](int r, uint32_t t) { return (uint32_t*)xrow(r, t) + lane; };
     // step t: this wave's 3 survivors -> 24 planes -> its part of every row;
     // the other rows' parts out to LDS; copy-through of its data survivors (GET)
     auto part = [&](uint32_t t) {
@@ -208,7 +222,7 @@ __device__ __forceinline__ void netq_wave(const GfApplyParams& p, uint64_t n, ui
         uint32_t w[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) w[i] = keep[i] ^ xa[64 * i];
-        if constexpr (!ENC) {  // ENC: the target hasher clears it
+        if constexpr (!(L::TR && Q < L::NT)) {  // a target row's area: the target hasher clears it
 #pragma unroll
             for (int i = 0; i < 8; ++i) xa[64 * i] = 0u;
         }
@@ -221,16 +235,14 @@ __device__ __forceinline__ void netq_wave(const GfApplyParams& p, uint64_t n, ui
                     if (!ragged) put8_q(ob[j] + p.out_off[Q] + (uint64_t)s * CH, v);
                     else st64_part(ob[j] + p.out_off[Q] + (uint64_t)s * CH, u64_of(v), lane * 8u, tail);
                 }
-                if constexpr (ENC)  // over the accumulator just read
-                    *(uint2*)(xbuf + (s % L::NXB) * L::XSLOT + Q * L::XROW + j * PP + lane * 8u) = v;
+                if constexpr (L::TR)  // over the accumulator just read
+                    *(uint2*)(xrow(Q, s) + j * PP + lane * 8u) = v;
                 else if constexpr (TH > 0)
                     *(uint2*)(trow + (s & 1) * L::TSLOT + (Q * SPW + j) * PP + lane * 8u) = v;
             }
-            if constexpr (ENC) {  // the accumulator's words the rows' pitch skips (the hasher clears the rest)
-                static_assert(PP - dma::CH == 32 && L::XROW >= 8 * 64 * 4, "row pitch against the plane words");
-                if (lane < 24u)
-                    *(uint32_t*)(xbuf + (s % L::NXB) * L::XSLOT + Q * L::XROW + dma::CH + (lane / 8u) * PP +
-                                 (lane % 8u) * 4u) = 0u;
+            if constexpr (L::TR) {  // the accumulator's words the rows' pitch skips (the hasher clears the rest)
+                static_assert(PP - dma::CH == 32 && L::XROW_T >= 8 * 64 * 4 && Q < L::NT, "row pitch against the plane words");
+                if (lane < 24u) *(uint32_t*)(xrow(Q, s) + dma::CH + (lane / 8u) * PP + (lane % 8u) * 4u) = 0u;
             }
         } else if (!ragged) {
 #pragma unroll
@@ -247,7 +259,7 @@ __device__ __forceinline__ void netq_wave(const GfApplyParams& p, uint64_t n, ui
     };
     if constexpr (FIN) {  // every accumulator of row Q starts cleared
 #pragma unroll
-        for (int b = 0; b < L::NXB; ++b)
+        for (int b = 0; b < (Q < L::NT ? L::NTS : L::NCS); ++b)
 #pragma unroll
             for (int i = 0; i < 8; ++i) xb_at(Q, b)[64 * i] = 0u;
     }
@@ -294,19 +306,20 @@ __device__ __forceinline__ void netq_wave(const GfApplyParams& p, uint64_t n, ui
 // all four parity shards over a stripe buffer, every digest written to the
 // batch digest layout.
 template <int PID, int NF, int TH, bool ENC = false, int RDX = 4>
-__global__ __launch_bounds__((64 * NetQShape<NF, TH>::WAVES)) void RSG_NETQ_NAME(k_decode_records_, )(
+__global__ __launch_bounds__((64 * NetQShape<NF, TH, RDX, ENC>::WAVES))
+__attribute__((amdgpu_waves_per_eu(NetQShape<NF, TH, RDX, ENC>::WPE))) void RSG_NETQ_NAME(k_decode_records_, )(
     const GfApplyParams p, const HashParams h) {
     using L = NetQShape<NF, TH, RDX, ENC>;
     __shared__ __attribute__((aligned(16))) uint8_t ring[L::RD * L::DSLOT];
-    __shared__ __attribute__((aligned(16))) uint8_t xbuf[L::NXB * L::XSLOT];
-    __shared__ __attribute__((aligned(16))) uint8_t trow[TH && !ENC ? 2 * L::TSLOT : 16];
+    __shared__ __attribute__((aligned(16))) uint8_t xbuf[L::XBYTES];
+    __shared__ __attribute__((aligned(16))) uint8_t trow[TH && !L::TR ? 2 * L::TSLOT : 16];
     __shared__ Verdict vd;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t steps = p.units;
     const uint64_t s0 = (uint64_t)blockIdx.x * L::SPW;
     if (TH && wave >= (uint32_t)(L::HW + kNQ)) {
-        if constexpr (ENC)  // the target rows in the exchange slots, cleared once hashed
-            records_target_hasher<4, TH, 2, true, L::NXB, L::XSLOT, true>(p, h, xbuf, wave - L::HW - kNQ, steps, s0);
+        if constexpr (L::TR)  // the target rows in their exchange slots, cleared once hashed
+            records_target_hasher<4, TH, 2, ENC, L::NTS, L::TSLOTX, true>(p, h, xbuf, wave - L::HW - kNQ, steps, s0);
         else
             records_target_hasher<4, TH, 2>(p, h, trow, wave - L::HW - kNQ, steps, s0);
         return;
@@ -319,6 +332,12 @@ __global__ __launch_bounds__((64 * NetQShape<NF, TH>::WAVES)) void RSG_NETQ_NAME
         else if (q == 2) netq_wave<PID, NF, TH, 2, RDX, ENC>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
         else netq_wave<PID, NF, TH, 3, RDX, ENC>(p, h.n, steps, s0, ring, xbuf, trow, &vd);
         return;
+    }
+    if constexpr (L::MERGE) {
+        if (wave == (uint32_t)(L::HW - 1)) {  // the last hash wave hashes the target rows too
+            records_hash_target_wave<NF, 4, L::RD, TH, L::NTS, L::TSLOTX>(p, h, ring, xbuf, wave, steps, s0);
+            return;
+        }
     }
     records_hash_wave<NF, 4, L::XB, L::RD, ENC>(h, p.wave_prio, ring, wave, steps, s0);
 }
@@ -333,7 +352,19 @@ static_assert(NetQShape<15, 0>::LDS <= 160 * 1024 && NetQShape<14, 0>::LDS <= 16
 static_assert(NetQShape<15, 0, 2>::LDS <= 80 * 1024 && NetQShape<14, 0, 2>::LDS <= 80 * 1024 &&
                   NetQShape<12, 4, 2, true>::LDS <= 80 * 1024,
               "RS(12,4) GET and fused encode with a 2-slot ring: two workgroups per CU");
+static_assert(NetQShape<14, 2, 2>::LDS <= 80 * 1024 && NetQShape<13, 3, 2>::LDS <= 80 * 1024 &&
+                  NetQShape<15, 1, 2>::LDS > 80 * 1024,
+              "RS(12,4) heal of 2+ targets on a 2-slot ring: two workgroups per CU (1 target: one, 4 slots)");
 #endif
+static_assert(NetQShape<12, 2, 2>::LDS <= 80 * 1024 && NetQShape<13, 1, 2>::LDS <= 80 * 1024,
+              "RS(10,4) heal on a 2-slot ring: two workgroups per CU");
+
+// heal: a 2-slot ring and two workgroups per CU where its LDS (the target rows
+// in their accumulators) fits half a CU, else one on a 4-slot ring
+template <int NF, int TH>
+constexpr int heal_rd() {
+    return NetQShape<NF, TH, 2>::LDS <= 80 * 1024 ? 2 : 4;
+}
 
 using NetQLaunch = void (*)(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream);
 
@@ -342,20 +373,20 @@ void launch_netq(uint64_t blocks, const GfApplyParams& p, const HashParams& h, h
     constexpr decq::Pattern pat = decq::kPatterns[PID];
     constexpr int NF = pat.nf, TH = pat.heal ? pat.n_store : 0;
     // GET: a 2-slot ring and two workgroups per CU (RSG_NET12_RD=4: the
-    // 4-slot form); heal: its target rows do not fit two workgroups' LDS
-    const dim3 block(64 * NetQShape<NF, TH>::WAVES);
+    // 4-slot form); heal: the same where its LDS fits (heal_rd)
     if constexpr (TH == 0) {
         if (!RSG_MEASUREMENT_BUILD || tuning().net12_rd == 2)
             hipLaunchKernelGGL((RSG_NETQ_NAME(k_decode_records_, )<PID, NF, TH, false, 2>), dim3((uint32_t)blocks),
-                               block, 0, stream, p, h);
+                               dim3(64 * NetQShape<NF, TH, 2>::WAVES), 0, stream, p, h);
 #if RSG_MEASUREMENT_BUILD  // the 4-slot A/B form
         else
-            hipLaunchKernelGGL((RSG_NETQ_NAME(k_decode_records_, )<PID, NF, TH>), dim3((uint32_t)blocks), block, 0,
-                               stream, p, h);
+            hipLaunchKernelGGL((RSG_NETQ_NAME(k_decode_records_, )<PID, NF, TH>), dim3((uint32_t)blocks),
+                               dim3(64 * NetQShape<NF, TH>::WAVES), 0, stream, p, h);
 #endif
     } else {
-        hipLaunchKernelGGL((RSG_NETQ_NAME(k_decode_records_, )<PID, NF, TH>), dim3((uint32_t)blocks), block, 0,
-                           stream, p, h);
+        constexpr int RD = heal_rd<NF, TH>();
+        hipLaunchKernelGGL((RSG_NETQ_NAME(k_decode_records_, )<PID, NF, TH, false, RD>), dim3((uint32_t)blocks),
+                           dim3(64 * NetQShape<NF, TH, RD>::WAVES), 0, stream, p, h);
     }
 }
 
@@ -409,7 +440,7 @@ const uint8_t* encode_net12_coef() { return &decq::kPatterns[kEncodePid].coef[0]
 // data shards, out_off = the parity shards); h: key, out (digests).
 hipError_t launch_encode_hash_net12(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                     hipStream_t stream) {
-    using L = NetQShape<12, 4>;
+    using L = NetQShape<12, 4, 2, true>;
     if (p.C != 12 || p.R != 4 || n_stripes == 0 || shard_len == 0 || p.base != p.out_base ||
         p.stripe_stride != p.out_stripe_stride || 5 * p.stripe_stride >= (1ull << 32) ||
         (n_stripes + L::SPW - 1) / L::SPW > 0x7fffffffull || (shard_len + dma::CH - 1) / dma::CH > 0xffffffffull)

@@ -206,6 +206,164 @@ __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t 
     if (live && q == 0) h.flag_base[file][s0 + stripe_l] = ((bal >> lane) & 0xFull) ? 0 : 1;
 }
 
+// The last DMA + verify-hash wave of a heal workgroup whose idle quads
+// (16 - 2 LAST of them: its instructions cover half the wave) take over the
+// target hasher's streams (TTH target rows x G stripes), so the workgroup has
+// one wave fewer — RS(12,4)'s heal of one data + one parity shard: 8 waves
+// instead of 9, which is what lets two workgroups share a CU (5 waves on a
+// SIMD left 96 registers a wave: 12 spilled).  Ring quads walk their records
+// exactly as records_hash_wave (same DMA pipeline and barriers, XB = 1); target
+// quad tq hashes target row stream tq (row tq / G of stripe tq % G) two steps
+// behind the DMA from the target area (TNS slots of TSLOT bytes at `trow`, the
+// rows at pitch PP), clears what it read, and at the end writes the target
+// record's digest header (BitrotWriter::write).  steps + 2 barriers.
+template <int NF, int G, int RD, int TTH, int TNS, uint32_t TSLOT>
+__device__ __forceinline__ void records_hash_target_wave(const GfApplyParams& p, const HashParams& h, uint8_t* ring,
+                                                         uint8_t* trow, uint32_t hw, uint32_t steps, uint64_t s0) {
+    using dma::CH;
+    using dma::IP;
+    using dma::PP;
+    constexpr int D = RD;
+    using dma::vmcnt_imm;
+    using L = RecRing<NF, G>;
+    constexpr int HS = L::HS;
+    constexpr int NDI = L::LAST;  // this (last) wave's instructions
+    static_assert(2 * (8 - NDI) >= G * TTH && TTH > 0, "the idle quads cover the target streams");
+    if (p.wave_prio & kPrioHash) __builtin_amdgcn_s_setprio(2);
+    const uint32_t lane = threadIdx.x & 63u, q = lane & 3u, j = lane >> 2;
+    const uint64_t n = h.n;
+    const uint32_t ring_base = (uint32_t)(uintptr_t)ring, trow_base = (uint32_t)(uintptr_t)trow;
+    const uint32_t idx = 8 * hw + (j & 7u), half = j >> 3;
+    const bool quad_on = (int)(j & 7u) < NDI;  // a ring quad
+    const uint32_t file = quad_on ? idx / HS : 0, stripe_l = (idx % HS) + HS * half;
+    const uint32_t roff = (quad_on ? idx : 0) * IP + half * CH + 8 * q;
+    const bool live = quad_on && s0 + stripe_l < n;
+    // target quad tq: stream tq = row tq / G of stripe tq % G
+    const uint32_t tq = quad_on ? 0u : ((j & 7u) - NDI) + half * (8 - NDI);
+    const bool ton = !quad_on && tq < (uint32_t)(G * TTH);
+    const uint32_t tr = ton ? tq / G : 0, te = tq % G;
+    const bool tlive = ton && s0 + te < n;
+    const uint32_t troff = (ton ? tq : 0) * PP + 8 * q;
+    const uint32_t tail = walk_tail(h.len, steps);
+    const bool ragged = tail != CH;
+    HHQuad st;
+    hhq_init(st, h.key, q);
+    uint64_t ubo[HS];
+    uint32_t vlane[HS];
+#pragma unroll
+    for (int i = 0; i < HS; ++i) {
+        const uint64_t lo = s0 + i, hi = lo + HS;
+        ubo[i] = (lo < n ? lo : 0) * h.stripe_stride;
+        vlane[i] = (lane & 31u) * 16u + ((lane >> 5) && hi < n ? (uint32_t)(HS * h.stripe_stride) : 0u);
+    }
+    const uint8_t* ibase[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t ins = 8 * hw + (k < NDI ? k : 0);
+        ibase[k] = h.base[ins / HS] + ubo[k % HS];
+    }
+    auto dma_step = [&](uint32_t step) -> bool {
+        if (ragged && step + 1 == steps) return false;
+        uint32_t voff[HS];
+#pragma unroll
+        for (int i = 0; i < HS; ++i) voff[i] = vlane[i] + step * CH;
+#pragma unroll
+        for (int k = 0; k < NDI; ++k) {
+            const uint32_t ins = 8 * hw + k;
+            const uint8_t* src = ibase[k] + (uint64_t)voff[k % HS];
+            __builtin_amdgcn_global_load_lds(
+                (const void*)src, (__attribute__((address_space(3))) void*)(ring + (step % D) * L::DSLOT + ins * IP), 16,
+                0, 0);
+        }
+        return true;
+    };
+    uint64_t tlo[8], thi[8];
+    auto tail_load = [&]() {
+        const uint32_t boff = (steps - 1) * CH + (lane & 31u) * 16u;
+#pragma unroll
+        for (int k = 0; k < NDI; ++k) {
+            const uint8_t* src = ibase[k] + (uint64_t)vlane[k % HS] + (steps - 1) * CH;
+            tlo[k] = ld64_part(src, boff, h.len);
+            thi[k] = ld64_part(src + 8, boff + 8, h.len);
+        }
+    };
+    auto tail_store = [&]() {
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+#pragma unroll
+        for (int k = 0; k < NDI; ++k) {
+            const uint32_t ins = 8 * hw + k;
+            *(uint4*)(ring + ((steps - 1) % D) * L::DSLOT + ins * IP + lane * 16u) =
+                make_uint4((uint32_t)tlo[k], (uint32_t)(tlo[k] >> 32), (uint32_t)thi[k], (uint32_t)(thi[k] >> 32));
+        }
+    };
+    auto wait_next = [&](bool issued) {
+        if (!issued) __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+        else __builtin_amdgcn_s_waitcnt(vmcnt_imm((D - 2) * NDI));
+    };
+    // interval i (after B(i)): ring quads absorb ring step i (i < steps), target
+    // quads target step i - 2 (2 <= i < steps + 2); `rag`: this quad's step is
+    // the walk's ragged last one (its whole packets, then the remainder packet)
+    auto absorb = [&](uint32_t i) {
+        const bool t_act = ton && i >= 2u;
+        const bool act = quad_on ? i < steps : t_act;
+        const uint32_t ts = i - 2u;
+        const uint32_t a = quad_on ? ring_base + (i % D) * L::DSLOT + roff : trow_base + (ts % TNS) * TSLOT + troff;
+        const bool rag = ragged && (quad_on ? i + 1 == steps : ts + 1 == steps);
+        uint64_t w[16];
+        dma::read16(a, w);
+        if (act) {
+            const uint32_t full = rag ? tail / 32 : 16u;
+#pragma unroll
+            for (int t = 0; t < 16; ++t)
+                if ((uint32_t)t < full) hhq_update(st, w[t]);
+            if (rag && tail % 32) {
+                const uint8_t* tb = quad_on ? (const uint8_t*)ring + (i % D) * L::DSLOT + roff
+                                            : (const uint8_t*)trow + (ts % TNS) * TSLOT + troff;
+                hhq_remainder(st, tb - 8 * q + full * 32, tail % 32, q);
+            }
+        }
+        if (t_act) dma::zero16(a);
+    };
+    bool issued = true;
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d) issued = dma_step(d < (int)steps ? d : steps - 1);
+    if (ragged && steps == 1) {
+        tail_load();
+        tail_store();
+    }
+    wait_next(issued);
+    lds_barrier();  // B(0)
+#pragma unroll 1
+    for (uint32_t s = 0; s + 1 < steps; ++s) {
+        issued = dma_step(s + D - 1 < steps ? s + D - 1 : steps - 1);
+        const bool fill = ragged && s + 2 == steps;
+        if (fill) tail_load();
+        absorb(s);
+        if (fill) tail_store();
+        wait_next(issued);
+        lds_barrier();  // B(s+1)
+    }
+    {  // the ring's last step
+        const uint32_t s = steps - 1;
+        if (!ragged) (void)dma_step(s);
+        absorb(s);
+        wait_next(!ragged);
+        lds_barrier();  // B(steps)
+    }
+    __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+    absorb(steps);  // target step steps - 2
+    lds_barrier();  // B(steps+1): the last target rows published
+    absorb(steps + 1);  // target step steps - 1
+    // ring quads: verify before use (bitrot.rs:227-247); target quads: the
+    // target record's digest header (BitrotWriter::write)
+    const uint64_t d = hhq_digest(st, q);
+    bool mis = false;
+    if (live) mis = d != ld64_any(h.base[file] + (s0 + stripe_l) * h.stripe_stride - 32 + 8 * q);
+    const uint64_t bal = __builtin_amdgcn_ballot_w64(mis);
+    if (live && q == 0) h.flag_base[file][s0 + stripe_l] = ((bal >> lane) & 0xFull) ? 0 : 1;
+    if (tlive) st64_any(p.out_base + (s0 + te) * p.out_stripe_stride + p.out_off[tr] - 32 + 8 * q, d);
+}
+
 // Target-hasher wave tw of a heal workgroup: quad j hashes target row stream
 // pi = 16 tw + j (row r = pi / SPW of stripe pi % SPW) from the double-
 // buffered LDS row area LAG steps behind the DMA (step t-LAG's rows,

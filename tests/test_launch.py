@@ -158,31 +158,47 @@ def test_config5_plan(world):
 
 
 def test_pmc_traffic_covers_the_default_line():
-    """Every traffic entry the default bench line and the RS(12,4) lines look
-    up is in tools/pmc_traffic.json (shipped with the tree), and each is
-    within 3 % of the algorithmic bytes of its launch (no wasted re-reads)."""
+    """Every traffic entry the default bench line looks up (headline, configs
+    3/4/5, the RS(8,4) engines and the RS(12,4) extras) is in
+    tools/pmc_traffic.json (shipped with the tree), and each is within 3 % of
+    the algorithmic bytes of its launch (no wasted re-reads)."""
     import bench
-    k, m, S, n = 8, 4, 131072, 4096
-    t, rec = k + m, 32 + S
-    want = {
-        f"rs{k}{m}_S{S}_n{n}": n * (k + m) * S,
-        f"rs{k}{m}_S{S}_n{n}_hash": n * (k + m) * S,
-        "rs164_S65536_n4096": 4096 * 20 * 65536,
-        f"get_into0_rs{k}{m}_S{S}_n{n}": n * k * rec,
-        f"get_into2_rs{k}{m}_S{S}_n{n}": n * ((t - 2) * rec + 2 * S),
-        f"get_gather0_rs{k}{m}_S{S}_n{n}": n * (k * rec + k * S),
-        f"get_gather2_rs{k}{m}_S{S}_n{n}": n * ((t - 2) * rec + k * S),
-        f"heal_1d1p_rs{k}{m}_S{S}_n{n}": n * t * rec,
-        f"verify_all_rs{k}{m}_S{S}_n{n}": t * n * rec,
-        "rs124_S87382_n4096": 4096 * 16 * 87382,
-        "rs124_S87382_n4096_hash": 4096 * 16 * 87382,
-    }
+    want = {}
+    for k, S in ((8, 131072), (12, 87382)):
+        n = 4096
+        t, rec = k + 4, 32 + S
+        want[f"rs{k}4_S{S}_n{n}"] = n * t * S
+        want[f"rs{k}4_S{S}_n{n}_hash"] = n * t * S
+        for name, alg, key in bench.engine_plan(k, 4, S, n, full=False):
+            want[key] = alg
+    want["rs164_S65536_n4096"] = 4096 * 20 * 65536
     for r in (1, 2, 3, 4):
-        want[f"reconstruct_e{r}_rs{k}{m}_S{S}_n{n}"] = n * (k + r) * S
+        want[f"reconstruct_e{r}_rs84_S131072_n4096"] = 4096 * (8 + r) * 131072
     for key, alg in want.items():
         got = bench.pmc_lookup(key)
         assert got is not None, key
         assert abs(got / alg - 1) < 0.03, (key, got, alg)
+
+
+def test_pmc_traffic_sources_are_committed_counters():
+    """Every entry of tools/pmc_traffic.json names a committed directory of raw
+    rocprofv3 counters (profiles/r05/pmc/<key>/, tools/pmc_table.sh on the
+    shipped library), and its bytes_per_launch is FETCH_SIZE x 2 + WRITE_SIZE
+    (KiB, the microarch guide's gfx950 correction) recomputed from those
+    CSVs."""
+    import json
+    import subprocess
+    import tools.pmc_traffic as P
+    data = json.load(open(os.path.join(ROOT, "tools", "pmc_traffic.json")))
+    tracked = set(subprocess.run(["git", "ls-files"], cwd=ROOT, capture_output=True, text=True,
+                                 check=True).stdout.split())
+    assert data
+    for key, v in data.items():
+        src = v["source"]
+        for f in ("meta.json", "FETCH_SIZE/run_counter_collection.csv", "WRITE_SIZE/run_counter_collection.csv"):
+            assert f"{src}/{f}" in tracked, (key, f)
+        k2, again = P.entry(os.path.join(ROOT, src))
+        assert k2 == key and again["bytes_per_launch"] == v["bytes_per_launch"], key
 
 
 def test_engine_plan_rs12_4():
