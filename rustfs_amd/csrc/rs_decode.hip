@@ -258,12 +258,15 @@ bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len) {
     return one_pass_geometry(k, m, shard_len) && nf >= k && targets >= 1 && nf + targets <= k + m;
 }
 
-// The table kernel's heal against the two-pass path (GF pass, then verify +
-// target digests): one pass for k <= 8; above 8 survivors the workgroup holds
-// 4 stripes and its GF waves (k survivors x up to 4 rows each) set the pace —
-// at RS(16,4) two-pass is faster (n = 4096, one data + one parity disk: 2.14
-// ms one-pass, 1.98 ms two-pass; profiles/r03/eng_ab/).
-bool heal_table_preferred(int k) { return k <= 8; }
+// The table kernel against the two-pass path (GF pass over every column, then
+// a verify launch): its GF waves, one per stripe, apply k survivors x R rows
+// of v_perm tables per step, so past some k*R they set the pace.  At 1 MiB
+// blocks, n = 4096 (profiles/r05/geom/): one pass wins up to k*R = 40 — RS(9,4)
+// with 2 lost (R = 4: 36) GET 1.57 vs 2.16 ms, heal 1.61 vs 2.53; RS(13,3)
+// (39) GET 1.84 vs 1.86, heal 1.84 vs 1.98; RS(15,1) (15) GET 0.96 vs 1.64 —
+// and loses beyond: RS(11,4) (44) GET 2.23 vs 2.15 ms, RS(16,4) (64) GET 2.35
+// vs 1.82, heal 2.32 vs 1.96.
+bool table_one_pass_preferred(int k, int R) { return k * R <= 40; }
 
 // Patterns with a compile-time XOR network (RS(4,4), RS(6,4), RS(8,4):
 // rs_decode_net.hip; RS(10,4), RS(12,4): rs_decode_netq.hip): the launch's
@@ -338,13 +341,13 @@ hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, 
     p.byte_end = shard_len;
     h.n = n_stripes;
     if (launch_net_if_listed(1, k, m, nf, coef, n_stripes, p, h, stream)) return hipGetLastError();
-    if (!any_table && !heal_table_preferred(k)) return hipErrorNotSupported;
+    if (!any_table && !table_one_pass_preferred(k, (int)p.R)) return hipErrorNotSupported;
     if (!launch_get_any(k, nf, targets, n_stripes, p, h, stream)) return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
 hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int k, int m, int nf, uint64_t shard_len,
-                                     uint64_t n_stripes, const uint8_t* coef, hipStream_t stream) {
+                                     uint64_t n_stripes, const uint8_t* coef, bool any_table, hipStream_t stream) {
     p.wave_prio = dma_prio();
     if (!decode_dma_supported(k, m, nf, shard_len) || (int)p.C != k || n_stripes == 0 || p.R > 4 ||
         p.n_store > p.R || !dma_records_walkable(h))
@@ -353,6 +356,7 @@ hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int k, int m
     p.byte_end = shard_len;
     h.n = n_stripes;
     if (launch_net_if_listed(0, k, m, nf, coef, n_stripes, p, h, stream)) return hipGetLastError();
+    if (!any_table && !table_one_pass_preferred(k, (int)p.R)) return hipErrorNotSupported;
     if (!launch_get_any(k, nf, 0, n_stripes, p, h, stream)) return hipErrorInvalidValue;
     return hipGetLastError();
 }

@@ -138,16 +138,21 @@ hipError_t launch_encode_hash_net12(GfApplyParams p, HashParams h, uint64_t shar
 bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len);
 // coef: the launch's R x k coefficient rows (host memory, row-major), matched
 // against the compile-time XOR-network patterns (rs_decode_net.hip); may be null.
+// A listed pattern runs its network; otherwise the table kernel runs if
+// `any_table` (a forced one-pass engine) or table_one_pass_preferred(k, R),
+// else hipErrorNotSupported (the caller takes the two-pass path).
 hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int k, int m, int nf, uint64_t shard_len,
-                                     uint64_t n_stripes, const uint8_t* coef, hipStream_t stream);
+                                     uint64_t n_stripes, const uint8_t* coef, bool any_table, hipStream_t stream);
 // One-pass heal (k_decode_records_dma with target hashing), the same
 // geometries: nf present source files, `targets` absent target files written
 // with digests (nf + targets <= k + m).  A pattern with a compile-time network
 // runs it; otherwise the table kernel runs if `any_table` (a forced one-pass
-// engine) or the table heal is the faster path for k (heal_table_preferred),
-// else hipErrorNotSupported: the caller takes the two-pass path.
+// engine) or table_one_pass_preferred(k, R), else hipErrorNotSupported: the
+// caller takes the two-pass path.
 bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len);
-bool heal_table_preferred(int k);
+// The run-time-table one-pass kernel against the two-pass path for k
+// survivors and R rows (rebuilt / healed + compared): rs_decode.hip.
+bool table_one_pass_preferred(int k, int R);
 hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, int nf, int targets,
                                    uint64_t shard_len, uint64_t n_stripes, const uint8_t* coef, bool any_table,
                                    hipStream_t stream);

@@ -1516,7 +1516,11 @@ int launch_get_one_pass(RecJob& j, const std::vector<int>& files) {
         h.flag_base[f] = j.d_flags() + (size_t)files[f] * j.n;
     }
     j.sc->tmark(j.s);  // the timing hook opens after the host-side preparation
-    return hip_status(rsg::launch_decode_records_dma(p, h, k, j.m, (int)files.size(), j.S, j.n, coef.data(), j.s));
+    const bool any_table = j.ctx->record_engine.load() == RSG_RECORD_ENGINE_ONE_PASS;  // forced: the table kernel too
+    const hipError_t e =
+        rsg::launch_decode_records_dma(p, h, k, j.m, (int)files.size(), j.S, j.n, coef.data(), any_table, j.s);
+    if (e == hipErrorNotSupported) j.sc->tunmark();
+    return e == hipErrorNotSupported ? RSG_ERR_UNSUPPORTED : hip_status(e);  // unsupported: nothing launched
 }
 
 // GET submit: the pass the call normally needs alone, then the verdict copy.
@@ -1552,18 +1556,26 @@ int get_begin(RecJob& j) {
         j.phase = RecJob::FAST;
         // (record files and slots at any alignment: the ring's LDS-DMA and
         // the kernels' 8-byte stores take unaligned addresses)
-        const bool one_pass = get_dma_enabled(j.ctx, n) && rsg::decode_dma_supported(k, m, nfiles, j.S);
-        j.one_pass = one_pass;
+        bool one_pass = get_dma_enabled(j.ctx, n) && rsg::decode_dma_supported(k, m, nfiles, j.S);
         if (one_pass) {
             // verify every present record, rebuild (and gather) and check
             // the surplus parity in ONE pass; the kernel writes every present
             // file's flags and, with surplus rows, every stripe's verdict
             // whole (no memsets before it)
-            if ((st = launch_get_one_pass(j, all_idx))) return st;  // opens the timing mark
-            j.sc->tmark(j.s);
-            if (!j.any_verify && (st = hip_status(hipMemsetAsync(j.d_ok(), 1, n, j.s)))) return st;
-            for (uint64_t x = 0; x < n; ++x) j.h_status[x] = RSG_OK;
-        } else {
+            st = launch_get_one_pass(j, all_idx);  // opens the timing mark when it launches
+            if (st == RSG_ERR_UNSUPPORTED) {  // no network and the table kernel is the slower path here
+                one_pass = false;
+                j.any_verify = false;
+            } else if (st) {
+                return st;
+            } else {
+                j.sc->tmark(j.s);
+                if (!j.any_verify && (st = hip_status(hipMemsetAsync(j.d_ok(), 1, n, j.s)))) return st;
+                for (uint64_t x = 0; x < n; ++x) j.h_status[x] = RSG_OK;
+            }
+        }
+        j.one_pass = one_pass;
+        if (!one_pass) {
             if ((st = hip_status(hipMemsetAsync(j.d_ok(), 1, n, j.s)))) return st;
             j.sc->tmark(j.s);
             if ((st = get_rebuild_run(j, 0, n, j.present0, !j.out.into()))) return st;
