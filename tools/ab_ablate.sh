@@ -4,6 +4,7 @@
 # library and of exp/librsgpu_ablate.so (built with -DRSG_NET_ABLATE=1: the
 # network waves load, store and compare but do no transposes or XORs).
 # Usage: bash tools/ab_ablate.sh TAG
+. "$(dirname "$0")/measure_env.sh"  # RSG_* knobs: the measurement build (ABI 6)
 set -o pipefail
 TAG=${1:-r3_ablate}
 R=$GRAFT_REPO_ROOT

@@ -1,5 +1,6 @@
 #!/bin/bash
 # A/B of the vector GF kernels' workgroup size (RSG_VEC_BLOCK) through bench.py.
+. "$(dirname "$0")/measure_env.sh"  # RSG_* knobs: the measurement build (ABI 6)
 set -o pipefail
 OUT=gpurun_out/ab_block
 mkdir -p $OUT

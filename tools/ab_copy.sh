@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B of the hash kernel's copy mode (RSG_HASH_COPY=1: direct 8-byte stores;
 # default: LDS-staged 16-byte stores) on the GET engine, after the GPU tests.
+. "$(dirname "$0")/measure_env.sh"  # RSG_* knobs: the measurement build (ABI 6)
 set -o pipefail
 TAG=${1:-abcopy}
 OUT=gpurun_out/$TAG

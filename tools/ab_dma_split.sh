@@ -1,6 +1,7 @@
 #!/bin/bash
 # Fused DMA kernel (RS(8,4), n >= 2048): one encoder wave per 4-stripe group
 # (default) vs two taking alternate steps (RSG_DMA_EW=4), 1 and 2 MiB stripes.
+. "$(dirname "$0")/measure_env.sh"  # RSG_* knobs: the measurement build (ABI 6)
 set -o pipefail
 OUT=gpurun_out/${TAG:-ab_dma_split}; mkdir -p $OUT
 for rep in 1 2; do

@@ -3,6 +3,7 @@
 # encoder waves per stripe group, per-row folds) vs the default (one wave per
 # group, generated XOR network).  Fused parity tests first, then interleaved
 # bench --digests runs.  Usage: bash tools/ab_ew.sh TAG
+. "$(dirname "$0")/measure_env.sh"  # RSG_* knobs: the measurement build (ABI 6)
 set -o pipefail
 TAG=${1:-ab_ew}
 OUT=gpurun_out/$TAG

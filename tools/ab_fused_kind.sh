@@ -4,6 +4,7 @@
 # (2, 4, 8, 16 MiB stripes, n = 4 GiB / stripe), one process per kind (the
 # kind is read once per process).  Output: gpurun_out/<TAG>/<kind>_<MiB>m.json
 # Usage: [SIZES="1 2 4 8 16"] bash tools/ab_fused_kind.sh TAG [kinds...]  (1 MiB: n = 4096)
+. "$(dirname "$0")/measure_env.sh"  # RSG_* knobs: the measurement build (ABI 6)
 set -o pipefail
 TAG=${1:-ab_kind}; shift
 KINDS=${@:-auto ring wide2 wide4 dma}

@@ -2,6 +2,7 @@
 # A/B of the hash kernel's prefetch depth (RSG_HASH_DEPTH = batches of 8
 # packets in flight per lane) on the record engines (bench.py extras:
 # GET, heal, bitrot_verify) and the fused-digest fallback paths.
+. "$(dirname "$0")/measure_env.sh"  # RSG_* knobs: the measurement build (ABI 6)
 set -o pipefail
 OUT=gpurun_out/ab_hash
 mkdir -p $OUT

@@ -1,5 +1,6 @@
 #!/bin/bash
 # A/B of the vector kernels' resident waves per SIMD (RSG_VEC_OCC).
+. "$(dirname "$0")/measure_env.sh"  # RSG_* knobs: the measurement build (ABI 6)
 set -o pipefail
 OUT=gpurun_out/ab_occ2
 mkdir -p $OUT

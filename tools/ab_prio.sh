@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B of wave priorities: one-pass GET/heal kernels (RSG_DMA_PRIO) and the
 # DMA fused encode+hash kernel (RSG_ENC_PRIO).
+. "$(dirname "$0")/measure_env.sh"  # RSG_* knobs: the measurement build (ABI 6)
 set -o pipefail
 OUT=gpurun_out/ab_prio2
 mkdir -p $OUT

@@ -3,6 +3,7 @@
 # heal suites, then bench.py's engine extras with the networks on and off
 # (RSG_DECODE_NET=0: run-time-table GF waves) and a rocprof kernel-stats run
 # of the engine extras.  Usage: bash tools/gpu_nets.sh TAG [skip-tests]
+. "$(dirname "$0")/measure_env.sh"  # RSG_* knobs: the measurement build (ABI 6)
 set -o pipefail
 TAG=${1:-r3_nets}
 OUT=gpurun_out/$TAG

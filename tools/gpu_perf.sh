@@ -1,5 +1,6 @@
 #!/bin/bash
 # Perf pass on the GPU box: bench variants (each under its own time limit).
+. "$(dirname "$0")/measure_env.sh"  # RSG_* knobs: the measurement build (ABI 6)
 set -o pipefail
 TAG=${1:-perf}
 OUT=gpurun_out/$TAG

@@ -1,4 +1,5 @@
 set -e
+. "$(dirname "$0")/measure_env.sh"  # RSG_* knobs: the measurement build (ABI 6)
 mkdir -p gpurun_out/small
 for kib in 2048 4096 8192 16384; do
   bytes=$((kib*1024)); n4=$(( (4*1024*1024*1024)/bytes ))
