@@ -78,10 +78,11 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(2))) void k_g
 // 2 waves per SIMD); rolled in groups of 4, RS(16,4) ran at 65-66 % of HBM
 // peak, in groups of 8 (128 B in flight per lane, 105 VGPRs) at 72-73 %
 // (tools/kbench/xor3_variants.hip).  For C <= 8, R <= 4 the unrolled kernel is
-// faster and stays the default there.
-template <int R, int B, bool PRE>
+// faster and stays the default there.  G = 12 for 9-12 inputs (RS(12,4), the
+// 16-drive default; RS(10,4)): one group, every input's load in flight at
+// once instead of 8 then 4.
+template <int R, int B, bool PRE, int G = 8>
 __global__ __launch_bounds__(B) void k_gf_apply_loop(const GfApplyParams p) {
-    constexpr int G = 8;
     const uint32_t stripe = blockIdx.x / p.chunks_per_stripe;
     const uint32_t chunk = blockIdx.x - stripe * p.chunks_per_stripe;
     const uint8_t* sbase = p.base + (uint64_t)stripe * p.stripe_stride;
@@ -1349,6 +1350,14 @@ static GfKernel pick_vec_b(int C, int R) {
         return nullptr;
     }
     if (C < 1 || C > kMaxC) return nullptr;
+    if (C > 8 && C <= 12 && R <= 4 && !tuning().rolled) {
+        switch (R) {
+            case 1: return k_gf_apply_loop<1, B, PRE, 12>;
+            case 2: return k_gf_apply_loop<2, B, PRE, 12>;
+            case 3: return k_gf_apply_loop<3, B, PRE, 12>;
+            case 4: return k_gf_apply_loop<4, B, PRE, 12>;
+        }
+    }
     switch (R) {
         case 1: return k_gf_apply_loop<1, B, PRE>;
         case 2: return k_gf_apply_loop<2, B, PRE>;
