@@ -48,20 +48,32 @@ namespace rsg {
 // profiles/r02/ab_prio/).  Tuning::get_prio overrides it for A/B runs.
 [[maybe_unused]] static uint32_t dma_prio() { return (uint32_t)tuning().get_prio; }
 
-template <int NF, int G, int TH = 0>
+// RD: ring slots (RD - 1 steps of DMA in flight).  3 by default; 2 for the
+// 4-stripe workgroups of C > 8 survivors where the workgroup then fits half a
+// CU's LDS, so two share a CU (two hash chains and two GF waves per SIMD),
+// as the RS(12,4) network kernels do.
+template <int NF, int G, int TH = 0, int RD = dma::D>
 struct GetShape : RecRing<NF, G, TH> {
-    static constexpr int WAVES = RecRing<NF, G, TH>::HW + G + RecRing<NF, G, TH>::TW;
+    // a heal on a 2-slot ring whose last hash wave's idle quads cover the
+    // target streams hashes its targets there (records_hash_target_wave, LAG
+    // 1): one wave fewer
+    static constexpr bool MERGE = RD == 2 && TH > 0 && 2 * (8 - RecRing<NF, G, TH>::LAST) >= G * TH;
+    static constexpr int WAVES = RecRing<NF, G, TH>::HW + G + (MERGE ? 0 : RecRing<NF, G, TH>::TW);
+    static constexpr uint32_t LDS = RD * RecRing<NF, G, TH>::DSLOT + (TH ? 2 * RecRing<NF, G, TH>::TSLOT : 16);
+    // waves per SIMD the register budget must allow (two workgroups per CU on a 2-slot ring)
+    static constexpr int WPE = RD == 2 ? (2 * WAVES + 3) / 4 : 1;
 };
 
-template <int C, int NF, int G, int TH>
-__global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_records_dma(const GfApplyParams p,
-                                                                                          const HashParams h) {
+template <int C, int NF, int G, int TH, int RD = dma::D>
+__global__ __launch_bounds__((64 * GetShape<NF, G, TH, RD>::WAVES))
+__attribute__((amdgpu_waves_per_eu(GetShape<NF, G, TH, RD>::WPE))) void k_decode_records_dma(const GfApplyParams p,
+                                                                                            const HashParams h) {
     static_assert(C >= 1 && C <= kMaxC && NF >= C && NF <= C + 4 && TH <= 4 && NF + TH <= C + 4, "RS(C, <= 4)");
     using dma::CH;
-    using dma::D;
     using dma::IP;
     using dma::PP;
-    using L = GetShape<NF, G, TH>;
+    constexpr int D = RD;
+    using L = GetShape<NF, G, TH, RD>;
     constexpr int SPW = L::SPW, HS = L::HS;
     constexpr int RM = 4;
     __shared__ __attribute__((aligned(16))) uint8_t ring[D * L::DSLOT];
@@ -82,6 +94,12 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_re
     if (TH && wave >= (uint32_t)(L::HW + SPW)) {
         records_target_hasher<G, TH>(p, h, trow, wave - L::HW - SPW, steps, s0);
         return;
+    }
+    if constexpr (L::MERGE) {
+        if (wave == (uint32_t)(L::HW - 1)) {  // the last hash wave hashes the target rows too
+            records_hash_target_wave<NF, G, RD, TH, 2, L::TSLOT, 1, false>(p, h, ring, trow, wave, steps, s0);
+            return;
+        }
     }
     if (wave >= (uint32_t)L::HW) {
         // ------------------------- GF wave: one stripe -------------------------
@@ -167,76 +185,95 @@ __global__ __launch_bounds__((64 * GetShape<NF, G, TH>::WAVES)) void k_decode_re
         return;
     }
     // ------------------------- DMA + verify-hash wave -------------------------
-    records_hash_wave<NF, G>(h, p.wave_prio, ring, wave, steps, s0);
+    records_hash_wave<NF, G, 0, RD>(h, p.wave_prio, ring, wave, steps, s0);
+}
+
+// 4-stripe workgroups (C > 8) on a 2-slot ring where it fits half a CU's LDS
+// and at most 8 waves (two workgroups: 4 a SIMD) — a heal's target hashing
+// merged into its last hash wave where that wave has room.  9-wave shapes
+// (RS(16,4) GET, RS(15,4) GET, RS(14,4) heal) fit two a CU at 96 registers
+// too, but measured no better than on 3 slots, and slower than two passes
+// (GET RS(16,4) 2.16 vs 1.78 ms, RS(15,4) 2.20 vs 2.10; profiles/r05/ab_rd2/)
+template <int C, int NF, int G, int TH>
+constexpr int table_rd() {
+    return (G == 4 && GetShape<NF, G, TH, 2>::LDS + C * 4 * 32 <= 80 * 1024 - 512 &&
+            GetShape<NF, G, TH, 2>::WAVES <= 8)
+               ? 2
+               : dma::D;
 }
 
 template <int C, int NF, int G, int TH = 0>
 static void launch_get(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
-    hipLaunchKernelGGL((k_decode_records_dma<C, NF, G, TH>), dim3((uint32_t)blocks),
-                       dim3(64 * GetShape<NF, G, TH>::WAVES), 0, stream, p, h);
+    constexpr int RD = table_rd<C, NF, G, TH>();
+    hipLaunchKernelGGL((k_decode_records_dma<C, NF, G, TH, RD>), dim3((uint32_t)blocks),
+                       dim3(64 * GetShape<NF, G, TH, RD>::WAVES), 0, stream, p, h);
 }
 
-// nf present files -> the k_decode_records_dma<C, NF, G, TH> instantiation
+// nf present files -> the k_decode_records_dma<C, NF, G, TH> instantiation:
+// kTabLaunched, kTabDeclined (not `any_table` and the two-pass path is the
+// faster one, table_one_pass_preferred) or kTabInvalid
+enum { kTabInvalid = 0, kTabLaunched = 1, kTabDeclined = 2 };
 template <int C, int G, int TH, int NF>
-static bool launch_get_nf(int nf, uint64_t n_stripes, const GfApplyParams& p, const HashParams& h,
-                          hipStream_t stream) {
+static int launch_get_nf(int nf, uint64_t n_stripes, const GfApplyParams& p, const HashParams& h, bool any_table,
+                         hipStream_t stream) {
     if constexpr (NF + (TH ? TH : 1) > C + 4) {
-        return false;
+        return kTabInvalid;
     } else {
-        if (nf != NF) return launch_get_nf<C, G, TH, NF + 1>(nf, n_stripes, p, h, stream);
+        if (nf != NF) return launch_get_nf<C, G, TH, NF + 1>(nf, n_stripes, p, h, any_table, stream);
+        if (!any_table && !table_one_pass_preferred(C, (int)p.R, table_rd<C, NF, G, TH>() == 2)) return kTabDeclined;
         const uint64_t blocks = (n_stripes + G - 1) / G;
-        if (blocks > 0x7fffffffull) return false;
+        if (blocks > 0x7fffffffull) return kTabInvalid;
         launch_get<C, NF, G, TH>(blocks, p, h, stream);
-        return true;
+        return kTabLaunched;
     }
 }
 
-using TabLaunch = bool (*)(int nf, int th, uint64_t n_stripes, const GfApplyParams& p, const HashParams& h,
-                           hipStream_t stream);
+using TabLaunch = int (*)(int nf, int th, uint64_t n_stripes, const GfApplyParams& p, const HashParams& h,
+                          bool any_table, hipStream_t stream);
 
 #define RSG_DEC_CAT2(a, b) a##b
 #define RSG_DEC_CAT(a, b) RSG_DEC_CAT2(a, b)
 
 #ifdef RSG_DECODE_C
 // This part's survivor count: GET (th = 0) and heal (th = 1..4 targets).
-bool RSG_DEC_CAT(launch_get_tab_, RSG_DECODE_C)(int nf, int th, uint64_t n_stripes, const GfApplyParams& p,
-                                                const HashParams& h, hipStream_t stream) {
+int RSG_DEC_CAT(launch_get_tab_, RSG_DECODE_C)(int nf, int th, uint64_t n_stripes, const GfApplyParams& p,
+                                               const HashParams& h, bool any_table, hipStream_t stream) {
     constexpr int C = RSG_DECODE_C, G = get_group(C);
     switch (th) {
-        case 0: return launch_get_nf<C, G, 0, C>(nf, n_stripes, p, h, stream);
-        case 1: return launch_get_nf<C, G, 1, C>(nf, n_stripes, p, h, stream);
-        case 2: return launch_get_nf<C, G, 2, C>(nf, n_stripes, p, h, stream);
-        case 3: return launch_get_nf<C, G, 3, C>(nf, n_stripes, p, h, stream);
-        case 4: return launch_get_nf<C, G, 4, C>(nf, n_stripes, p, h, stream);
+        case 0: return launch_get_nf<C, G, 0, C>(nf, n_stripes, p, h, any_table, stream);
+        case 1: return launch_get_nf<C, G, 1, C>(nf, n_stripes, p, h, any_table, stream);
+        case 2: return launch_get_nf<C, G, 2, C>(nf, n_stripes, p, h, any_table, stream);
+        case 3: return launch_get_nf<C, G, 3, C>(nf, n_stripes, p, h, any_table, stream);
+        case 4: return launch_get_nf<C, G, 4, C>(nf, n_stripes, p, h, any_table, stream);
     }
-    return false;
+    return kTabInvalid;
 }
 #else
-bool launch_get_tab_1(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
-bool launch_get_tab_2(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
-bool launch_get_tab_3(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
-bool launch_get_tab_4(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
-bool launch_get_tab_5(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
-bool launch_get_tab_6(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
-bool launch_get_tab_7(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
-bool launch_get_tab_8(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
-bool launch_get_tab_9(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
-bool launch_get_tab_10(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
-bool launch_get_tab_11(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
-bool launch_get_tab_12(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
-bool launch_get_tab_13(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
-bool launch_get_tab_14(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
-bool launch_get_tab_15(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
-bool launch_get_tab_16(int, int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+int launch_get_tab_1(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_tab_2(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_tab_3(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_tab_4(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_tab_5(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_tab_6(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_tab_7(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_tab_8(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_tab_9(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_tab_10(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_tab_11(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_tab_12(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_tab_13(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_tab_14(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_tab_15(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_tab_16(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
 
-static bool launch_get_any(int k, int nf, int th, uint64_t n_stripes, const GfApplyParams& p, const HashParams& h,
-                           hipStream_t stream) {
+static int launch_get_any(int k, int nf, int th, uint64_t n_stripes, const GfApplyParams& p, const HashParams& h,
+                          bool any_table, hipStream_t stream) {
     static const TabLaunch parts[16] = {launch_get_tab_1,  launch_get_tab_2,  launch_get_tab_3,  launch_get_tab_4,
                                         launch_get_tab_5,  launch_get_tab_6,  launch_get_tab_7,  launch_get_tab_8,
                                         launch_get_tab_9,  launch_get_tab_10, launch_get_tab_11, launch_get_tab_12,
                                         launch_get_tab_13, launch_get_tab_14, launch_get_tab_15, launch_get_tab_16};
-    if (k < 1 || k > 16 || th < 0 || th > 4) return false;
-    return parts[k - 1](nf, th, n_stripes, p, h, stream);
+    if (k < 1 || k > 16 || th < 0 || th > 4) return kTabInvalid;
+    return parts[k - 1](nf, th, n_stripes, p, h, any_table, stream);
 }
 
 // Geometries with a one-pass kernel: every k <= 16 with m <= 4 — every set
@@ -260,13 +297,15 @@ bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len) {
 
 // The table kernel against the two-pass path (GF pass over every column, then
 // a verify launch): its GF waves, one per stripe, apply k survivors x R rows
-// of v_perm tables per step, so past some k*R they set the pace.  At 1 MiB
-// blocks, n = 4096 (profiles/r05/geom/): one pass wins up to k*R = 40 — RS(9,4)
-// with 2 lost (R = 4: 36) GET 1.57 vs 2.16 ms, heal 1.61 vs 2.53; RS(13,3)
-// (39) GET 1.84 vs 1.86, heal 1.84 vs 1.98; RS(15,1) (15) GET 0.96 vs 1.64 —
-// and loses beyond: RS(11,4) (44) GET 2.23 vs 2.15 ms, RS(16,4) (64) GET 2.35
-// vs 1.82, heal 2.32 vs 1.96.
-bool table_one_pass_preferred(int k, int R) { return k * R <= 40; }
+// of v_perm tables per step, so past some k*R they set the pace — unless two
+// workgroups share a CU (`two_per_cu`: the 2-slot ring, table_rd), which
+// doubles the GF waves a SIMD interleaves.  At 1 MiB blocks, n = 4096: one
+// workgroup a CU wins up to k*R = 40 (profiles/r05/geom/) — RS(9,4) with 2
+// lost (R = 4: 36) GET 1.57 vs 2.16 ms, heal 1.61 vs 2.53; RS(15,1) (15) GET
+// 0.96 vs 1.64 — and loses beyond: RS(16,4) (64, 9 waves: one a CU) GET 2.35 vs
+// 1.82, heal 2.32 vs 1.96.  Two a CU win past it (profiles/r05/ab_rd2/):
+// RS(11,4) (44) GET 1.50 vs 2.26 ms, RS(13,3) (39) GET 1.25 vs 1.86.
+bool table_one_pass_preferred(int k, int R, bool two_per_cu) { return two_per_cu || k * R <= 40; }
 
 // Patterns with a compile-time XOR network (RS(4,4), RS(6,4), RS(8,4):
 // rs_decode_net.hip; RS(10,4), RS(12,4): rs_decode_netq.hip): the launch's
@@ -341,8 +380,9 @@ hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, 
     p.byte_end = shard_len;
     h.n = n_stripes;
     if (launch_net_if_listed(1, k, m, nf, coef, n_stripes, p, h, stream)) return hipGetLastError();
-    if (!any_table && !table_one_pass_preferred(k, (int)p.R)) return hipErrorNotSupported;
-    if (!launch_get_any(k, nf, targets, n_stripes, p, h, stream)) return hipErrorInvalidValue;
+    const int r = launch_get_any(k, nf, targets, n_stripes, p, h, any_table, stream);
+    if (r == kTabDeclined) return hipErrorNotSupported;
+    if (r != kTabLaunched) return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
@@ -356,8 +396,9 @@ hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int k, int m
     p.byte_end = shard_len;
     h.n = n_stripes;
     if (launch_net_if_listed(0, k, m, nf, coef, n_stripes, p, h, stream)) return hipGetLastError();
-    if (!any_table && !table_one_pass_preferred(k, (int)p.R)) return hipErrorNotSupported;
-    if (!launch_get_any(k, nf, 0, n_stripes, p, h, stream)) return hipErrorInvalidValue;
+    const int r = launch_get_any(k, nf, 0, n_stripes, p, h, any_table, stream);
+    if (r == kTabDeclined) return hipErrorNotSupported;
+    if (r != kTabLaunched) return hipErrorInvalidValue;
     return hipGetLastError();
 }
 #endif  // RSG_DECODE_C

@@ -151,8 +151,9 @@ hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int k, int m
 // caller takes the two-pass path.
 bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len);
 // The run-time-table one-pass kernel against the two-pass path for k
-// survivors and R rows (rebuilt / healed + compared): rs_decode.hip.
-bool table_one_pass_preferred(int k, int R);
+// survivors and R rows (rebuilt / healed + compared), two_per_cu: the launch
+// shape fits two workgroups a CU (rs_decode.hip).
+bool table_one_pass_preferred(int k, int R, bool two_per_cu);
 hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, int nf, int targets,
                                    uint64_t shard_len, uint64_t n_stripes, const uint8_t* coef, bool any_table,
                                    hipStream_t stream);

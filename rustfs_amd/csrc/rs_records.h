@@ -174,12 +174,14 @@ __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t 
     for (uint32_t s = 0; s + 1 < steps; ++s) {
         issued = dma_step(s + D - 1 < steps ? s + D - 1 : steps - 1);  // into the slot step s-1 used
         const bool fill = ragged && s + 2 == steps;  // the ragged last step is next
-        if (fill) tail_load();
         uint64_t w[16];
         dma::read16(ring_base + (s % D) * L::DSLOT + roff, w);
 #pragma unroll
         for (int t = 0; t < 16; ++t) hhq_update(st, w[t]);
-        if (fill) tail_store();
+        if (fill) {  // after the packets: tlo/thi and w[] never live together (78-90 VGPRs, not 103)
+            tail_load();
+            tail_store();
+        }
         wait_next(issued);
         lds_barrier();  // B(s+1)
     }
@@ -212,12 +214,14 @@ __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t 
 // one wave fewer — RS(12,4)'s heal of one data + one parity shard: 8 waves
 // instead of 9, which is what lets two workgroups share a CU (5 waves on a
 // SIMD left 96 registers a wave: 12 spilled).  Ring quads walk their records
-// exactly as records_hash_wave (same DMA pipeline and barriers, XB = 1); target
-// quad tq hashes target row stream tq (row tq / G of stripe tq % G) two steps
-// behind the DMA from the target area (TNS slots of TSLOT bytes at `trow`, the
-// rows at pitch PP), clears what it read, and at the end writes the target
-// record's digest header (BitrotWriter::write).  steps + 2 barriers.
-template <int NF, int G, int RD, int TTH, int TNS, uint32_t TSLOT>
+// exactly as records_hash_wave (same DMA pipeline and barriers, XB = LAG - 1);
+// target quad tq hashes target row stream tq (row tq / G of stripe tq % G) LAG
+// steps behind the DMA from the target area (TNS slots of TSLOT bytes at
+// `trow`, the rows at pitch PP) — ZERO: clearing what it read (the network
+// kernels' accumulators; LAG 1: the table kernel's GF waves write whole rows) —
+// and at the end writes the target record's digest header
+// (BitrotWriter::write).  steps + LAG barriers.
+template <int NF, int G, int RD, int TTH, int TNS, uint32_t TSLOT, int LAG = 2, bool ZERO = true>
 __device__ __forceinline__ void records_hash_target_wave(const GfApplyParams& p, const HashParams& h, uint8_t* ring,
                                                          uint8_t* trow, uint32_t hw, uint32_t steps, uint64_t s0) {
     using dma::CH;
@@ -301,12 +305,13 @@ __device__ __forceinline__ void records_hash_target_wave(const GfApplyParams& p,
         else __builtin_amdgcn_s_waitcnt(vmcnt_imm((D - 2) * NDI));
     };
     // interval i (after B(i)): ring quads absorb ring step i (i < steps), target
-    // quads target step i - 2 (2 <= i < steps + 2); `rag`: this quad's step is
-    // the walk's ragged last one (its whole packets, then the remainder packet)
+    // quads target step i - LAG (LAG <= i < steps + LAG); `rag`: this quad's
+    // step is the walk's ragged last one (its whole packets, then the remainder
+    // packet)
     auto absorb = [&](uint32_t i) {
-        const bool t_act = ton && i >= 2u;
+        const bool t_act = ton && i >= (uint32_t)LAG;
         const bool act = quad_on ? i < steps : t_act;
-        const uint32_t ts = i - 2u;
+        const uint32_t ts = i - (uint32_t)LAG;
         const uint32_t a = quad_on ? ring_base + (i % D) * L::DSLOT + roff : trow_base + (ts % TNS) * TSLOT + troff;
         const bool rag = ragged && (quad_on ? i + 1 == steps : ts + 1 == steps);
         uint64_t w[16];
@@ -322,7 +327,9 @@ __device__ __forceinline__ void records_hash_target_wave(const GfApplyParams& p,
                 hhq_remainder(st, tb - 8 * q + full * 32, tail % 32, q);
             }
         }
-        if (t_act) dma::zero16(a);
+        if constexpr (ZERO) {
+            if (t_act) dma::zero16(a);
+        }
     };
     bool issued = true;
 #pragma unroll
@@ -337,9 +344,11 @@ __device__ __forceinline__ void records_hash_target_wave(const GfApplyParams& p,
     for (uint32_t s = 0; s + 1 < steps; ++s) {
         issued = dma_step(s + D - 1 < steps ? s + D - 1 : steps - 1);
         const bool fill = ragged && s + 2 == steps;
-        if (fill) tail_load();
         absorb(s);
-        if (fill) tail_store();
+        if (fill) {
+            tail_load();
+            tail_store();
+        }
         wait_next(issued);
         lds_barrier();  // B(s+1)
     }
@@ -351,9 +360,11 @@ __device__ __forceinline__ void records_hash_target_wave(const GfApplyParams& p,
         lds_barrier();  // B(steps)
     }
     __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
-    absorb(steps);  // target step steps - 2
-    lds_barrier();  // B(steps+1): the last target rows published
-    absorb(steps + 1);  // target step steps - 1
+#pragma unroll
+    for (int l = 0; l < LAG; ++l) {  // target steps steps - LAG .. steps - 1
+        if (l > 0) lds_barrier();  // B(steps+l): the last target rows published
+        absorb(steps + l);
+    }
     // ring quads: verify before use (bitrot.rs:227-247); target quads: the
     // target record's digest header (BitrotWriter::write)
     const uint64_t d = hhq_digest(st, q);

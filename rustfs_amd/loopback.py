@@ -28,7 +28,8 @@ Commit: a PUT writes every shard file into a directory of its own version id
 (the reference's per-version data_dir, which xl.meta points to), and only once
 the write quorum holds replaces each disk's meta.json (naming that version and
 its modification time) — one atomic rename switches a disk's part and
-metadata together — then removes the disk's other version directories.  A
+metadata together — then removes the version directory that meta.json named
+before (a concurrent PUT's uncommitted directory is left to that PUT).  A
 crash or an interleaved PUT can leave a disk on either version, never with one
 version's part under another's metadata.  A disk whose writer was dropped
 loses its previous version (heal rebuilds it), and a PUT that fails leaves the
@@ -205,17 +206,21 @@ class LocalErasureSet:
         for i in range(self.k + self.m):
             shutil.rmtree(os.path.join(self.dirs[i], name, version), ignore_errors=True)
 
-    def _drop_other_versions(self, i: int, name: str, keep: Optional[str]) -> None:
-        """Remove disk i's version directories other than `keep` (after its
-        meta.json switched: nothing reads them any more)."""
-        base = os.path.join(self.dirs[i], name)
+    def _disk_version(self, i: int, name: str) -> Optional[str]:
+        """The version disk i's meta.json names (None: none committed)."""
         try:
-            entries = os.listdir(base)
-        except OSError:
-            return
-        for d in entries:
-            if d != keep and os.path.isdir(os.path.join(base, d)):
-                shutil.rmtree(os.path.join(base, d), ignore_errors=True)
+            with open(os.path.join(self.dirs[i], name, "meta.json")) as f:
+                return json.load(f).get("version")
+        except (OSError, ValueError):
+            return None
+
+    def _drop_version(self, i: int, name: str, version: Optional[str]) -> None:
+        """Remove one version's directory on disk i — the one its meta.json
+        named before a switch (nothing reads it any more).  Only that one: a
+        concurrent PUT's uncommitted directory stays (that PUT commits or
+        discards it)."""
+        if version:
+            shutil.rmtree(os.path.join(self.dirs[i], name, version), ignore_errors=True)
 
     def _commit(self, name: str, size: int, version: str, skip=()) -> dict:
         """Switch each disk to the new version: its meta.json is replaced in
@@ -228,15 +233,18 @@ class LocalErasureSet:
                 "shard_size": e.shard_size(), "algorithm": self.algo.name, "version": version,
                 "mod_time": time.time_ns()}
         for i in range(self.k + self.m):
+            old = self._disk_version(i, name)
             if i in skip:
                 try:
                     os.unlink(os.path.join(self.dirs[i], name, "meta.json"))
                 except OSError:
                     pass
-                self._drop_other_versions(i, name, None)
+                self._drop_version(i, name, old)
+                self._drop_version(i, name, version)  # the dropped writer's partial part
                 continue
             self._write_meta_file(i, name, meta)
-            self._drop_other_versions(i, name, version)
+            if old != version:
+                self._drop_version(i, name, old)
         return meta
 
     def _write_meta_file(self, i: int, name: str, meta: dict) -> None:
@@ -379,8 +387,10 @@ class LocalErasureSet:
             with open(tmp, "wb") as f:
                 f.write(bytes(out[i]))
             os.replace(tmp, path)
+            old = self._disk_version(i, name)
             self._write_meta_file(i, name, meta)
-            self._drop_other_versions(i, name, meta["version"])
+            if old != meta["version"]:
+                self._drop_version(i, name, old)
 
     # --------------------------------------------------------------- VERIFY
     def verify_object(self, name: str) -> List[int]:

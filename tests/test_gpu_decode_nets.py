@@ -324,7 +324,9 @@ GEOS = {(6, 4): (11, 1001), (10, 4): (9, 1002), (4, 4): (13, 1003),
         # RS(7,1), RS(13,3), RS(1,1) (2 drives) — ragged S, records at every
         # alignment mod 8
         (5, 4): (19, 1005), (11, 4): (9, 1006), (15, 1): (11, 1007), (3, 2): (17, 999), (7, 1): (19, 1011),
-        (13, 3): (5, 1013), (1, 1): (9, 997), (9, 4): (7, 1019)}
+        (13, 3): (5, 1013), (1, 1): (9, 997), (9, 4): (7, 1019),
+        # C = 14 heals with the target hashing merged into the last hash wave
+        (14, 2): (7, 1021)}
 LISTED4 = _listed("rs44_decode_nets.h", 8)
 LISTED6 = _listed("rs64_decode_nets.h", 10)
 LISTED10 = _listed("rs104_decode_nets.h", 14)
@@ -443,7 +445,7 @@ def test_rs10_every_listed_pattern(gpu, oracle, records10, one_pass, heal, lost)
     _geo_case(oracle, 10, records10, heal, lost, 4)
 
 
-TABLE_GEOS = [(5, 4), (11, 4), (15, 1), (3, 2), (7, 1), (13, 3), (1, 1), (9, 4)]
+TABLE_GEOS = [(5, 4), (11, 4), (15, 1), (3, 2), (7, 1), (13, 3), (1, 1), (9, 4), (14, 2)]
 TABLE_CASES = [(k, m, heal, lost) for k, m in TABLE_GEOS for heal, lost in _every_pattern(k, m)]
 
 

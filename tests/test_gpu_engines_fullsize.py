@@ -1,6 +1,7 @@
 """The record engines at the bench line's full sizes (the pattern
 tests run n <= 19 stripes; the line checked one stripe): RS(8,4) at S = 131072
-and RS(12,4) at S = 87382 (ragged walks, records at every even offset), n =
+RS(12,4) at S = 87382 and RS(11,4) at S = 95326 (ragged walks, records at
+every even offset), n =
 4096 BitrotWriter records per file, through the one-pass kernels the engine
 picks at that scale.
 
@@ -36,7 +37,9 @@ def _records(torch, k, m, S, n, seed):
     return e, st, dig, files
 
 
-@pytest.mark.parametrize("k,S", [(8, 131072), (12, 87382)])
+# RS(11,4): the run-time-table kernel on the 2-slot ring (two workgroups a CU),
+# its heal hashing the targets in the last hash wave (round 5)
+@pytest.mark.parametrize("k,S", [(8, 131072), (12, 87382), (11, 95326)])
 def test_engines_every_stripe_at_bench_size(gpu, oracle, k, S):
     import torch
     m, n = 4, 4096
