@@ -15,7 +15,7 @@ namespace rsg {
 
 // ---------------------------------------------------------------------------
 // One-pass degraded GET (rsg_decode_records_dev, a data disk lost) for
-// RS(k, m) with k <= 16 and m <= 4: every present record of G
+// RS(k, m) with k <= 16 and m <= 4 (and EC:5..8, below): every present record of G
 // stripes is verified, the missing data shards rebuilt from the first C = k
 // present (survivors), the present data shards copied through and the
 // surplus parity compared with its re-derived value — reading each present
@@ -26,8 +26,9 @@ namespace rsg {
 // one per stripe (survivor rows from the ring: rebuilt rows stored to the
 // output, surplus rows compared against their ring rows, survivor data
 // copied to the output).  One barrier per step.  The host redoes the stripes
-// whose verify flags differ from the assumed pattern.  At most m <= 4 rows
-// (missing data + surplus parity, or heal targets + surplus) are ever needed.
+// whose verify flags differ from the assumed pattern.  At most m rows
+// (missing data + surplus parity, or heal targets + surplus) are ever needed:
+// RM = 4 table slots, 8 for m > 4.
 //   p: tab[r][c] over the C survivors (present files 0..C-1 of the launch),
 //      rows [0, n_store) rebuilt into out_base + s*out_stripe_stride +
 //      out_off[r], rows [n_store, R) compared with present file 8 + (r -
@@ -64,18 +65,19 @@ struct GetShape : RecRing<NF, G, TH> {
     static constexpr int WPE = RD == 2 ? (2 * WAVES + 3) / 4 : 1;
 };
 
-template <int C, int NF, int G, int TH, int RD = dma::D>
+template <int C, int NF, int G, int TH, int RD = dma::D, int RM = 4>
 __global__ __launch_bounds__((64 * GetShape<NF, G, TH, RD>::WAVES))
 __attribute__((amdgpu_waves_per_eu(GetShape<NF, G, TH, RD>::WPE))) void k_decode_records_dma(const GfApplyParams p,
                                                                                             const HashParams h) {
-    static_assert(C >= 1 && C <= kMaxC && NF >= C && NF <= C + 4 && TH <= 4 && NF + TH <= C + 4, "RS(C, <= 4)");
+    static_assert(C >= 1 && C <= kMaxC && (RM == 4 || RM == 8) && RM <= kMaxR && NF >= C && NF <= C + RM &&
+                      TH <= RM && NF + TH <= C + RM,
+                  "RS(C, <= RM)");
     using dma::CH;
     using dma::IP;
     using dma::PP;
     constexpr int D = RD;
     using L = GetShape<NF, G, TH, RD>;
     constexpr int SPW = L::SPW, HS = L::HS;
-    constexpr int RM = 4;
     __shared__ __attribute__((aligned(16))) uint8_t ring[D * L::DSLOT];
     __shared__ __attribute__((aligned(16))) uint8_t tabs[C * RM * 32];
     __shared__ __attribute__((aligned(16))) uint8_t trow[TH ? 2 * L::TSLOT : 16];
@@ -194,18 +196,18 @@ __attribute__((amdgpu_waves_per_eu(GetShape<NF, G, TH, RD>::WPE))) void k_decode
 // (RS(16,4) GET, RS(15,4) GET, RS(14,4) heal) fit two a CU at 96 registers
 // too, but measured no better than on 3 slots, and slower than two passes
 // (GET RS(16,4) 2.16 vs 1.78 ms, RS(15,4) 2.20 vs 2.10; profiles/r05/ab_rd2/)
-template <int C, int NF, int G, int TH>
+template <int C, int NF, int G, int TH, int RM = 4>
 constexpr int table_rd() {
-    return (G == 4 && GetShape<NF, G, TH, 2>::LDS + C * 4 * 32 <= 80 * 1024 - 512 &&
+    return (G == 4 && GetShape<NF, G, TH, 2>::LDS + C * RM * 32 <= 80 * 1024 - 512 &&
             GetShape<NF, G, TH, 2>::WAVES <= 8)
                ? 2
                : dma::D;
 }
 
-template <int C, int NF, int G, int TH = 0>
+template <int C, int NF, int G, int TH = 0, int RM = 4>
 static void launch_get(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
-    constexpr int RD = table_rd<C, NF, G, TH>();
-    hipLaunchKernelGGL((k_decode_records_dma<C, NF, G, TH, RD>), dim3((uint32_t)blocks),
+    constexpr int RD = table_rd<C, NF, G, TH, RM>();
+    hipLaunchKernelGGL((k_decode_records_dma<C, NF, G, TH, RD, RM>), dim3((uint32_t)blocks),
                        dim3(64 * GetShape<NF, G, TH, RD>::WAVES), 0, stream, p, h);
 }
 
@@ -234,7 +236,56 @@ using TabLaunch = int (*)(int nf, int th, uint64_t n_stripes, const GfApplyParam
 #define RSG_DEC_CAT2(a, b) a##b
 #define RSG_DEC_CAT(a, b) RSG_DEC_CAT2(a, b)
 
-#ifdef RSG_DECODE_C
+using WideLaunch = int (*)(int m, int nf, int th, uint64_t n_stripes, const GfApplyParams& p, const HashParams& h,
+                           bool any_table, hipStream_t stream);
+
+#if defined(RSG_DECODE_C) && defined(RSG_DECODE_WIDE)
+// Explicit storage classes EC:5..8 (m > 4 parity shards, m <= k, k + m <= 16
+// drives: storageclass.rs:480-498, fileinfo.rs:38): the table kernel with up
+// to RM = 8 rows (missing data + surplus parity, or heal targets + surplus)
+// for every one- and two-loss pattern — GET with one or two files absent,
+// heal of one target (the other files present, or one more absent) or two —
+// in 4-stripe workgroups (the ring of up to 15 files would not fit 8).  Other
+// patterns take the two-pass path.
+template <int C, int NF, int TH>
+static int launch_wide(uint64_t n_stripes, const GfApplyParams& p, const HashParams& h, bool any_table,
+                       hipStream_t stream) {
+    constexpr int G = 4, RM = 8;
+    if (!any_table && !table_one_pass_preferred(C, (int)p.R, table_rd<C, NF, G, TH, RM>() == 2)) return kTabDeclined;
+    const uint64_t blocks = (n_stripes + G - 1) / G;
+    if (blocks > 0x7fffffffull) return kTabInvalid;
+    launch_get<C, NF, G, TH, RM>(blocks, p, h, stream);
+    return kTabLaunched;
+}
+
+template <int C, int M>
+static int launch_wide_m(int nf, int th, uint64_t n_stripes, const GfApplyParams& p, const HashParams& h,
+                         bool any_table, hipStream_t stream) {
+    if constexpr (M > C || C + M > 16) {
+        return kTabInvalid;
+    } else {
+        constexpr int T = C + M;
+        if (th == 0 && nf == T - 1) return launch_wide<C, T - 1, 0>(n_stripes, p, h, any_table, stream);
+        if (th == 0 && nf == T - 2) return launch_wide<C, T - 2, 0>(n_stripes, p, h, any_table, stream);
+        if (th == 1 && nf == T - 1) return launch_wide<C, T - 1, 1>(n_stripes, p, h, any_table, stream);
+        if (th == 1 && nf == T - 2) return launch_wide<C, T - 2, 1>(n_stripes, p, h, any_table, stream);
+        if (th == 2 && nf == T - 2) return launch_wide<C, T - 2, 2>(n_stripes, p, h, any_table, stream);
+        return kTabInvalid;
+    }
+}
+
+int RSG_DEC_CAT(launch_get_wide_, RSG_DECODE_C)(int m, int nf, int th, uint64_t n_stripes, const GfApplyParams& p,
+                                                const HashParams& h, bool any_table, hipStream_t stream) {
+    constexpr int C = RSG_DECODE_C;
+    switch (m) {
+        case 5: return launch_wide_m<C, 5>(nf, th, n_stripes, p, h, any_table, stream);
+        case 6: return launch_wide_m<C, 6>(nf, th, n_stripes, p, h, any_table, stream);
+        case 7: return launch_wide_m<C, 7>(nf, th, n_stripes, p, h, any_table, stream);
+        case 8: return launch_wide_m<C, 8>(nf, th, n_stripes, p, h, any_table, stream);
+    }
+    return kTabInvalid;
+}
+#elif defined(RSG_DECODE_C)
 // This part's survivor count: GET (th = 0) and heal (th = 1..4 targets).
 int RSG_DEC_CAT(launch_get_tab_, RSG_DECODE_C)(int nf, int th, uint64_t n_stripes, const GfApplyParams& p,
                                                const HashParams& h, bool any_table, hipStream_t stream) {
@@ -265,9 +316,22 @@ int launch_get_tab_13(int, int, uint64_t, const GfApplyParams&, const HashParams
 int launch_get_tab_14(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
 int launch_get_tab_15(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
 int launch_get_tab_16(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_wide_5(int, int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_wide_6(int, int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_wide_7(int, int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_wide_8(int, int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_wide_9(int, int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_wide_10(int, int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+int launch_get_wide_11(int, int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
 
-static int launch_get_any(int k, int nf, int th, uint64_t n_stripes, const GfApplyParams& p, const HashParams& h,
-                          bool any_table, hipStream_t stream) {
+static int launch_get_any(int k, int m, int nf, int th, uint64_t n_stripes, const GfApplyParams& p,
+                          const HashParams& h, bool any_table, hipStream_t stream) {
+    if (m > 4) {
+        static const WideLaunch wide[7] = {launch_get_wide_5, launch_get_wide_6,  launch_get_wide_7, launch_get_wide_8,
+                                           launch_get_wide_9, launch_get_wide_10, launch_get_wide_11};
+        if (k < 5 || k > 11 || m > 8 || th < 0 || th > 2) return kTabInvalid;
+        return wide[k - 5](m, nf, th, n_stripes, p, h, any_table, stream);
+    }
     static const TabLaunch parts[16] = {launch_get_tab_1,  launch_get_tab_2,  launch_get_tab_3,  launch_get_tab_4,
                                         launch_get_tab_5,  launch_get_tab_6,  launch_get_tab_7,  launch_get_tab_8,
                                         launch_get_tab_9,  launch_get_tab_10, launch_get_tab_11, launch_get_tab_12,
@@ -282,16 +346,28 @@ static int launch_get_any(int k, int nf, int th, uint64_t n_stripes, const GfApp
 // redundancy class's one parity shard (storageclass.rs:99, 326-331) and
 // explicit EC:1..4 — any shard length (a ragged last step, rs_records.h
 // walk_tail).
-static bool one_pass_geometry(int k, int m, uint64_t shard_len) {
-    return k >= 1 && k <= 16 && m >= 1 && m <= 4 && shard_len >= 1 &&
-           (shard_len + dma::CH - 1) / dma::CH <= 0xffffffffull;
+static bool walk_length_ok(uint64_t shard_len) {
+    return shard_len >= 1 && (shard_len + dma::CH - 1) / dma::CH <= 0xffffffffull;
 }
+static bool one_pass_geometry(int k, int m, uint64_t shard_len) {
+    return k >= 1 && k <= 16 && m >= 1 && m <= 4 && walk_length_ok(shard_len);
+}
+// ... and the explicit classes EC:5..8 (m <= k, k + m <= 16 drives:
+// storageclass.rs:480-498) for their one- and two-loss patterns
+// (launch_get_wide_C above)
+static bool wide_geometry(int k, int m, uint64_t shard_len) {
+    return m >= 5 && m <= 8 && m <= k && k + m <= 16 && walk_length_ok(shard_len);
+}
+static int rows_max(int m) { return m > 4 ? 8 : 4; }
 
 bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len) {
+    if (wide_geometry(k, m, shard_len)) return nf >= k + m - 2 && nf < k + m;
     return one_pass_geometry(k, m, shard_len) && nf >= k && nf < k + m;
 }
 
 bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len) {
+    if (wide_geometry(k, m, shard_len))
+        return (targets == 1 && nf >= k + m - 2 && nf <= k + m - 1) || (targets == 2 && nf == k + m - 2);
     return one_pass_geometry(k, m, shard_len) && nf >= k && targets >= 1 && nf + targets <= k + m;
 }
 
@@ -372,7 +448,8 @@ hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, 
                                    uint64_t shard_len, uint64_t n_stripes, const uint8_t* coef, bool any_table,
                                    hipStream_t stream) {
     p.wave_prio = dma_prio();
-    if (!heal_one_pass_shape(k, m, nf, targets, shard_len) || (int)p.C != k || n_stripes == 0 || p.R > 4 ||
+    if (!heal_one_pass_shape(k, m, nf, targets, shard_len) || (int)p.C != k || n_stripes == 0 ||
+        p.R > (uint32_t)rows_max(m) ||
         p.n_store != (uint32_t)targets || p.copy_mask || !dma_records_walkable(h) ||
         p.out_stripe_stride != h.stripe_stride)
         return hipErrorInvalidValue;
@@ -380,7 +457,7 @@ hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, 
     p.byte_end = shard_len;
     h.n = n_stripes;
     if (launch_net_if_listed(1, k, m, nf, coef, n_stripes, p, h, stream)) return hipGetLastError();
-    const int r = launch_get_any(k, nf, targets, n_stripes, p, h, any_table, stream);
+    const int r = launch_get_any(k, m, nf, targets, n_stripes, p, h, any_table, stream);
     if (r == kTabDeclined) return hipErrorNotSupported;
     if (r != kTabLaunched) return hipErrorInvalidValue;
     return hipGetLastError();
@@ -389,14 +466,15 @@ hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, 
 hipError_t launch_decode_records_dma(GfApplyParams p, HashParams h, int k, int m, int nf, uint64_t shard_len,
                                      uint64_t n_stripes, const uint8_t* coef, bool any_table, hipStream_t stream) {
     p.wave_prio = dma_prio();
-    if (!decode_dma_supported(k, m, nf, shard_len) || (int)p.C != k || n_stripes == 0 || p.R > 4 ||
+    if (!decode_dma_supported(k, m, nf, shard_len) || (int)p.C != k || n_stripes == 0 ||
+        p.R > (uint32_t)rows_max(m) ||
         p.n_store > p.R || !dma_records_walkable(h))
         return hipErrorInvalidValue;
     p.units = (uint32_t)((shard_len + dma::CH - 1) / dma::CH);
     p.byte_end = shard_len;
     h.n = n_stripes;
     if (launch_net_if_listed(0, k, m, nf, coef, n_stripes, p, h, stream)) return hipGetLastError();
-    const int r = launch_get_any(k, nf, 0, n_stripes, p, h, any_table, stream);
+    const int r = launch_get_any(k, m, nf, 0, n_stripes, p, h, any_table, stream);
     if (r == kTabDeclined) return hipErrorNotSupported;
     if (r != kTabLaunched) return hipErrorInvalidValue;
     return hipGetLastError();

@@ -134,7 +134,8 @@ hipError_t launch_encode_hash_net12(GfApplyParams p, HashParams h, uint64_t shar
                                     hipStream_t stream);
 // One-pass degraded GET (k_decode_records_dma) for RS(k, m), k <= 16, m <= 4,
 // any shard length (a ragged last step), over nf (k..k+m-1) present record
-// files: false if the shape is not supported.
+// files — and EC:5..8 (m <= k, k + m <= 16) with one or two files absent:
+// false if the shape is not supported.
 bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len);
 // coef: the launch's R x k coefficient rows (host memory, row-major), matched
 // against the compile-time XOR-network patterns (rs_decode_net.hip); may be null.
@@ -233,7 +234,8 @@ RSG_NET12_PART_DECL(6)
 RSG_NET12_PART_DECL(7)
 #undef RSG_NET12_PART_DECL
 // One-pass heal possible for this shape (the table kernel takes every k <=
-// 16, m <= 4; which kernel runs is decided at launch).
+// 16, m <= 4, and EC:5..8's heals of one or two targets; which kernel runs is
+// decided at launch).
 bool heal_one_pass_shape(int k, int m, int nf, int targets, uint64_t shard_len);
 hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                     hipStream_t stream);

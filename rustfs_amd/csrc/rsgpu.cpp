@@ -1488,7 +1488,7 @@ int launch_get_one_pass(RecJob& j, const std::vector<int>& files) {
             ++R;
         }
     }
-    if (R > 4 || R == 0) return RSG_ERR_UNSUPPORTED;
+    if (R > (j.m > 4 ? 8 : 4) || R == 0) return RSG_ERR_UNSUPPORTED;
     if (R > n_store) j.any_verify = true;
     for (int r = 0; r < R; ++r)
         for (int c = 0; c < k; ++c) coef_tables(coef[(size_t)r * k + c], p.tab[r][c]);
@@ -1689,7 +1689,7 @@ int launch_heal_one_pass(RecJob& j, const std::vector<int>& files, const std::ve
     }
     const int n_store = R;
     for (int f = k; f < (int)files.size(); ++f) {  // present non-survivors: parity, ascending
-        if (R >= 4) return RSG_ERR_UNSUPPORTED;
+        if (R >= (j.m > 4 ? 8 : 4)) return RSG_ERR_UNSUPPORTED;
         coef.resize((size_t)(R + 1) * k);
         plan_row(*j.cd, *plan, files[f], &coef[(size_t)R * k]);
         ++R;

@@ -326,7 +326,11 @@ GEOS = {(6, 4): (11, 1001), (10, 4): (9, 1002), (4, 4): (13, 1003),
         (5, 4): (19, 1005), (11, 4): (9, 1006), (15, 1): (11, 1007), (3, 2): (17, 999), (7, 1): (19, 1011),
         (13, 3): (5, 1013), (1, 1): (9, 997), (9, 4): (7, 1019),
         # C = 14 heals with the target hashing merged into the last hash wave
-        (14, 2): (7, 1021)}
+        (14, 2): (7, 1021),
+        # explicit classes EC:5..8 (m > 4, m <= k, k + m <= 16 drives,
+        # storageclass.rs:480-498): the table kernel with 8 row slots
+        (8, 8): (7, 1031), (10, 6): (5, 1033), (5, 5): (9, 1035), (11, 5): (5, 1037), (7, 7): (7, 1039),
+        (9, 7): (5, 1041)}
 LISTED4 = _listed("rs44_decode_nets.h", 8)
 LISTED6 = _listed("rs64_decode_nets.h", 10)
 LISTED10 = _listed("rs104_decode_nets.h", 14)
@@ -445,7 +449,8 @@ def test_rs10_every_listed_pattern(gpu, oracle, records10, one_pass, heal, lost)
     _geo_case(oracle, 10, records10, heal, lost, 4)
 
 
-TABLE_GEOS = [(5, 4), (11, 4), (15, 1), (3, 2), (7, 1), (13, 3), (1, 1), (9, 4), (14, 2)]
+TABLE_GEOS = [(5, 4), (11, 4), (15, 1), (3, 2), (7, 1), (13, 3), (1, 1), (9, 4), (14, 2),
+              (8, 8), (10, 6), (5, 5), (11, 5), (7, 7), (9, 7)]
 TABLE_CASES = [(k, m, heal, lost) for k, m in TABLE_GEOS for heal, lost in _every_pattern(k, m)]
 
 
@@ -463,19 +468,22 @@ def table_records(gpu, oracle):
 def test_table_patterns_cover_every_loss():
     """RS(5,4): 5 + (36 - 6) GET (every pair but the 6 all-parity ones) and
     9 + 36 heal patterns; RS(15,1): 15 GET and 16 heal (one parity shard: one
-    loss at most); RS(11,4) 11 + (105 - 6) and 15 + 105."""
+    loss at most); RS(11,4) 11 + (105 - 6) and 15 + 105; RS(8,8) (EC:8 on
+    16 drives) 8 + (120 - 28) and 16 + 120."""
     def count(k, m, heal):
         return len([x for x in _every_pattern(k, m) if x[0] == heal])
     assert (count(5, 4, 0), count(5, 4, 1)) == (5 + 30, 9 + 36)
     assert (count(15, 1, 0), count(15, 1, 1)) == (15, 16)
     assert (count(11, 4, 0), count(11, 4, 1)) == (11 + 99, 15 + 105)
+    assert (count(8, 8, 0), count(8, 8, 1)) == (8 + 92, 16 + 120)
 
 
 @pytest.mark.parametrize("k,m,heal,lost", TABLE_CASES, ids=str)
 def test_table_kernel_every_pattern(gpu, oracle, table_records, one_pass, k, m, heal, lost):
     """The run-time-table one-pass kernel (k_decode_records_dma, one part per
-    survivor count) at the data counts without networks: every one- and
-    two-shard loss, GET in both forms and heal, ragged S."""
+    survivor count) at the data counts without networks and at m > 4 (8 row
+    slots): every one- and two-shard loss, GET in both forms and heal, ragged
+    S."""
     _geo_case(oracle, k, table_records(k, m), heal, lost, m)
 
 

@@ -1,5 +1,6 @@
 """One-pass against two-pass GET / heal at the geometries without a network
-(round 5: the run-time-table one-pass kernel for every k <= 16, m <= 4), at
+(round 5: the run-time-table one-pass kernel for every k <= 16, m <= 4, and
+EC:5..8's one- and two-loss patterns), at
 1 MiB blocks (S = ceil(1 MiB / k)), n stripes of BitrotWriter records on the
 device.  For each geometry: the in-place GET with the most data shards lost
 that m allows (two, or one at m = 1), and the heal of one data + one parity
