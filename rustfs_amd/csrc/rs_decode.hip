@@ -93,13 +93,16 @@ __attribute__((amdgpu_waves_per_eu(GetShape<NF, G, TH, RD>::WPE))) void k_decode
     }
     // (the tables are published by B(0), which every wave passes before use)
 
-    if (TH && wave >= (uint32_t)(L::HW + SPW)) {
-        records_target_hasher<G, TH>(p, h, trow, wave - L::HW - SPW, steps, s0);
-        return;
+    if constexpr (TH > 0 && !L::MERGE) {
+        if (wave >= (uint32_t)(L::HW + SPW)) {
+            records_target_hasher<G, TH, 1, false, 2, 0, false, L::WPE>(&karg_gf(), &karg_hash(), trow,
+                                                                       wave - L::HW - SPW, steps, s0);
+            return;
+        }
     }
     if constexpr (L::MERGE) {
         if (wave == (uint32_t)(L::HW - 1)) {  // the last hash wave hashes the target rows too
-            records_hash_target_wave<NF, G, RD, TH, 2, L::TSLOT, 1, false>(p, h, ring, trow, wave, steps, s0);
+            records_hash_target_wave<NF, G, RD, TH, 2, L::TSLOT, 1, false, L::WPE>(&karg_gf(), &karg_hash(), ring, trow, wave, steps, s0);
             return;
         }
     }
@@ -187,7 +190,7 @@ __attribute__((amdgpu_waves_per_eu(GetShape<NF, G, TH, RD>::WPE))) void k_decode
         return;
     }
     // ------------------------- DMA + verify-hash wave -------------------------
-    records_hash_wave<NF, G, 0, RD>(h, p.wave_prio, ring, wave, steps, s0);
+    records_hash_wave<NF, G, 0, RD, false, L::WPE>(&karg_hash(), p.wave_prio, ring, wave, steps, s0);
 }
 
 // 4-stripe workgroups (C > 8) on a 2-slot ring where it fits half a CU's LDS

@@ -230,14 +230,14 @@ __global__ __launch_bounds__((64 * NetShape<NF, TH>::WAVES)) void RSG_NET_NAME(k
     const uint32_t steps = p.units;
     const uint64_t s0 = (uint64_t)blockIdx.x * L::SPW;
     if (TH && wave >= (uint32_t)(L::HW + L::NG)) {
-        records_target_hasher<8, TH>(p, h, trow, wave - L::HW - L::NG, steps, s0);
+        records_target_hasher<8, TH>(&karg_gf(), &karg_hash(), trow, wave - L::HW - L::NG, steps, s0);
         return;
     }
     if (wave >= (uint32_t)L::HW) {
         net_wave<PID, NF, TH>(p, h.n, steps, s0, wave - L::HW, ring, trow);
         return;
     }
-    records_hash_wave<NF, 8>(h, p.wave_prio, ring, wave, steps, s0);
+    records_hash_wave<NF, 8>(&karg_hash(), p.wave_prio, ring, wave, steps, s0);
 }
 
 using NetLaunch = void (*)(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream);

@@ -319,9 +319,9 @@ __attribute__((amdgpu_waves_per_eu(NetQShape<NF, TH, RDX, ENC>::WPE))) void RSG_
     const uint64_t s0 = (uint64_t)blockIdx.x * L::SPW;
     if (TH && wave >= (uint32_t)(L::HW + kNQ)) {
         if constexpr (L::TR)  // the target rows in their exchange slots, cleared once hashed
-            records_target_hasher<4, TH, 2, ENC, L::NTS, L::TSLOTX, true>(p, h, xbuf, wave - L::HW - kNQ, steps, s0);
+            records_target_hasher<4, TH, 2, ENC, L::NTS, L::TSLOTX, true, L::WPE>(&karg_gf(), &karg_hash(), xbuf, wave - L::HW - kNQ, steps, s0);
         else
-            records_target_hasher<4, TH, 2>(p, h, trow, wave - L::HW - kNQ, steps, s0);
+            records_target_hasher<4, TH, 2, false, 2, 0, false, L::WPE>(&karg_gf(), &karg_hash(), trow, wave - L::HW - kNQ, steps, s0);
         return;
     }
     if (wave >= (uint32_t)L::HW) {
@@ -335,11 +335,11 @@ __attribute__((amdgpu_waves_per_eu(NetQShape<NF, TH, RDX, ENC>::WPE))) void RSG_
     }
     if constexpr (L::MERGE) {
         if (wave == (uint32_t)(L::HW - 1)) {  // the last hash wave hashes the target rows too
-            records_hash_target_wave<NF, 4, L::RD, TH, L::NTS, L::TSLOTX>(p, h, ring, xbuf, wave, steps, s0);
+            records_hash_target_wave<NF, 4, L::RD, TH, L::NTS, L::TSLOTX, 2, true, L::WPE>(&karg_gf(), &karg_hash(), ring, xbuf, wave, steps, s0);
             return;
         }
     }
-    records_hash_wave<NF, 4, L::XB, L::RD, ENC>(h, p.wave_prio, ring, wave, steps, s0);
+    records_hash_wave<NF, 4, L::XB, L::RD, ENC, L::WPE>(&karg_hash(), p.wave_prio, ring, wave, steps, s0);
 }
 
 static_assert(NetQShape<13, 0, 2>::LDS <= 80 * 1024 && NetQShape<12, 2>::LDS <= 160 * 1024 &&

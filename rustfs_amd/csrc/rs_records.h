@@ -11,6 +11,41 @@
 
 namespace rsg {
 
+// The record waves below are functions of their own (noinline): one copy per
+// ring shape and role, called once per wave, instead of one inlined copy per
+// pattern kernel — the per-pattern network kernels compile in half the time.
+// They read the kernel's arguments where they lie, in the kernarg segment:
+// every record kernel takes (const GfApplyParams p, const HashParams h), laid
+// out in that order at their natural alignment.  (Taking the address of a
+// by-value kernel argument instead makes the compiler copy it to scratch,
+// ~1 KiB per lane.)
+#define RSG_KARG const __attribute__((address_space(4)))
+using KGf = RSG_KARG GfApplyParams;
+using KHash = RSG_KARG HashParams;
+__device__ __forceinline__ KGf& karg_gf() { return *(KGf*)__builtin_amdgcn_kernarg_segment_ptr(); }
+__device__ __forceinline__ KHash& karg_hash() {
+    constexpr size_t off = (sizeof(GfApplyParams) + alignof(HashParams) - 1) / alignof(HashParams) * alignof(HashParams);
+    return *(KHash*)((RSG_KARG char*)__builtin_amdgcn_kernarg_segment_ptr() + off);
+}
+// OCC (template argument): the calling kernel's waves per SIMD
+// (amdgpu_waves_per_eu) — a function shared by kernels of different
+// occupancy gets the loosest register budget among them (RS(13,3)'s heal
+// kernel took its target hasher's 129 registers, so one workgroup a CU);
+// instantiating per occupancy keeps each at its kernels' budget.
+#define RSG_RECORD_WAVE __device__ __attribute__((noinline))
+// A called function takes its arguments in VGPRs: the wave-uniform ones are
+// made scalar again on entry (SGPRs, SALU) as they were in the kernel.
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni(uint64_t v) {
+    return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
+}
+template <class T>
+__device__ __forceinline__ T* uni(T* v) {
+    return (T*)(uintptr_t)uni((uint64_t)(uintptr_t)v);
+}
+__device__ __forceinline__ KGf& uni(KGf* v) { return *(KGf*)(uintptr_t)uni((uint64_t)(uintptr_t)v); }
+__device__ __forceinline__ KHash& uni(KHash* v) { return *(KHash*)(uintptr_t)uni((uint64_t)(uintptr_t)v); }
+
 // Ring of one workgroup: G stripes, NF present files, 512-byte steps.
 // Present file f of stripe e sits in DMA instruction f*HS + e%HS, half e/HS
 // (stripes e and e + HS share one 1 KiB LDS row pair of pitch IP).
@@ -55,9 +90,14 @@ __device__ __forceinline__ uint64_t part_mask8(uint32_t off, uint32_t valid) {
 // ENC (the fused encode + HH256S, k_encode_hash_net12): the sources are the
 // data shards of a stripe buffer and each digest is written, not checked, to
 // h.out + (stripe * h.shards + file) * 32 (the batch digest layout).
-template <int NF, int G, int XB = 0, int RD = dma::D, bool ENC = false>
-__device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t wave_prio, uint8_t* ring,
-                                                  uint32_t hw, uint32_t steps, uint64_t s0) {
+template <int NF, int G, int XB = 0, int RD = dma::D, bool ENC = false, int OCC = 0>
+RSG_RECORD_WAVE void records_hash_wave(KHash* h_in, uint32_t wave_prio, uint8_t* ring_in, uint32_t hw_in,
+                                       uint32_t steps_in, uint64_t s0_in) {
+    KHash& h = uni(h_in);
+    uint8_t* const ring = uni(ring_in);
+    const uint32_t hw = uni(hw_in), steps = uni(steps_in);
+    const uint64_t s0 = uni(s0_in);
+    wave_prio = uni(wave_prio);
     using dma::CH;
     using dma::IP;
     constexpr int D = RD;  // ring slots: D - 1 steps of DMA in flight
@@ -77,7 +117,10 @@ __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t 
     const uint32_t tail = walk_tail(h.len, steps);
     const bool ragged = tail != CH;
     HHQuad st;
-    hhq_init(st, h.key, q);
+    {
+        const uint64_t key[4] = {h.key[0], h.key[1], h.key[2], h.key[3]};
+        hhq_init(st, key, q);
+    }
     // record sources as a wave-uniform base (SGPRs) + a 32-bit per-lane
     // offset (the upper half's stripe, or the lower one again past n): the
     // loads take the saddr form, a step costs HS VALU adds
@@ -221,9 +264,15 @@ __device__ __forceinline__ void records_hash_wave(const HashParams& h, uint32_t 
 // kernels' accumulators; LAG 1: the table kernel's GF waves write whole rows) —
 // and at the end writes the target record's digest header
 // (BitrotWriter::write).  steps + LAG barriers.
-template <int NF, int G, int RD, int TTH, int TNS, uint32_t TSLOT, int LAG = 2, bool ZERO = true>
-__device__ __forceinline__ void records_hash_target_wave(const GfApplyParams& p, const HashParams& h, uint8_t* ring,
-                                                         uint8_t* trow, uint32_t hw, uint32_t steps, uint64_t s0) {
+template <int NF, int G, int RD, int TTH, int TNS, uint32_t TSLOT, int LAG = 2, bool ZERO = true, int OCC = 0>
+RSG_RECORD_WAVE void records_hash_target_wave(KGf* p_in, KHash* h_in, uint8_t* ring_in, uint8_t* trow_in,
+                                              uint32_t hw_in, uint32_t steps_in, uint64_t s0_in) {
+    KGf& p = uni(p_in);
+    KHash& h = uni(h_in);
+    uint8_t* const ring = uni(ring_in);
+    uint8_t* const trow = uni(trow_in);
+    const uint32_t hw = uni(hw_in), steps = uni(steps_in);
+    const uint64_t s0 = uni(s0_in);
     using dma::CH;
     using dma::IP;
     using dma::PP;
@@ -251,7 +300,10 @@ __device__ __forceinline__ void records_hash_target_wave(const GfApplyParams& p,
     const uint32_t tail = walk_tail(h.len, steps);
     const bool ragged = tail != CH;
     HHQuad st;
-    hhq_init(st, h.key, q);
+    {
+        const uint64_t key[4] = {h.key[0], h.key[1], h.key[2], h.key[3]};
+        hhq_init(st, key, q);
+    }
     uint64_t ubo[HS];
     uint32_t vlane[HS];
 #pragma unroll
@@ -386,10 +438,14 @@ __device__ __forceinline__ void records_hash_target_wave(const GfApplyParams& p,
 // bytes (0: RecRing's TSLOT) used round robin; ZERO: each row cleared once
 // hashed (k_decode_records_net12's fused encode keeps its rows in the
 // network waves' accumulators).
-template <int G, int TH, int LAG = 1, bool ENC = false, int NS = 2, uint32_t SLOT = 0, bool ZERO = false>
-__device__ __forceinline__ void records_target_hasher(const GfApplyParams& p, const HashParams& h,
-                                                      const uint8_t* trow, uint32_t tw, uint32_t steps,
-                                                      uint64_t s0) {
+template <int G, int TH, int LAG = 1, bool ENC = false, int NS = 2, uint32_t SLOT = 0, bool ZERO = false, int OCC = 0>
+RSG_RECORD_WAVE void records_target_hasher(KGf* p_in, KHash* h_in, const uint8_t* trow_in, uint32_t tw_in,
+                                           uint32_t steps_in, uint64_t s0_in) {
+    KGf& p = uni(p_in);
+    KHash& h = uni(h_in);
+    const uint8_t* const trow = uni(trow_in);
+    const uint32_t tw = uni(tw_in), steps = uni(steps_in);
+    const uint64_t s0 = uni(s0_in);
     constexpr int SPW = G;
     constexpr uint32_t TSLOT = SLOT ? SLOT : RecRing<1, G, TH>::TSLOT;
     if (p.wave_prio & kPrioHash) __builtin_amdgcn_s_setprio(2);
@@ -401,7 +457,10 @@ __device__ __forceinline__ void records_target_hasher(const GfApplyParams& p, co
     const uint32_t roff = (on ? pi : 0) * dma::PP + 8 * q;
     const uint32_t tail = walk_tail(h.len, steps);
     HHQuad st;
-    hhq_init(st, h.key, q);
+    {
+        const uint64_t key[4] = {h.key[0], h.key[1], h.key[2], h.key[3]};
+        hhq_init(st, key, q);
+    }
     lds_barrier();  // B(0)
 #pragma unroll 1
     for (uint32_t t = 0; t < steps + LAG; ++t) {

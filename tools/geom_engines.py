@@ -8,7 +8,9 @@ shard (one data shard at m = 1), each on both record engines
 (rsg_set_record_engine ONE_PASS / TWO_PASS), timed like bench.py's engine
 extras: back-to-back calls until the device has been busy 0.5 s, then 20
 calls, kernel time from the in-call HIP events (median).  Prints one JSON line
-per geometry.  Usage: python tools/geom_engines.py 5,4 11,4 15,1 [--n 4096]"""
+per geometry.  --tune RSG_DECODE_NET=0 (repeatable) sets a kernel-choice knob
+through rsg_set_tuning for the whole run (e.g. the table kernel in place of the
+networks).  Usage: python tools/geom_engines.py 5,4 11,4 15,1 [--n 4096]"""
 import argparse
 import ctypes
 import json
@@ -25,12 +27,18 @@ def main():
     ap.add_argument("geoms", nargs="+")
     ap.add_argument("--n", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--tune", action="append", default=[])
+    ap.add_argument("--get-lost", default=None, help="shards lost for the GET, e.g. 0 or 0,3 (default: 0,k-1)")
+    ap.add_argument("--heal-lost", default=None, help="shards healed, e.g. 1,10 (default: 1,k)")
     a = ap.parse_args()
     import torch
     import bench
     from rustfs_amd import Erasure, _lib
     L = _lib.load()
     ctx = _lib.context(0).handle
+    for kv in a.tune:
+        name, value = kv.split("=", 1)
+        _lib.set_tuning(name, value)
     for g in a.geoms:
         k, m = map(int, g.split(","))
         t, n = k + m, a.n
@@ -49,13 +57,17 @@ def main():
         del dig
         lost_get = (0, k - 1) if m >= 2 and k >= 2 else (0,)
         lost_heal = (1 % k, k) if m >= 2 else (k - 1,)
+        if a.get_lost is not None:
+            lost_get = tuple(int(x) for x in a.get_lost.split(","))
+        if a.heal_lost is not None:
+            lost_heal = tuple(int(x) for x in a.heal_lost.split(","))
         slots = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
         tg = [torch.empty(n * rec, dtype=torch.uint8, device="cuda") if i in lost_heal else None for i in range(t)]
         gsrc = [None if i in lost_get else files[i] for i in range(t)]
         hsrc = [None if i in lost_heal else files[i] for i in range(t)]
         want = {i: st[n - 1, i].clone() for i in range(k)}
         out = {"geometry": f"RS({k},{m})", "shard_bytes": S, "stripes": n, "get_lost": list(lost_get),
-               "heal_lost": list(lost_heal)}
+               "heal_lost": list(lost_heal), "tuning": a.tune}
         cases = {
             "get": (lambda: e.decode_records_into_batch(gsrc, S, n, targets=slots),
                     n * ((t - len(lost_get)) * rec + len(lost_get) * S)),
