@@ -495,6 +495,9 @@ RSG_RECORD_WAVE void records_target_hasher(KGf* p_in, KHash* h_in, const uint8_t
 // NF KiB-rows fits the LDS, 4 for C = 16 (RS(16,4): up to 19 present files).
 // (Four stripes per workgroup at RS(8,4) — two workgroups of 7 waves per CU —
 // measured no faster, profiles/r02/ab_eng/.)
+// (Four-stripe workgroups for C <= 8 too — two or three a CU — measured
+// 2-110 % slower again in round 5: RS(5,4) GET 1.81 -> 2.58 ms, RS(4,4) heal
+// 1.85 -> 2.97; profiles/r05/ab_group/.)
 constexpr int get_group(int C) { return C > 8 ? 4 : 8; }
 
 }  // namespace rsg

@@ -91,7 +91,8 @@ def main():
                     _, src, status = r
                     assert all(x == 0 for x in status)
                     for i in lost_get:
-                        assert torch.equal(slots.view(n, k, S)[n - 1, i], want[i]), (g, engine, i)
+                        if i < k:  # a lost parity shard has no slot
+                            assert torch.equal(slots.view(n, k, S)[n - 1, i], want[i]), (g, engine, i)
                 else:
                     assert all(x == 0 for x in r)
                     for i in lost_heal:
