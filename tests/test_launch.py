@@ -160,11 +160,13 @@ def test_config5_plan(world):
 def test_pmc_traffic_covers_the_default_line():
     """Every traffic entry the default bench line looks up (headline, configs
     3/4/5, the RS(8,4) engines and the RS(12,4) extras) is in
-    tools/pmc_traffic.json (shipped with the tree), and each is within 4 % of
-    the algorithmic bytes of its launch (no wasted re-reads; the RS(12,4)
-    kernels' unaligned 87382-byte rows write 6-10 % more than their payload
-    because a row's first and last 32-byte sectors are shared with the
-    neighbouring step's row: 1.028-1.037 overall, RS(8,4) <= 1.008)."""
+    tools/pmc_traffic.json (shipped with the tree), and each is within 1.5 % of
+    the algorithmic bytes of its launch at RS(8,4) / RS(16,4) (no wasted
+    re-reads; the whole-file verify reads each 32-byte digest header as a
+    sector of its own: 1.011) and 5 % at RS(12,4): its unaligned 87382-byte rows are written a
+    512-byte step at a time, and a step's first and last sectors, shared with
+    the neighbouring step, leave the L2 twice (writes 1-15 % over the payload,
+    1.00-1.041 overall)."""
     import bench
     want = {}
     for k, S in ((8, 131072), (12, 87382)):
@@ -180,7 +182,7 @@ def test_pmc_traffic_covers_the_default_line():
     for key, alg in want.items():
         got = bench.pmc_lookup(key)
         assert got is not None, key
-        assert abs(got / alg - 1) < 0.04, (key, got, alg)
+        assert abs(got / alg - 1) < (0.05 if "rs124" in key else 0.015), (key, got, alg)
 
 
 def test_pmc_traffic_sources_are_committed_counters():
