@@ -411,7 +411,8 @@ def engine_plan(k, m, S, n, full=True):
             ("heal_1data_1parity", n * ((t - 2) * rec + 2 * rec), f"heal_1d1p_{g}"),
             ("bitrot_verify_all_files", t * n * rec, f"verify_all_{g}")]
     if full:
-        plan += [("get_2_data_lost_async", n * ((t - 2) * rec + 2 * S), None),
+        plan += [("get_all_present_async", n * k * rec, None),
+                 ("get_2_data_lost_async", n * ((t - 2) * rec + 2 * S), None),
                  ("heal_1data_1parity_async", n * ((t - 2) * rec + 2 * rec), None)]
     return plan
 
@@ -545,6 +546,10 @@ def engine_extras(e, stripes, k, m, S, n, stream, record_engine="auto", full=Tru
     lost = [None if i in (0, 3) else files[i] for i in range(t)]
     timed("get_all_present", lambda: e.decode_records_into_batch(files, S, n, targets=slots, stream=stream),
           ok_into(()))
+    if full:  # submitted back to back (rsg_decode_records_submit): the host's verdict reading overlapped
+        timed_pipelined("get_all_present_async",
+                        lambda: e.decode_records_submit(files, S, n, targets=slots, inplace=True, stream=stream),
+                        ok_into(()))
     timed("get_2_data_lost", lambda: e.decode_records_into_batch(lost, S, n, targets=slots, stream=stream),
           ok_into((0, 3)))
     if full:  # the same GETs submitted back to back (rsg_decode_records_submit)

@@ -211,7 +211,7 @@ def test_engine_plan_rs12_4():
     storageclass.rs:24-31): in-place GET with 0 and 2 data lost, heal of one
     data + one parity disk and the whole-file bitrot_verify, priced on the
     contract's minimum bytes at S = ceil(1 MiB / 12) = 87382, n = 4096; the
-    RS(8,4) line adds the asynchronous GET / heal."""
+    RS(8,4) line adds the asynchronous GETs (all present, two lost) and heal."""
     import bench
     k, m, n = 12, 4, 4096
     S = -(-(1 << 20) // k)
@@ -225,7 +225,7 @@ def test_engine_plan_rs12_4():
         "bitrot_verify_all_files": (t * n * rec, "verify_all_rs124_S87382_n4096"),
     }
     full = [name for name, _, _ in bench.engine_plan(8, 4, 131072, 4096)]
-    assert full[-2:] == ["get_2_data_lost_async", "heal_1data_1parity_async"]
+    assert full[-3:] == ["get_all_present_async", "get_2_data_lost_async", "heal_1data_1parity_async"]
     # the engine loops time at least 20 calls after a >= 0.5 s busy warm-up
     assert bench.ENGINE_REPS >= 20 and bench.ENGINE_WARM_S >= 0.5
     a = bench.parse([])
