@@ -38,11 +38,12 @@ def _records(torch, k, m, S, n, seed):
 
 
 # RS(11,4): the run-time-table kernel on the 2-slot ring (two workgroups a CU),
-# its heal hashing the targets in the last hash wave (round 5)
-@pytest.mark.parametrize("k,S", [(8, 131072), (12, 87382), (11, 95326)])
-def test_engines_every_stripe_at_bench_size(gpu, oracle, k, S):
+# its heal hashing the targets in the last hash wave; RS(8,8) (EC:8 on 16
+# drives): the table kernel with 8 row slots (round 5)
+@pytest.mark.parametrize("k,m,S", [(8, 4, 131072), (12, 4, 87382), (11, 4, 95326), (8, 8, 131072)])
+def test_engines_every_stripe_at_bench_size(gpu, oracle, k, m, S):
     import torch
-    m, n = 4, 4096
+    n = 4096
     t, rec = k + m, 32 + S
     e, st, dig, files = _records(torch, k, m, S, n, seed=k)
     for s in (0, 1777, n - 1):  # the encoder's parity and digests against the oracle
