@@ -118,6 +118,9 @@ struct HashParams {
 hipError_t launch_gf_apply_vec(GfApplyParams p, uint64_t n_stripes, hipStream_t stream);
 hipError_t launch_gf_apply_byte(GfApplyParams p, uint64_t n_stripes, hipStream_t stream);
 hipError_t launch_hh256(const HashParams& p, hipStream_t stream);
+// A multi-file verify of records at unaligned pitches on the LDS-DMA ring
+// (rs_verify.hip); false: not taken, launch_hh256 runs the quad kernel.
+bool launch_verify_records_dma(const HashParams& h, hipStream_t stream);
 // n bytes of device memory to page-locked host memory (dst = its device
 // view), as a kernel on the stream; 16-byte aligned ends.
 hipError_t launch_copy_to_host(uint8_t* dst, const uint8_t* src, uint64_t n, hipStream_t stream);

@@ -1469,6 +1469,7 @@ hipError_t launch_hh256(const HashParams& p, hipStream_t stream) {
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
     bool copy = false;  // copy mode when any file of the launch has a copy target
     for (uint32_t b = 0; b < p.nbases; ++b) copy = copy || p.copy_base[b];
+    if (!copy && launch_verify_records_dma(p, stream)) return hipGetLastError();
     // copy mode: staged 16-byte stores (COPY = 2) by default (Tuning:
     // direct 8-byte stores for A/B runs); 8-packet batches in flight per
     // lane: 2 by default

@@ -221,13 +221,17 @@ def test_kernel_timing_hook(gpu, oracle, engine_path):
         _lib.check(L.rsg_set_kernel_timing(ctx, 0))
 
 
-def test_into_serves_verified_records_in_place(gpu, oracle):
+@pytest.mark.parametrize("S", [4096, 4102, 4099])
+def test_into_serves_verified_records_in_place(gpu, oracle, S):
     """reconstruct_into's contract (bridge.rs:274-307, :52-54): with every data
     shard present nothing is written; a rotten data record is the only shard
-    rebuilt, into its slot, and reported as not served from its record."""
+    rebuilt, into its slot, and reported as not served from its record.
+    Records at 0 mod 16 (the quad hash kernel's verify), 6 mod 16 and odd
+    pitches (the LDS-DMA ring's, rs_verify.hip; 5 stripes: a partial
+    workgroup)."""
     import torch
     from conftest import SLOT_FILL
-    k, m, S, n = 8, 4, 4096, 5
+    k, m, n = 8, 4, 5
     e, st, files = _records(torch, k, m, S, n, seed=21)
     rec = 32 + S
     slots = torch.full((n, k * S), SLOT_FILL, dtype=torch.uint8, device="cuda")

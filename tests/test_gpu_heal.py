@@ -114,13 +114,14 @@ def _shard_file(oracle, part: bytes, S: int, legacy=False) -> bytes:
     return bytes(out)
 
 
-@pytest.mark.parametrize("legacy", [False, True])
-def test_bitrot_verify_batch(gpu, oracle, legacy):
+# S = 4096: records at 0 mod 16 (the quad hash kernel); 4102 and 4099: at 6
+# mod 16 and odd pitches (HH256S: the LDS-DMA ring verify, rs_verify.hip)
+@pytest.mark.parametrize("legacy,S", [(False, 4096), (True, 4096), (False, 4102), (False, 4099)])
+def test_bitrot_verify_batch(gpu, oracle, legacy, S):
     import torch
     from rustfs_amd import _lib
     from rustfs_amd.bitrot import HashAlgorithm, bitrot_shard_file_size, bitrot_verify, bitrot_verify_batch
     algo = HashAlgorithm.HighwayHash256SLegacy if legacy else HashAlgorithm.HighwayHash256S
-    S = 4096
     rng = np.random.default_rng(7)
     part = rng.integers(0, 256, 3 * S + 100, dtype=np.uint8).tobytes()
     good = _shard_file(oracle, part, S, legacy)
