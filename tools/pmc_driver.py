@@ -69,7 +69,8 @@ def main():
         slots = torch.empty((n, k * S), dtype=torch.uint8, device=dev)
         if what == "get_into0":
             fn = lambda: e.decode_records_into_batch(files, S, n, targets=slots)  # noqa: E731
-            filt = "k_hh256_quad"
+            # records off 16-byte alignment: the LDS-DMA ring verify (rs_verify.hip)
+            filt = "k_hh256_quad" if rec % 16 == 0 else "k_verify_records_dma"
         elif what == "get_into2":
             lost = [None if i in (0, 3) else files[i] for i in range(t)]
             fn = lambda: e.decode_records_into_batch(lost, S, n, targets=slots)  # noqa: E731
