@@ -34,7 +34,8 @@ constexpr int kVG = 4;  // records per file per workgroup
 // quad kernel; RS(12,4)'s 16, 1 % slower, stay on it).  Launches of 13-15
 // files at odd record pitches stay on the quad kernel's funnel (RS(14,2)'s 16:
 // 12 % slower on the ring), more files too; split launches of 8 + 8 files
-// measured 12-24 % slower than either (profiles/r05/ab_verify/).
+// measured 12-24 % slower than either, and 2-record workgroups on a 3-slot
+// ring past 12 files 12-30 % slower (profiles/r05/ab_verify/, g2/).
 template <int NF>
 struct VerifyShape : RecRing<NF, kVG> {
     static constexpr int RD = NF <= 12 ? 3 : 2;
