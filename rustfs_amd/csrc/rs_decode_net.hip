@@ -220,7 +220,11 @@ __device__ __forceinline__ void net_wave(const GfApplyParams& p, uint64_t n, uin
     }
 }
 
-template <int PID, int NF, int TH>
+// ENC: the fused encode + HH256S (launch_encode_hash_net below): the heal of
+// all four parity shards over a stripe buffer, every digest written to the
+// batch digest layout (the hash waves: the data shards' digests; the target
+// hashers: the parity shards').
+template <int PID, int NF, int TH, bool ENC = false>
 __global__ __launch_bounds__((64 * NetShape<NF, TH>::WAVES)) void RSG_NET_NAME(k_decode_records_net, )(const GfApplyParams p,
                                                                                        const HashParams h) {
     using L = NetShape<NF, TH>;
@@ -230,14 +234,14 @@ __global__ __launch_bounds__((64 * NetShape<NF, TH>::WAVES)) void RSG_NET_NAME(k
     const uint32_t steps = p.units;
     const uint64_t s0 = (uint64_t)blockIdx.x * L::SPW;
     if (TH && wave >= (uint32_t)(L::HW + L::NG)) {
-        records_target_hasher<8, TH>(&karg_gf(), &karg_hash(), trow, wave - L::HW - L::NG, steps, s0);
+        records_target_hasher<8, TH, 1, ENC>(&karg_gf(), &karg_hash(), trow, wave - L::HW - L::NG, steps, s0);
         return;
     }
     if (wave >= (uint32_t)L::HW) {
         net_wave<PID, NF, TH>(p, h.n, steps, s0, wave - L::HW, ring, trow);
         return;
     }
-    records_hash_wave<NF, 8>(&karg_hash(), p.wave_prio, ring, wave, steps, s0);
+    records_hash_wave<NF, 8, 0, dma::D, ENC>(&karg_hash(), p.wave_prio, ring, wave, steps, s0);
 }
 
 using NetLaunch = void (*)(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream);
@@ -273,6 +277,50 @@ bool RSG_NET_NAME(launch_records_net, RSG_NET_CAT(_part, RSG_NET_PART))(int pid,
 }
 
 #if RSG_NET_PART == 0
+// The fused encode + HH256S of RS(8,4) / RS(6,4) / RS(4,4) (BitrotWriter over
+// an encoded block, bitrot.rs:464-510 after erasure encode): the heal kernel
+// of all four parity shards (pattern kEncodePid, rows = the encode matrix)
+// walking the data shards of a stripe buffer in place, as
+// rs_decode_netq.hip's for RS(12,4) / RS(10,4).
+namespace {
+constexpr int encode_pid() {
+    for (int i = 0; i < decnet::kCount; ++i)
+        if (decnet::kPatterns[i].heal && decnet::kPatterns[i].absent == (0xFu << kNetC)) return i;
+    return -1;
+}
+constexpr int kEncodePid = encode_pid();
+static_assert(kEncodePid >= 0 && decnet::kPatterns[kEncodePid].nf == kNetC && decnet::kPatterns[kEncodePid].R == 4,
+              "the generated header lists the heal of every parity shard");
+}  // namespace
+
+const uint8_t* RSG_NET_NAME(encode_net, _coef)() { return &decnet::kPatterns[kEncodePid].coef[0][0]; }
+
+// p: the encode's table-GF launch (in place: base == out_base, in_off = the
+// data shards, out_off = the parity shards); h: key, out (digests).
+hipError_t RSG_NET_NAME(launch_encode_hash_net, )(GfApplyParams p, HashParams h, uint64_t shard_len,
+                                                  uint64_t n_stripes, hipStream_t stream) {
+    using L = NetShape<kNetC, 4>;
+    if (p.C != (uint32_t)kNetC || p.R != 4 || n_stripes == 0 || shard_len == 0 || p.base != p.out_base ||
+        p.stripe_stride != p.out_stripe_stride || 5 * p.stripe_stride >= (1ull << 32) ||
+        (n_stripes + L::SPW - 1) / L::SPW > 0x7fffffffull || (shard_len + dma::CH - 1) / dma::CH > 0xffffffffull)
+        return hipErrorInvalidValue;
+    p.n_store = 4;
+    p.copy_mask = 0;
+    p.cached_stores = tuning().get_cached ? 1u : 0u;
+    p.wave_prio = (uint32_t)tuning().get_prio;
+    p.units = (uint32_t)((shard_len + dma::CH - 1) / dma::CH);
+    p.byte_end = shard_len;
+    h.len = shard_len;
+    h.n = n_stripes;
+    h.shards = kNetC + 4;
+    h.stripe_stride = p.stripe_stride;
+    h.nbases = kNetC;
+    for (int c = 0; c < kNetC; ++c) h.base[c] = p.base + p.in_off[c];
+    hipLaunchKernelGGL((RSG_NET_NAME(k_decode_records_net, )<kEncodePid, kNetC, 4, true>),
+                       dim3((uint32_t)((n_stripes + L::SPW - 1) / L::SPW)), dim3(64 * L::WAVES), 0, stream, p, h);
+    return hipGetLastError();
+}
+
 // The pattern whose coefficient rows equal the launch's (R x K, row-major),
 // or -1: matched byte for byte, so a network is only ever run on exactly the
 // matrix it was generated for.

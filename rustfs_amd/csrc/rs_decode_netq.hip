@@ -416,32 +416,33 @@ bool RSG_NETQ_NAME(launch_records_, RSG_NETQ_CAT(_part, RSG_NET_PART))(int pid, 
     return true;
 }
 
-#if RSG_NET_PART == 0 && RSG_NETQ_K == 12
-// The fused encode + HH256S of RS(12,4) (BitrotWriter over an encoded block,
-// bitrot.rs:464-510 after erasure encode): the heal kernel of all four parity
-// shards (pattern kEncodePid, rows = the encode matrix) walking the data
-// shards of a stripe buffer in place — 12 data rows DMA'd and hashed, 4
-// parity rows computed by the network waves, stored and hashed by the target
-// hasher — every digest to h.out (stripe-major, 16 per stripe).
+#if RSG_NET_PART == 0
+// The fused encode + HH256S of RS(12,4) and RS(10,4) (BitrotWriter over an
+// encoded block, bitrot.rs:464-510 after erasure encode): the heal kernel of
+// all four parity shards (pattern kEncodePid, rows = the encode matrix)
+// walking the data shards of a stripe buffer in place — K data rows DMA'd and
+// hashed, 4 parity rows computed by the network waves, stored and hashed by
+// the target hasher — every digest to h.out (stripe-major, K + 4 per stripe).
 namespace {
 constexpr int encode_pid() {
     for (int i = 0; i < decq::kCount; ++i)
-        if (decq::kPatterns[i].heal && decq::kPatterns[i].absent == 0xF000) return i;
+        if (decq::kPatterns[i].heal && decq::kPatterns[i].absent == (0xFu << kKQ)) return i;
     return -1;
 }
 constexpr int kEncodePid = encode_pid();
-static_assert(kEncodePid >= 0 && decq::kPatterns[kEncodePid].nf == 12 && decq::kPatterns[kEncodePid].R == 4,
-              "rs124_decode_nets.h lists the heal of every parity shard");
+static_assert(kEncodePid >= 0 && decq::kPatterns[kEncodePid].nf == kKQ && decq::kPatterns[kEncodePid].R == 4,
+              "the generated header lists the heal of every parity shard");
+static_assert(NetQShape<kKQ, 4, 2, true>::LDS <= 80 * 1024, "the fused encode: two workgroups per CU");
 }  // namespace
 
-const uint8_t* encode_net12_coef() { return &decq::kPatterns[kEncodePid].coef[0][0]; }
+const uint8_t* RSG_NETQ_NAME(encode_, _coef)() { return &decq::kPatterns[kEncodePid].coef[0][0]; }
 
 // p: the encode's table-GF launch (in place: base == out_base, in_off = the
 // data shards, out_off = the parity shards); h: key, out (digests).
-hipError_t launch_encode_hash_net12(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
-                                    hipStream_t stream) {
-    using L = NetQShape<12, 4, 2, true>;
-    if (p.C != 12 || p.R != 4 || n_stripes == 0 || shard_len == 0 || p.base != p.out_base ||
+hipError_t RSG_NETQ_NAME(launch_encode_hash_, )(GfApplyParams p, HashParams h, uint64_t shard_len,
+                                                uint64_t n_stripes, hipStream_t stream) {
+    using L = NetQShape<kKQ, 4, 2, true>;
+    if (p.C != (uint32_t)kKQ || p.R != 4 || n_stripes == 0 || shard_len == 0 || p.base != p.out_base ||
         p.stripe_stride != p.out_stripe_stride || 5 * p.stripe_stride >= (1ull << 32) ||
         (n_stripes + L::SPW - 1) / L::SPW > 0x7fffffffull || (shard_len + dma::CH - 1) / dma::CH > 0xffffffffull)
         return hipErrorInvalidValue;
@@ -452,17 +453,17 @@ hipError_t launch_encode_hash_net12(GfApplyParams p, HashParams h, uint64_t shar
     p.byte_end = shard_len;
     h.len = shard_len;
     h.n = n_stripes;
-    h.shards = 16;
+    h.shards = kKQ + 4;
     h.stripe_stride = p.stripe_stride;
-    h.nbases = 12;
-    for (int c = 0; c < 12; ++c) h.base[c] = p.base + p.in_off[c];
+    h.nbases = kKQ;
+    for (int c = 0; c < kKQ; ++c) h.base[c] = p.base + p.in_off[c];
     // two workgroups per CU on a 2-slot ring (RSG_NET12_RD=4, measurement builds: one, 4 slots)
     if (!RSG_MEASUREMENT_BUILD || tuning().net12_rd == 2)
-        hipLaunchKernelGGL((k_decode_records_net12<kEncodePid, 12, 4, true, 2>),
+        hipLaunchKernelGGL((RSG_NETQ_NAME(k_decode_records_, )<kEncodePid, kKQ, 4, true, 2>),
                            dim3((uint32_t)((n_stripes + L::SPW - 1) / L::SPW)), dim3(64 * L::WAVES), 0, stream, p, h);
 #if RSG_MEASUREMENT_BUILD
     else
-        hipLaunchKernelGGL((k_decode_records_net12<kEncodePid, 12, 4, true, 4>),
+        hipLaunchKernelGGL((RSG_NETQ_NAME(k_decode_records_, )<kEncodePid, kKQ, 4, true, 4>),
                            dim3((uint32_t)((n_stripes + L::SPW - 1) / L::SPW)), dim3(64 * L::WAVES), 0, stream, p, h);
 #endif
     return hipGetLastError();

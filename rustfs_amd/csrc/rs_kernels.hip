@@ -1198,8 +1198,9 @@ bool set_knob(Tuning& v, const std::string& name, const char* value) {
     if (name == "RSG_HASH_COPY") return flag(v.hash_direct_copy);
     if (name == "RSG_HASH_DEPTH") return num(v.hash_depth, 1, 3);
     if (name == "RSG_FUSED_KIND") {
-        static const char* const kinds[] = {"auto", "packed", "ring", "dma", "wide2", "wide4", "split2", "split4"};
-        for (int i = 0; i < 8; ++i)
+        static const char* const kinds[] = {"auto",  "packed", "ring",   "dma",   "wide2",
+                                            "wide4", "split2", "split4", "net"};
+        for (int i = 0; i < 9; ++i)
             if (s == kinds[i]) {
                 v.fused_kind = i;
                 return true;
@@ -1232,8 +1233,9 @@ bool knob_value(const Tuning& v, const std::string& name, std::string& out) {
     if (name == "RSG_HASH_COPY") return b(v.hash_direct_copy);
     if (name == "RSG_HASH_DEPTH") return i(v.hash_depth);
     if (name == "RSG_FUSED_KIND") {
-        static const char* const kinds[] = {"auto", "packed", "ring", "dma", "wide2", "wide4", "split2", "split4"};
-        out = kinds[v.fused_kind >= 0 && v.fused_kind < 8 ? v.fused_kind : 0];
+        static const char* const kinds[] = {"auto",  "packed", "ring",   "dma",   "wide2",
+                                            "wide4", "split2", "split4", "net"};
+        out = kinds[v.fused_kind >= 0 && v.fused_kind < 9 ? v.fused_kind : 0];
         return true;
     }
     if (name == "RSG_FUSED_SPW1") return b(v.fused_spw1);
@@ -1609,12 +1611,32 @@ static bool tables_match(const GfApplyParams& p, const uint8_t* coef, int C, int
     return true;
 }
 
-// RS(12,4) encode in place over 1024+ stripes (256+ workgroups of 4):
-// k_encode_hash_net12 (rs_decode_netq.hip).
-static bool net12_supported(const GfApplyParams& p, uint64_t n_stripes) {
-    return p.C == 12 && p.R == 4 && p.mode == GF_MODE_STORE && !p.copy_mask && p.base == p.out_base &&
-           p.stripe_stride == p.out_stripe_stride && n_stripes >= 1024 && 5 * p.stripe_stride < (1ull << 32) &&
-           tables_match(p, encode_net12_coef(), 12, 4);
+// RS(12,4) / RS(10,4) encode in place over 1024+ stripes (256+ workgroups of
+// 4): the fused network kernel (rs_decode_netq.hip, k_decode_records_net12 /
+// _net10 with ENC).
+// RS(8,4) / RS(6,4) / RS(4,4) encode in place: the 8-stripe network kernel
+// with ENC (rs_decode_net.hip) — from 2048 stripes (256+ workgroups).
+static bool net_enc_supported(const GfApplyParams& p, uint64_t n_stripes) {
+    if ((p.C != 8 && p.C != 6 && p.C != 4) || p.R != 4 || p.mode != GF_MODE_STORE || p.copy_mask ||
+        p.base != p.out_base || p.stripe_stride != p.out_stripe_stride || n_stripes < 2048 ||
+        5 * p.stripe_stride >= (1ull << 32))
+        return false;
+    const uint8_t* coef = p.C == 8 ? encode_net_coef() : p.C == 6 ? encode_net6_coef() : encode_net4_coef();
+    return tables_match(p, coef, (int)p.C, 4);
+}
+
+static hipError_t launch_encode_hash_net_c(const GfApplyParams& p, const HashParams& h, uint64_t shard_len,
+                                           uint64_t n_stripes, hipStream_t stream) {
+    if (p.C == 8) return launch_encode_hash_net(p, h, shard_len, n_stripes, stream);
+    if (p.C == 6) return launch_encode_hash_net6(p, h, shard_len, n_stripes, stream);
+    return launch_encode_hash_net4(p, h, shard_len, n_stripes, stream);
+}
+
+static bool netq_enc_supported(const GfApplyParams& p, uint64_t n_stripes) {
+    if ((p.C != 12 && p.C != 10) || p.R != 4 || p.mode != GF_MODE_STORE || p.copy_mask || p.base != p.out_base ||
+        p.stripe_stride != p.out_stripe_stride || n_stripes < 1024 || 5 * p.stripe_stride >= (1ull << 32))
+        return false;
+    return p.C == 12 ? tables_match(p, encode_net12_coef(), 12, 4) : tables_match(p, encode_net10_coef(), 10, 4);
 }
 
 static bool dma_supported(const GfApplyParams& p, uint64_t shard_len, uint64_t n_stripes) {
@@ -1715,14 +1737,23 @@ hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shar
         if (ring_supported((int)p.C, (int)p.R, shard_len, E) && aligned16(p))
             return launch_encode_hash_ring(p, h, shard_len, n_stripes, E, stream);
     }
+    // RSG_FUSED_KIND=net: the 8-stripe network kernel for RS(8,4) too (A/B)
+    if (kind == 8 && net_enc_supported(p, n_stripes)) return launch_encode_hash_net_c(p, h, shard_len, n_stripes, stream);
     // RS(8,4), 2048+ stripes: the LDS-DMA bit-sliced kernel (RSG_FUSED_KIND=
     // packed keeps the table kernel for A/B runs)
     if (kind != 1 && (kind == 3 || n_stripes >= 2048) && dma_supported(p, shard_len, n_stripes))
         return launch_encode_hash_dma(p, h, shard_len, n_stripes, stream);
-    // RS(12,4), 1024+ stripes: the network kernel (LDS-DMA ring, 4 network
-    // waves, any shard length and alignment); RSG_FUSED_KIND=packed keeps the
-    // table kernel for A/B runs
-    if (kind != 1 && net12_supported(p, n_stripes)) return launch_encode_hash_net12(p, h, shard_len, n_stripes, stream);
+    // RS(12,4) / RS(10,4), 1024+ stripes: the network kernel (LDS-DMA ring, 4
+    // network waves, any shard length and alignment); RSG_FUSED_KIND=packed
+    // keeps the table kernel for A/B runs
+    if (kind != 1 && netq_enc_supported(p, n_stripes))
+        return p.C == 12 ? launch_encode_hash_net12(p, h, shard_len, n_stripes, stream)
+                         : launch_encode_hash_net10(p, h, shard_len, n_stripes, stream);
+    // RS(6,4), 2048+ stripes: the 8-stripe network kernel (n = 4096 at 1 MiB
+    // blocks: 2.11 -> 1.62 ms; RS(4,4) measured 1.5 % slower than the packed
+    // table kernel and keeps it, profiles/r05/ab_fused_net/)
+    if (kind != 1 && p.C == 6 && net_enc_supported(p, n_stripes))
+        return launch_encode_hash_net_c(p, h, shard_len, n_stripes, stream);
     const FusedPick f = pick_fused((int)p.C, (int)p.R, !unpacked);
     if (!f.k || !fused_supported((int)p.C, (int)p.R, shard_len) || n_stripes == 0 || n_stripes > 0x7fffffffull)
         return hipErrorInvalidValue;

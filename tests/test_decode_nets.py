@@ -75,18 +75,19 @@ def _expected_rows(p, files):
 
 def test_decode_net_table_shapes():
     src, pats = _table()
-    assert len(pats) == int(re.search(r"kCount = (\d+)", src).group(1)) == 146
+    assert len(pats) == int(re.search(r"kCount = (\d+)", src).group(1)) == 147
     keys = set()
     for p in pats:
         lost = [i for i in range(T) if p["absent"] >> i & 1]
         files = [i for i in range(T) if i not in lost]
-        assert 1 <= len(lost) <= 2 and p["nf"] == len(files)
+        # one or two lost shards, or (heal) all four parity shards: the fused encode's rows
+        assert (1 <= len(lost) <= 2 or (p["heal"] and lost == list(range(K, T)))) and p["nf"] == len(files)
         assert p["R"] == len(_expected_rows(p, files)) <= 4
         assert p["nst"] == (len(lost) if p["heal"] else len([i for i in lost if i < K])) >= 1
         keys.add((p["heal"], p["absent"]))
     assert len(keys) == len(pats)
     # GET: every pattern with a lost data shard; heal: every 1- and 2-shard loss
-    assert sum(1 for p in pats if p["heal"]) == 12 + 66
+    assert sum(1 for p in pats if p["heal"]) == 12 + 66 + 1  # + all four parity shards: the fused encode
     assert sum(1 for p in pats if not p["heal"]) == 8 + 28 + 8 * 4
 
 
@@ -192,7 +193,7 @@ def test_rs10_decode_nets_rebuild_true_shards(oracle):
         pats.append(dict(absent=int(m.group(1), 16), heal=int(m.group(2)), nf=int(m.group(3)), R=int(m.group(4)),
                          nst=int(m.group(5)), coef=rows, pid=int(m.group(7))))
     assert len(pats) == int(re.search(r"kCount = (\d+)", src).group(1))
-    assert sum(1 for p in pats if p["heal"]) == 14 + 91
+    assert sum(1 for p in pats if p["heal"]) == 14 + 91 + 1  # + all four parity shards: the fused encode
     assert sum(1 for p in pats if not p["heal"]) == 10 + 45 + 10 * 4
     rng = np.random.default_rng(104)
     gm = oracle.matrix(k, 4)
@@ -237,7 +238,7 @@ def test_rs6_rs4_decode_nets_rebuild_true_shards(oracle, k):
         pats.append(dict(absent=int(m.group(1), 16), heal=int(m.group(2)), nf=int(m.group(3)), R=int(m.group(4)),
                          nst=int(m.group(5)), coef=rows, pid=int(m.group(7))))
     assert len(pats) == int(re.search(r"kCount = (\d+)", src).group(1))
-    assert sum(1 for p in pats if p["heal"]) == t + t * (t - 1) // 2
+    assert sum(1 for p in pats if p["heal"]) == t + t * (t - 1) // 2 + 1  # + the fused encode's
     assert sum(1 for p in pats if not p["heal"]) == k + k * (k - 1) // 2 + k * 4
     rng = np.random.default_rng(k * 10 + 4)
     gm = oracle.matrix(k, 4)

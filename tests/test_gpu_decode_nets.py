@@ -370,10 +370,10 @@ def records4(gpu, oracle):
 def test_rs6_rs10_tables_list_every_pattern():
     """Every one- and two-shard loss: RS(6,4) 6 + 39 GET patterns (a data
     shard among the lost) and 10 + 45 heal patterns; RS(10,4) 10 + 85 and
-    14 + 91."""
-    assert len([x for x in LISTED6 if not x[0]]) == 6 + 39 and len([x for x in LISTED6 if x[0]]) == 10 + 45
-    assert len([x for x in LISTED10 if not x[0]]) == 10 + 85 and len([x for x in LISTED10 if x[0]]) == 14 + 91
-    assert len([x for x in LISTED4 if not x[0]]) == 4 + 22 and len([x for x in LISTED4 if x[0]]) == 8 + 28
+    14 + 91; each + the heal of all four parity shards (the fused encode's)."""
+    assert len([x for x in LISTED6 if not x[0]]) == 6 + 39 and len([x for x in LISTED6 if x[0]]) == 10 + 45 + 1
+    assert len([x for x in LISTED10 if not x[0]]) == 10 + 85 and len([x for x in LISTED10 if x[0]]) == 14 + 91 + 1
+    assert len([x for x in LISTED4 if not x[0]]) == 4 + 22 and len([x for x in LISTED4 if x[0]]) == 8 + 28 + 1
 
 
 def _geo_case(oracle, k, data, heal, lost, m=4):

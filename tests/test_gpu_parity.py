@@ -338,7 +338,13 @@ def test_host_batch_pipeline_matches_oracle(gpu, oracle, k, m, S, n, hashed):
     (12, 4, 31, 1030),     # network kernel: the remainder packet alone
     (12, 4, 1, 1024),      # network kernel: one-byte shards
     (6, 4, 174763, 3),   # RS(6,4) at 1 MiB: odd shard length
+    (6, 4, 174763, 2050),  # RS(6,4)'s 8-stripe network kernel (n >= 2048): odd records, a last workgroup of 2
+    (4, 4, 4000, 2048),    # RS(4,4)'s network kernel: ragged walk (7 steps + 416 bytes)
+    (6, 4, 31, 2049),      # RS(6,4) network kernel: the remainder packet alone
     (10, 4, 104858, 3),  # RS(10,4) at 1 MiB
+    (10, 4, 104858, 1030),  # RS(10,4)'s network kernel (n >= 1024): ragged walk, a last workgroup of 2 stripes
+    (10, 4, 1000, 1024),    # RS(10,4) network kernel: one whole step + 488 bytes
+    (10, 4, 31, 1025),      # RS(10,4) network kernel: the remainder packet alone
     (3, 2, 31, 5),       # a shard shorter than one packet: the remainder packet alone
     (5, 3, 1, 4),        # one-byte shards
     (8, 4, 544, 3),      # one whole chunk + one whole packet
@@ -346,7 +352,8 @@ def test_host_batch_pipeline_matches_oracle(gpu, oracle, k, m, S, n, hashed):
 ])
 def test_fused_kernel_selection_matches_oracle(gpu, oracle, k, m, S, n):
     """Every fused encode+HH256S kernel the launcher can pick (ring E=1/2,
-    packed, RS(12,4)'s network kernel) against the oracle; large batches are
+    packed, the network kernels of RS(12,4), RS(10,4), RS(6,4) and RS(4,4))
+    against the oracle; large batches are
     checked on a sample of stripes that includes the first and last."""
     import torch
     from rustfs_amd import Erasure
@@ -363,6 +370,16 @@ def test_fused_kernel_selection_matches_oracle(gpu, oracle, k, m, S, n):
         assert (host[s] == ref).all(), s
         for i in range(k + m):
             assert hd[s, i].tobytes() == oracle.hh256s(ref[i]), (s, i)
+
+
+@pytest.mark.parametrize("n,S", [(2048, 4096), (2051, 1000)])
+def test_fused_net_kernel_forced_rs84(gpu, oracle, n, S):
+    """RS(8,4) on the 8-stripe network kernel's fused encode (RSG_FUSED_KIND=
+    net through rsg_set_tuning; the default picks k_encode_hash_dma): parity
+    and all 12 digests against the oracle on a sample of stripes."""
+    from rustfs_amd import _lib
+    with _lib.tuned(RSG_FUSED_KIND="net"):
+        test_fused_kernel_selection_matches_oracle(gpu, oracle, 8, 4, S, n)
 
 
 @pytest.mark.parametrize("k,m,S", [(200, 56, 67), (128, 128, 48), (255, 1, 33), (1, 255, 40)])

@@ -113,7 +113,7 @@ def patterns():
     # RS(12,4): also the heal of all four parity shards — rows = the encode
     # matrix over the data shards, which the fused encode + HH256S kernel
     # (rs_decode_netq.hip, k_encode_hash_net12) runs as its network
-    every_parity = [tuple(range(K, T))] if K == 12 else []
+    every_parity = [tuple(range(K, T))] if K in (12, 10, 8, 6, 4) else []
     for heal in (0, 1):
         for lost in losses + (every_parity if heal else []):
             present = [0 if i in lost else 1 for i in range(T)]
