@@ -125,7 +125,7 @@ int rsg_set_record_engine(rsg_ctx *ctx, int engine);
  * syntax): RSG_FUSED, RSG_LOST_DISK_FAST, RSG_ZERO_COPY, RSG_ROLLED,
  * RSG_HASH_COPY, RSG_FUSED_SPW1, RSG_DECODE_NET, RSG_HASH_UNAL, RSG_GET_CACHED
  * (0|1); RSG_VEC_BLOCK (0|64|256); RSG_VEC_OCC (-1..8); RSG_HASH_DEPTH (1..3);
- * RSG_FUSED_KIND (auto|packed|ring|dma|wide2|wide4|split2|split4|net);
+ * RSG_FUSED_KIND (auto|packed|ring|dma|wide2|wide4|split2|split4|net|table);
  * RSG_ENC_PRIO, RSG_DMA_PRIO, RSG_DMA_NT (0..3); RSG_DMA_EW (2|4);
  * RSG_DMA_SPW (4|8); RSG_NET12_RD (2; 4 only in measurement builds, whose
  * library carries that A/B kernel form).  INTEGRATION.md lists what each

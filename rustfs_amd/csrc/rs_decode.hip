@@ -65,7 +65,11 @@ struct GetShape : RecRing<NF, G, TH> {
     static constexpr int WPE = RD == 2 ? (2 * WAVES + 3) / 4 : 1;
 };
 
-template <int C, int NF, int G, int TH, int RD = dma::D, int RM = 4>
+// ENC: the fused encode + HH256S over a stripe buffer (launch_encode_hash_table:
+// the heal of every parity shard, p.out_* the parity rows in place, every
+// digest to h.out in the batch digest layout instead of verified / written
+// record headers).
+template <int C, int NF, int G, int TH, int RD = dma::D, int RM = 4, bool ENC = false>
 __global__ __launch_bounds__((64 * GetShape<NF, G, TH, RD>::WAVES))
 __attribute__((amdgpu_waves_per_eu(GetShape<NF, G, TH, RD>::WPE))) void k_decode_records_dma(const GfApplyParams p,
                                                                                             const HashParams h) {
@@ -95,14 +99,14 @@ __attribute__((amdgpu_waves_per_eu(GetShape<NF, G, TH, RD>::WPE))) void k_decode
 
     if constexpr (TH > 0 && !L::MERGE) {
         if (wave >= (uint32_t)(L::HW + SPW)) {
-            records_target_hasher<G, TH, 1, false, 2, 0, false, L::WPE>(&karg_gf(), &karg_hash(), trow,
+            records_target_hasher<G, TH, 1, ENC, 2, 0, false, L::WPE>(&karg_gf(), &karg_hash(), trow,
                                                                        wave - L::HW - SPW, steps, s0);
             return;
         }
     }
     if constexpr (L::MERGE) {
         if (wave == (uint32_t)(L::HW - 1)) {  // the last hash wave hashes the target rows too
-            records_hash_target_wave<NF, G, RD, TH, 2, L::TSLOT, 1, false, L::WPE>(&karg_gf(), &karg_hash(), ring, trow, wave, steps, s0);
+            records_hash_target_wave<NF, G, RD, TH, 2, L::TSLOT, 1, false, L::WPE, ENC>(&karg_gf(), &karg_hash(), ring, trow, wave, steps, s0);
             return;
         }
     }
@@ -190,7 +194,7 @@ __attribute__((amdgpu_waves_per_eu(GetShape<NF, G, TH, RD>::WPE))) void k_decode
         return;
     }
     // ------------------------- DMA + verify-hash wave -------------------------
-    records_hash_wave<NF, G, 0, RD, false, L::WPE>(&karg_hash(), p.wave_prio, ring, wave, steps, s0);
+    records_hash_wave<NF, G, 0, RD, ENC, L::WPE>(&karg_hash(), p.wave_prio, ring, wave, steps, s0);
 }
 
 // 4-stripe workgroups (C > 8) on a 2-slot ring where it fits half a CU's LDS
@@ -207,10 +211,10 @@ constexpr int table_rd() {
                : dma::D;
 }
 
-template <int C, int NF, int G, int TH = 0, int RM = 4>
+template <int C, int NF, int G, int TH = 0, int RM = 4, bool ENC = false>
 static void launch_get(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
     constexpr int RD = table_rd<C, NF, G, TH, RM>();
-    hipLaunchKernelGGL((k_decode_records_dma<C, NF, G, TH, RD, RM>), dim3((uint32_t)blocks),
+    hipLaunchKernelGGL((k_decode_records_dma<C, NF, G, TH, RD, RM, ENC>), dim3((uint32_t)blocks),
                        dim3(64 * GetShape<NF, G, TH, RD>::WAVES), 0, stream, p, h);
 }
 
@@ -289,6 +293,22 @@ int RSG_DEC_CAT(launch_get_wide_, RSG_DECODE_C)(int m, int nf, int th, uint64_t 
     return kTabInvalid;
 }
 #elif defined(RSG_DECODE_C)
+// This part's fused encode + HH256S (k = C data shards, m = 1..4 parity):
+// the heal of every parity shard with ENC.
+bool RSG_DEC_CAT(launch_enc_tab_, RSG_DECODE_C)(int m, uint64_t n_stripes, const GfApplyParams& p,
+                                                const HashParams& h, hipStream_t stream) {
+    constexpr int C = RSG_DECODE_C, G = get_group(C);
+    const uint64_t blocks = (n_stripes + G - 1) / G;
+    if (blocks > 0x7fffffffull) return false;
+    switch (m) {
+        case 1: launch_get<C, C, G, 1, 4, true>(blocks, p, h, stream); return true;
+        case 2: launch_get<C, C, G, 2, 4, true>(blocks, p, h, stream); return true;
+        case 3: launch_get<C, C, G, 3, 4, true>(blocks, p, h, stream); return true;
+        case 4: launch_get<C, C, G, 4, 4, true>(blocks, p, h, stream); return true;
+    }
+    return false;
+}
+
 // This part's survivor count: GET (th = 0) and heal (th = 1..4 targets).
 int RSG_DEC_CAT(launch_get_tab_, RSG_DECODE_C)(int nf, int th, uint64_t n_stripes, const GfApplyParams& p,
                                                const HashParams& h, bool any_table, hipStream_t stream) {
@@ -319,6 +339,22 @@ int launch_get_tab_13(int, int, uint64_t, const GfApplyParams&, const HashParams
 int launch_get_tab_14(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
 int launch_get_tab_15(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
 int launch_get_tab_16(int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
+bool launch_enc_tab_1(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_enc_tab_2(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_enc_tab_3(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_enc_tab_4(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_enc_tab_5(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_enc_tab_6(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_enc_tab_7(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_enc_tab_8(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_enc_tab_9(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_enc_tab_10(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_enc_tab_11(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_enc_tab_12(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_enc_tab_13(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_enc_tab_14(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_enc_tab_15(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+bool launch_enc_tab_16(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
 int launch_get_wide_5(int, int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
 int launch_get_wide_6(int, int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
 int launch_get_wide_7(int, int, int, uint64_t, const GfApplyParams&, const HashParams&, bool, hipStream_t);
@@ -463,6 +499,37 @@ hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, 
     const int r = launch_get_any(k, m, nf, targets, n_stripes, p, h, any_table, stream);
     if (r == kTabDeclined) return hipErrorNotSupported;
     if (r != kTabLaunched) return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+// The fused encode + HH256S on the run-time-table one-pass kernel (the heal
+// of every parity shard over a stripe buffer in place, ENC): k data shards
+// (1..16), m = p.R parity (1..4).  p: the encode's table launch (base ==
+// out_base, in_off the data rows, out_off the parity rows); h: key, out.
+hipError_t launch_encode_hash_table(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
+                                    hipStream_t stream) {
+    using EncLaunch = bool (*)(int, uint64_t, const GfApplyParams&, const HashParams&, hipStream_t);
+    static const EncLaunch parts[16] = {launch_enc_tab_1,  launch_enc_tab_2,  launch_enc_tab_3,  launch_enc_tab_4,
+                                        launch_enc_tab_5,  launch_enc_tab_6,  launch_enc_tab_7,  launch_enc_tab_8,
+                                        launch_enc_tab_9,  launch_enc_tab_10, launch_enc_tab_11, launch_enc_tab_12,
+                                        launch_enc_tab_13, launch_enc_tab_14, launch_enc_tab_15, launch_enc_tab_16};
+    const int k = (int)p.C, m = (int)p.R;
+    if (k < 1 || k > 16 || m < 1 || m > 4 || n_stripes == 0 || !walk_length_ok(shard_len) || p.base != p.out_base ||
+        p.stripe_stride != p.out_stripe_stride || 5 * p.stripe_stride >= (1ull << 32))
+        return hipErrorInvalidValue;
+    p.n_store = (uint32_t)m;
+    p.copy_mask = 0;
+    p.mode = GF_MODE_STORE_COMPARE;
+    p.wave_prio = dma_prio();
+    p.units = (uint32_t)((shard_len + dma::CH - 1) / dma::CH);
+    p.byte_end = shard_len;
+    h.len = shard_len;
+    h.n = n_stripes;
+    h.shards = (uint64_t)(k + m);
+    h.stripe_stride = p.stripe_stride;
+    h.nbases = (uint32_t)k;
+    for (int c = 0; c < k; ++c) h.base[c] = p.base + p.in_off[c];
+    if (!parts[k - 1](m, n_stripes, p, h, stream)) return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

@@ -39,7 +39,7 @@ struct Tuning {
     bool rolled = false;          // RSG_ROLLED=1: rolled GF kernel for every C
     bool hash_direct_copy = false;  // RSG_HASH_COPY=1: 8-byte copy stores in the GET gather
     int hash_depth = 2;           // RSG_HASH_DEPTH=1..3: 8-packet batches in flight per lane
-    int fused_kind = 0;           // RSG_FUSED_KIND=packed|ring|dma|wide2|wide4|split2|split4|net (0: by batch size)
+    int fused_kind = 0;  // RSG_FUSED_KIND=packed|ring|dma|wide2|wide4|split2|split4|net|table (0: by batch size)
     bool fused_spw1 = false;      // RSG_FUSED_SPW1=1: one stripe per packed workgroup
     int enc_prio = 0;             // RSG_ENC_PRIO=<0..3>: wave priorities of the fused DMA kernel
     int dma_ew = 2;               // RSG_DMA_EW=4: two encoder waves per stripe group (split, alternate steps)
@@ -138,6 +138,10 @@ hipError_t launch_encode_hash_net12(GfApplyParams p, HashParams h, uint64_t shar
 // ... and RS(10,4)'s (k_decode_records_net10 over rs104_decode_nets.h).
 const uint8_t* encode_net10_coef();
 hipError_t launch_encode_hash_net10(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
+                                    hipStream_t stream);
+// The fused encode + HH256S on the run-time-table one-pass kernel for any k
+// <= 16, m <= 4 (rs_decode.hip, ENC).
+hipError_t launch_encode_hash_table(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                     hipStream_t stream);
 // ... and RS(8,4)'s, RS(6,4)'s, RS(4,4)'s (rs_decode_net.hip, 8-stripe
 // workgroups, two network waves).

@@ -1198,9 +1198,9 @@ bool set_knob(Tuning& v, const std::string& name, const char* value) {
     if (name == "RSG_HASH_COPY") return flag(v.hash_direct_copy);
     if (name == "RSG_HASH_DEPTH") return num(v.hash_depth, 1, 3);
     if (name == "RSG_FUSED_KIND") {
-        static const char* const kinds[] = {"auto",  "packed", "ring",   "dma",   "wide2",
-                                            "wide4", "split2", "split4", "net"};
-        for (int i = 0; i < 9; ++i)
+        static const char* const kinds[] = {"auto",   "packed", "ring", "dma",  "wide2",
+                                            "wide4",  "split2", "split4", "net", "table"};
+        for (int i = 0; i < 10; ++i)
             if (s == kinds[i]) {
                 v.fused_kind = i;
                 return true;
@@ -1233,9 +1233,9 @@ bool knob_value(const Tuning& v, const std::string& name, std::string& out) {
     if (name == "RSG_HASH_COPY") return b(v.hash_direct_copy);
     if (name == "RSG_HASH_DEPTH") return i(v.hash_depth);
     if (name == "RSG_FUSED_KIND") {
-        static const char* const kinds[] = {"auto",  "packed", "ring",   "dma",   "wide2",
-                                            "wide4", "split2", "split4", "net"};
-        out = kinds[v.fused_kind >= 0 && v.fused_kind < 9 ? v.fused_kind : 0];
+        static const char* const kinds[] = {"auto",   "packed", "ring", "dma",  "wide2",
+                                            "wide4",  "split2", "split4", "net", "table"};
+        out = kinds[v.fused_kind >= 0 && v.fused_kind < 10 ? v.fused_kind : 0];
         return true;
     }
     if (name == "RSG_FUSED_SPW1") return b(v.fused_spw1);
@@ -1632,6 +1632,14 @@ static hipError_t launch_encode_hash_net_c(const GfApplyParams& p, const HashPar
     return launch_encode_hash_net4(p, h, shard_len, n_stripes, stream);
 }
 
+// Any k <= 16, m <= 4 encode in place: the run-time-table one-pass kernel
+// with ENC (rs_decode.hip).
+static bool table_enc_supported(const GfApplyParams& p, uint64_t n_stripes) {
+    return p.C >= 1 && p.C <= 16 && p.R >= 1 && p.R <= 4 && p.mode == GF_MODE_STORE && !p.copy_mask &&
+           p.base == p.out_base && p.stripe_stride == p.out_stripe_stride && n_stripes >= 1 &&
+           5 * p.stripe_stride < (1ull << 32);
+}
+
 static bool netq_enc_supported(const GfApplyParams& p, uint64_t n_stripes) {
     if ((p.C != 12 && p.C != 10) || p.R != 4 || p.mode != GF_MODE_STORE || p.copy_mask || p.base != p.out_base ||
         p.stripe_stride != p.out_stripe_stride || n_stripes < 1024 || 5 * p.stripe_stride >= (1ull << 32))
@@ -1737,6 +1745,9 @@ hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shar
         if (ring_supported((int)p.C, (int)p.R, shard_len, E) && aligned16(p))
             return launch_encode_hash_ring(p, h, shard_len, n_stripes, E, stream);
     }
+    // RSG_FUSED_KIND=table: the run-time-table one-pass kernel (A/B)
+    if (kind == 9 && table_enc_supported(p, n_stripes))
+        return launch_encode_hash_table(p, h, shard_len, n_stripes, stream);
     // RSG_FUSED_KIND=net: the 8-stripe network kernel for RS(8,4) too (A/B)
     if (kind == 8 && net_enc_supported(p, n_stripes)) return launch_encode_hash_net_c(p, h, shard_len, n_stripes, stream);
     // RS(8,4), 2048+ stripes: the LDS-DMA bit-sliced kernel (RSG_FUSED_KIND=
@@ -1754,6 +1765,13 @@ hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shar
     // table kernel and keeps it, profiles/r05/ab_fused_net/)
     if (kind != 1 && p.C == 6 && net_enc_supported(p, n_stripes))
         return launch_encode_hash_net_c(p, h, shard_len, n_stripes, stream);
+    // k >= 9 without a network (RS(9,4), RS(11,4), RS(13,3), RS(14,2),
+    // RS(15,1), ...) and RS(4,4), 1024+ stripes: the run-time-table one-pass
+    // kernel with ENC — 2-9 % faster than the packed kernel there (4-stripe
+    // workgroups, two a CU), 6-12 % slower at k <= 8 otherwise
+    // (profiles/r05/fused_table/)
+    if (kind != 1 && n_stripes >= 1024 && (p.C >= 9 || (p.C == 4 && p.R == 4)) && table_enc_supported(p, n_stripes))
+        return launch_encode_hash_table(p, h, shard_len, n_stripes, stream);
     const FusedPick f = pick_fused((int)p.C, (int)p.R, !unpacked);
     if (!f.k || !fused_supported((int)p.C, (int)p.R, shard_len) || n_stripes == 0 || n_stripes > 0x7fffffffull)
         return hipErrorInvalidValue;

@@ -264,7 +264,8 @@ RSG_RECORD_WAVE void records_hash_wave(KHash* h_in, uint32_t wave_prio, uint8_t*
 // kernels' accumulators; LAG 1: the table kernel's GF waves write whole rows) —
 // and at the end writes the target record's digest header
 // (BitrotWriter::write).  steps + LAG barriers.
-template <int NF, int G, int RD, int TTH, int TNS, uint32_t TSLOT, int LAG = 2, bool ZERO = true, int OCC = 0>
+template <int NF, int G, int RD, int TTH, int TNS, uint32_t TSLOT, int LAG = 2, bool ZERO = true, int OCC = 0,
+          bool ENC = false>
 RSG_RECORD_WAVE void records_hash_target_wave(KGf* p_in, KHash* h_in, uint8_t* ring_in, uint8_t* trow_in,
                                               uint32_t hw_in, uint32_t steps_in, uint64_t s0_in) {
     KGf& p = uni(p_in);
@@ -418,8 +419,14 @@ RSG_RECORD_WAVE void records_hash_target_wave(KGf* p_in, KHash* h_in, uint8_t* r
         absorb(steps + l);
     }
     // ring quads: verify before use (bitrot.rs:227-247); target quads: the
-    // target record's digest header (BitrotWriter::write)
+    // target record's digest header (BitrotWriter::write).  ENC (the fused
+    // encode): every digest to the batch digest layout, data then parity.
     const uint64_t d = hhq_digest(st, q);
+    if constexpr (ENC) {
+        if (live) st64_any(h.out + ((s0 + stripe_l) * h.shards + file) * 32 + 8 * q, d);
+        if (tlive) st64_any(h.out + ((s0 + te) * h.shards + p.C + tr) * 32 + 8 * q, d);
+        return;
+    }
     bool mis = false;
     if (live) mis = d != ld64_any(h.base[file] + (s0 + stripe_l) * h.stripe_stride - 32 + 8 * q);
     const uint64_t bal = __builtin_amdgcn_ballot_w64(mis);
