@@ -225,7 +225,9 @@ enum { kTabInvalid = 0, kTabLaunched = 1, kTabDeclined = 2 };
 template <int C, int G, int TH, int NF>
 static int launch_get_nf(int nf, uint64_t n_stripes, const GfApplyParams& p, const HashParams& h, bool any_table,
                          hipStream_t stream) {
-    if constexpr (NF + (TH ? TH : 1) > C + 4) {
+    // (patterns of more than 16 shards are not built: rustfs stores at most
+    // 16, MAX_ERASURE_SHARDS, fileinfo.rs:38 — one_pass_geometry)
+    if constexpr (NF + (TH ? TH : 1) > C + 4 || NF + (TH ? TH : 1) > 16) {
         return kTabInvalid;
     } else {
         if (nf != NF) return launch_get_nf<C, G, TH, NF + 1>(nf, n_stripes, p, h, any_table, stream);
@@ -294,17 +296,28 @@ int RSG_DEC_CAT(launch_get_wide_, RSG_DECODE_C)(int m, int nf, int th, uint64_t 
 }
 #elif defined(RSG_DECODE_C)
 // This part's fused encode + HH256S (k = C data shards, m = 1..4 parity):
-// the heal of every parity shard with ENC.
+// the heal of every parity shard with ENC — built where the fused launcher
+// takes it (table_enc_geometry: k >= 9, and RS(4,4)); false elsewhere.
+constexpr bool table_enc_geometry(int k, int m) { return (k >= 9 && k + m <= 16) || (k == 4 && m == 4); }
+template <int C, int M>
+static bool launch_enc_m(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
+    if constexpr (!table_enc_geometry(C, M)) {
+        return false;
+    } else {
+        launch_get<C, C, get_group(C), M, 4, true>(blocks, p, h, stream);
+        return true;
+    }
+}
 bool RSG_DEC_CAT(launch_enc_tab_, RSG_DECODE_C)(int m, uint64_t n_stripes, const GfApplyParams& p,
                                                 const HashParams& h, hipStream_t stream) {
     constexpr int C = RSG_DECODE_C, G = get_group(C);
     const uint64_t blocks = (n_stripes + G - 1) / G;
     if (blocks > 0x7fffffffull) return false;
     switch (m) {
-        case 1: launch_get<C, C, G, 1, 4, true>(blocks, p, h, stream); return true;
-        case 2: launch_get<C, C, G, 2, 4, true>(blocks, p, h, stream); return true;
-        case 3: launch_get<C, C, G, 3, 4, true>(blocks, p, h, stream); return true;
-        case 4: launch_get<C, C, G, 4, 4, true>(blocks, p, h, stream); return true;
+        case 1: return launch_enc_m<C, 1>(blocks, p, h, stream);
+        case 2: return launch_enc_m<C, 2>(blocks, p, h, stream);
+        case 3: return launch_enc_m<C, 3>(blocks, p, h, stream);
+        case 4: return launch_enc_m<C, 4>(blocks, p, h, stream);
     }
     return false;
 }
@@ -379,17 +392,17 @@ static int launch_get_any(int k, int m, int nf, int th, uint64_t n_stripes, cons
     return parts[k - 1](nf, th, n_stripes, p, h, any_table, stream);
 }
 
-// Geometries with a one-pass kernel: every k <= 16 with m <= 4 — every set
-// of 2 to 16 drives (disks_layout.rs:25, MAX_ERASURE_SHARDS = 16 in
-// fileinfo.rs:38) at its default parity (storageclass.rs:24-31), the reduced-
-// redundancy class's one parity shard (storageclass.rs:99, 326-331) and
-// explicit EC:1..4 — any shard length (a ragged last step, rs_records.h
-// walk_tail).
+// Geometries with a one-pass kernel: every k <= 16 with m <= 4 and k + m <=
+// 16 — every set of 2 to 16 drives (disks_layout.rs:25, MAX_ERASURE_SHARDS =
+// 16 in fileinfo.rs:38) at its default parity (storageclass.rs:24-31), the
+// reduced-redundancy class's one parity shard (storageclass.rs:99, 326-331)
+// and explicit EC:1..4 — any shard length (a ragged last step, rs_records.h
+// walk_tail).  Larger sets (RS(16,4): 20 shards) take the two-pass path.
 static bool walk_length_ok(uint64_t shard_len) {
     return shard_len >= 1 && (shard_len + dma::CH - 1) / dma::CH <= 0xffffffffull;
 }
 static bool one_pass_geometry(int k, int m, uint64_t shard_len) {
-    return k >= 1 && k <= 16 && m >= 1 && m <= 4 && walk_length_ok(shard_len);
+    return k >= 1 && k <= 16 && m >= 1 && m <= 4 && k + m <= 16 && walk_length_ok(shard_len);
 }
 // ... and the explicit classes EC:5..8 (m <= k, k + m <= 16 drives:
 // storageclass.rs:480-498) for their one- and two-loss patterns

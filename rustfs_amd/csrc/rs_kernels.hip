@@ -1632,10 +1632,11 @@ static hipError_t launch_encode_hash_net_c(const GfApplyParams& p, const HashPar
     return launch_encode_hash_net4(p, h, shard_len, n_stripes, stream);
 }
 
-// Any k <= 16, m <= 4 encode in place: the run-time-table one-pass kernel
-// with ENC (rs_decode.hip).
+// k >= 9 (m <= 4, k + m <= 16) or RS(4,4) encode in place: the run-time-table
+// one-pass kernel with ENC (rs_decode.hip builds it for those geometries only).
 static bool table_enc_supported(const GfApplyParams& p, uint64_t n_stripes) {
-    return p.C >= 1 && p.C <= 16 && p.R >= 1 && p.R <= 4 && p.mode == GF_MODE_STORE && !p.copy_mask &&
+    return ((p.C >= 9 && p.C + p.R <= 16) || (p.C == 4 && p.R == 4)) && p.R >= 1 && p.R <= 4 &&
+           p.mode == GF_MODE_STORE && !p.copy_mask &&
            p.base == p.out_base && p.stripe_stride == p.out_stripe_stride && n_stripes >= 1 &&
            5 * p.stripe_stride < (1ull << 32);
 }
@@ -1770,7 +1771,7 @@ hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shar
     // kernel with ENC — 2-9 % faster than the packed kernel there (4-stripe
     // workgroups, two a CU), 6-12 % slower at k <= 8 otherwise
     // (profiles/r05/fused_table/)
-    if (kind != 1 && n_stripes >= 1024 && (p.C >= 9 || (p.C == 4 && p.R == 4)) && table_enc_supported(p, n_stripes))
+    if (kind != 1 && n_stripes >= 1024 && table_enc_supported(p, n_stripes))
         return launch_encode_hash_table(p, h, shard_len, n_stripes, stream);
     const FusedPick f = pick_fused((int)p.C, (int)p.R, !unpacked);
     if (!f.k || !fused_supported((int)p.C, (int)p.R, shard_len) || n_stripes == 0 || n_stripes > 0x7fffffffull)

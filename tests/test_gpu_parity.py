@@ -382,15 +382,16 @@ def test_fused_net_kernel_forced_rs84(gpu, oracle, n, S):
         test_fused_kernel_selection_matches_oracle(gpu, oracle, 8, 4, S, n)
 
 
-@pytest.mark.parametrize("k,m,S,n", [(5, 4, 1000, 19), (11, 4, 4099, 9), (3, 2, 31, 7), (14, 2, 1536, 5),
-                                     (16, 4, 600, 6), (1, 1, 100, 3), (9, 4, 1024, 13), (13, 3, 2049, 4),
-                                     (8, 4, 4096, 10), (15, 1, 513, 11)])
+@pytest.mark.parametrize("k,m,S,n", [(4, 4, 1000, 19), (11, 4, 4099, 9), (9, 2, 31, 7), (14, 2, 1536, 5),
+                                     (12, 3, 600, 6), (10, 1, 100, 3), (9, 4, 1024, 13), (13, 3, 2049, 4),
+                                     (12, 4, 4096, 10), (15, 1, 513, 11)])
 def test_fused_table_kernel_forced(gpu, oracle, k, m, S, n):
     """The fused encode + HH256S on the run-time-table one-pass kernel (ENC:
     the heal of every parity shard over the stripe buffer; RSG_FUSED_KIND=
     table through rsg_set_tuning): parity and every digest against the oracle
-    — 8- and 4-stripe workgroups, partial last workgroups, ragged walks, a
-    lone remainder packet."""
+    — RS(4,4)'s 8-stripe and k >= 9's 4-stripe workgroups (the geometries it
+    is built for), partial last workgroups, ragged walks, a lone remainder
+    packet."""
     from rustfs_amd import _lib
     with _lib.tuned(RSG_FUSED_KIND="table"):
         test_fused_kernel_selection_matches_oracle(gpu, oracle, k, m, S, n)
