@@ -19,5 +19,5 @@ timeout -k 10 600 python -u -m pytest tests -x -q --timeout 120 --timeout-method
 tail -1 $OUT/pytest_gpu.log
 timeout -k 10 300 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || exit 1
 cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $R/bench.py > $OUT/bench_prof.json 2> $OUT/bench_prof.err || exit 1
-cd $R && timeout -k 10 500 python -u tools/geom_engines.py 5,4 11,4 15,1 9,4 13,3 7,1 3,2 14,4 14,2 16,4 8,8 10,6 > $OUT/geom_engines.jsonl 2> $OUT/geom_engines.err || exit 1
+cd $R && timeout -k 10 500 python -u tools/geom_engines.py 5,4 11,4 15,1 9,4 13,3 7,1 3,2 14,2 8,8 10,6 > $OUT/geom_engines.jsonl 2> $OUT/geom_engines.err && timeout -k 10 300 python -u tools/verify_geoms.py 12,4 10,4 6,4 5,4 3,2 14,2 8,4 > $OUT/verify_geoms.jsonl 2> $OUT/verify_geoms.err || exit 1
 echo done
