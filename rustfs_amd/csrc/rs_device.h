@@ -165,7 +165,9 @@ __device__ __forceinline__ void gf_store_late(const GfApplyParams& p, uint8_t* o
         }
         const uint4 v = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
         if (mode == GF_MODE_STORE) {
-            st16(dst, v);
+            // non-temporal: the parity / rebuilt rows are not read back by this
+            // pass (RS(8,4) encode 1.074 -> 1.043-1.056 ms, profiles/r05/ab_nt/)
+            st16_nt(dst, v);
         } else if (mode == GF_MODE_XOR) {
             const uint4 o = ld16(dst);
             st16(dst, make_uint4(o.x ^ v.x, o.y ^ v.y, o.z ^ v.z, o.w ^ v.w));
