@@ -168,7 +168,10 @@ __attribute__((amdgpu_waves_per_eu(GetShape<NF, G, TH, RD>::WPE))) void k_decode
                 const uint2 v = make_uint2(acc[r][0], acc[r][1]);
                 if ((uint32_t)r < nst) {
                     if (live) {
-                        if (!part) st16_nt_half(ob + p.out_off[r] + (uint64_t)s * CH, v);
+                        // cached 8-byte stores: the L2 gathers the rows' 512-byte
+                        // steps (against non-temporal: GET -1 to -4 %, heal level,
+                        // profiles/r05/ab_tc/)
+                        if (!part) st64_any(ob + p.out_off[r] + (uint64_t)s * CH, u64_of(v));
                         else st64_part(ob + p.out_off[r] + (uint64_t)s * CH, u64_of(v), lane * 8u, tail);
                     }
                     if constexpr (TH > 0)
