@@ -2,7 +2,8 @@
 (rsg_set_tuning) on a device-resident batch at 1 MiB blocks: steady state
 (0.5 s busy), median of 20 calls timed with HIP events around each (the
 encode is one launch on the current stream).
-Usage: python tools/fused_kinds.py K M KIND [KIND ...]  (e.g. 8 4 auto dma net)"""
+Usage: python tools/fused_kinds.py K M KIND [KIND ...]  (e.g. 8 4 auto dma net);
+FK_TUNE="RSG_DMA_NT=1 ..." sets further knobs for the run."""
 import json
 import os
 import sys
@@ -20,8 +21,10 @@ def main():
     st = bench.random_stripes(torch.device("cuda", 0), k, m, S, n, 3)
     dig = torch.empty((n, k + m, 32), dtype=torch.uint8, device="cuda")
     out = {"geometry": f"RS({k},{m})", "n": n, "S": S}
+    extra = dict(kv.split("=", 1) for kv in os.environ.get("FK_TUNE", "").split() if kv)  # e.g. FK_TUNE="RSG_DMA_NT=1"
+    out["tune"] = extra
     for kind in sys.argv[3:]:
-        with _lib.tuned(RSG_FUSED_KIND=kind):
+        with _lib.tuned(RSG_FUSED_KIND=kind, **extra):
             fn = lambda: e.encode_batch(st, dig)  # noqa: E731
             bench.steady_loop(fn, 0.5)
             kms = []
