@@ -3,7 +3,8 @@
 (0.5 s busy), median of 20 calls timed with HIP events around each (the
 encode is one launch on the current stream).
 Usage: python tools/fused_kinds.py K M KIND [KIND ...]  (e.g. 8 4 auto dma net);
-FK_TUNE="RSG_DMA_NT=1 ..." sets further knobs for the run."""
+FK_TUNE="RSG_DMA_NT=1 ..." sets further knobs for the run; FK_PLAIN=1 times the
+plain encode (no digests) instead."""
 import json
 import os
 import sys
@@ -25,7 +26,7 @@ def main():
     out["tune"] = extra
     for kind in sys.argv[3:]:
         with _lib.tuned(RSG_FUSED_KIND=kind, **extra):
-            fn = lambda: e.encode_batch(st, dig)  # noqa: E731
+            fn = lambda: e.encode_batch(st, None if os.environ.get("FK_PLAIN") else dig)  # noqa: E731
             bench.steady_loop(fn, 0.5)
             kms = []
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
