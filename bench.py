@@ -68,6 +68,10 @@ def parse(argv=None):
                     help="config 5 extra: RS(16,4) stripes split over all GPUs (one GPU: its 1/8 share)")
     ap.add_argument("--no-rs12", action="store_true", help="skip the RS(12,4) (16-drive default) extras")
     ap.add_argument("--rs12-batch", type=int, default=4096, help="RS(12,4) extras: stripes")
+    ap.add_argument("--no-host-path", action="store_true",
+                    help="skip extras.host_path (host memory at both ends: pinned copies, host-batch encode, "
+                         "streamed GET / PUT)")
+    ap.add_argument("--host-path-blocks", type=int, default=1024, help="extras.host_path: 1 MiB blocks per call")
     ap.add_argument("--record-engine", choices=["auto", "one-pass", "two-pass"], default="auto",
                     help="GET/heal engine path for the engine extras (rsg_set_record_engine)")
     return ap.parse_args(argv)
@@ -601,6 +605,215 @@ def rs12_4_extras(a, dev, stream):
     return out
 
 
+def link_bound_ms(in_bytes, out_bytes, h2d_gbs, d2h_gbs):
+    """The fastest a host-memory call can run on the link: its bytes in at the
+    measured pinned H2D rate and its bytes out at the D2H rate, the two
+    directions overlapped (PCIe is full duplex), so the larger of the two."""
+    return max(in_bytes / (h2d_gbs * 1e9), out_bytes / (d2h_gbs * 1e9)) * 1e3
+
+
+def host_path_plan(k, m, S, n):
+    """The host-memory (PCIe-inclusive) entries of extras.host_path, north_star's
+    "the rate including pinned hipMemcpyAsync to and from the GPU": (name, bytes
+    in over the link, bytes out, payload bytes) per call.  Encode moves the k
+    data shards in and the m parity shards (+ all digests) out
+    (rsg_encode_batch_host, encode_batched's dispatch, encode.rs:795-919); the
+    streamed GET (pipeline.get_stream, decode_inner, decode.rs:1702-1968) moves
+    every present record in and only the rebuilt data shards out (the
+    in-place GET: present data are served from the host stage they were read
+    into); the streamed PUT moves the data in and every record's parity +
+    digests out."""
+    t, rec = k + m, 32 + S
+    return [("encode_batch_host", n * k * S, n * m * S, n * k * S),
+            ("encode_batch_host_hh256s", n * k * S, n * m * S + n * t * 32, n * k * S),
+            ("get_stream_all_present", n * t * rec, 0, n * k * S),
+            ("get_stream_2_data_lost", n * (t - 2) * rec, n * 2 * S, n * k * S),
+            ("put_stream_hh256s", n * k * S, n * m * S + n * t * 32, n * k * S)]
+
+
+def host_path_extras(dev, stream, n=1024, reps=5):
+    """extras.host_path: the path as the reference runs it, starting and
+    ending in host memory (north_star; SURVEY §8(d)'s pinned hipMemcpyAsync
+    rate).  RS(8,4), 1 MiB blocks, n blocks (1 GiB of payload):
+    - raw page-locked copy rates, H2D, D2H and both at once (two streams);
+    - rsg_encode_batch_host on page-locked stripes, without and with the fused
+      HH256S digests (H2D -> encode -> D2H pipelined inside the library);
+    - pipeline.get_stream over BitrotWriter shard files in tmpfs, all present
+      and with two data disks lost (pread into page-locked stages, H2D,
+      verify + rebuild on the GPU, rebuilt shards D2H, the range's bytes
+      yielded block by block);
+    - pipeline.put_stream of the same object from a tmpfs body file (pread
+      into page-locked batches, encode + digests on the GPU, one writev per
+      shard file).
+    Each entry: ms per call (best of `reps` after a warm-up call), payload
+    GiB/s, bytes over the link, the link-bound time at the measured copy
+    rates (link_bound_ms) and frac_link = that bound / the measured time."""
+    import shutil
+    import numpy as np
+    import torch
+    from rustfs_amd import Erasure
+    from rustfs_amd import pipeline
+    from rustfs_amd.pipeline import _pinned
+    k, m = 8, 4
+    bs = 1 << 20
+    S, t, rec = bs // k, k + m, 32 + bs // k
+    out = {"workload": f"RS(8,4), 1 MiB blocks (S={S}), {n} blocks = {n * bs / GiB:.2f} GiB of payload, "
+                       f"host memory at both ends"}
+
+    def copy_gbs(nbytes):
+        h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+        h2 = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+        d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        d2 = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        s2 = torch.cuda.Stream(dev)
+        res = {}
+        for name, fn in (("h2d", lambda: d.copy_(h, non_blocking=True)),
+                         ("d2h", lambda: h.copy_(d, non_blocking=True))):
+            fn()
+            torch.cuda.synchronize()
+            best = None
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                fn()
+                torch.cuda.synchronize()
+                el = time.perf_counter() - t0
+                best = el if best is None else min(best, el)
+            res[name] = nbytes / best / 1e9
+        best = None
+        for _ in range(reps):  # both directions at once, one copy per stream
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            d.copy_(h, non_blocking=True)
+            with torch.cuda.stream(s2):
+                h2.copy_(d2, non_blocking=True)
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            best = el if best is None else min(best, el)
+        res["both"] = 2 * nbytes / best / 1e9
+        return res
+
+    link = copy_gbs(1 << 30)
+    out["pinned_copy_GB_s"] = {"h2d": round(link["h2d"], 2), "d2h": round(link["d2h"], 2),
+                               "h2d_plus_d2h_concurrent": round(link["both"], 2), "bytes_per_copy": 1 << 30}
+    plan = {name: (bi, bo, pay) for name, bi, bo, pay in host_path_plan(k, m, S, n)}
+
+    def entry(name, ms, extra=None):
+        bi, bo, pay = plan[name]
+        bound = link_bound_ms(bi, bo, link["h2d"], link["d2h"])
+        r = {"ms": round(ms, 3), "GiB_s_payload": round(pay / (ms * 1e-3) / GiB, 2),
+             "link_bytes_in": bi, "link_bytes_out": bo, "link_bound_ms": round(bound, 3),
+             "frac_link": round(bound / ms, 4)}
+        if extra:
+            r.update(extra)
+        out[name] = r
+
+    e = Erasure(k, m, bs, device=dev.index)
+    st = _pinned((n, t, S))
+    g = torch.Generator(device=dev).manual_seed(77)
+    for s0 in range(0, n, 256):  # random data made on the device, copied into the page-locked stripes
+        s1 = min(n, s0 + 256)
+        torch.from_numpy(st[s0:s1, :k]).copy_(
+            torch.randint(0, 256, (s1 - s0, k, S), dtype=torch.uint8, device=dev, generator=g))
+    dg = _pinned((n, t, 32))
+
+    def best_ms(fn):
+        fn()  # warm-up: staging allocation, clock ramp
+        b = None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            el = (time.perf_counter() - t0) * 1e3
+            b = el if b is None else min(b, el)
+        return b
+
+    entry("encode_batch_host", best_ms(lambda: e.encode_batch_host(st)))
+    entry("encode_batch_host_hh256s", best_ms(lambda: e.encode_batch_host(st, dg)))
+    # the records of the encoded object, checked against the device path once
+    chk = torch.from_numpy(st[:4].copy()).to(dev)
+    cd = torch.empty((4, t, 32), dtype=torch.uint8, device=dev)
+    e.encode_batch(chk, cd)
+    torch.cuda.synchronize()
+    assert torch.equal(chk.cpu(), torch.from_numpy(st[:4])) and torch.equal(cd.cpu(), torch.from_numpy(dg[:4]))
+    del chk, cd
+
+    need = int(n * bs * (1 + 2 * t / k) * 1.1)  # body + GET files + PUT files
+    root = None
+    try:
+        sv = os.statvfs("/dev/shm")
+        if sv.f_bavail * sv.f_frsize > need + (2 << 30):
+            root = os.path.join("/dev/shm", f"rsg_bench_{os.getpid()}")
+    except OSError:
+        pass
+    if root is None:
+        out["streams"] = "skipped: /dev/shm lacks room for the shard files (tmpfs keeps the figures the host pipeline's)"
+        return out
+    os.makedirs(root)
+    try:
+        paths = [os.path.join(root, f"part.{i}") for i in range(t)]
+        for i in range(t):  # BitrotWriter records [HH256S][shard] per block (bitrot.rs:464-510)
+            recs = np.empty((n, rec), dtype=np.uint8)
+            recs[:, :32] = dg[:, i]
+            recs[:, 32:] = st[:, i]
+            with open(paths[i], "wb") as f:
+                f.write(recs.data)
+            del recs
+        size = n * bs
+        stage = pipeline.GetStage()
+
+        def get(lost):
+            fds = [None if i in lost else os.open(paths[i], os.O_RDONLY) for i in range(t)]
+            try:
+                got = 0
+                for chunk in pipeline.get_stream(e, fds, size, stage=stage):
+                    got += len(chunk)
+                assert got == size
+            finally:
+                for fd in fds:
+                    if fd is not None:
+                        os.close(fd)
+
+        for lost in ((), (0, 3)):  # untimed correctness pass: every block against the stripes
+            fds = [None if i in lost else os.open(paths[i], os.O_RDONLY) for i in range(t)]
+            try:
+                for b, chunk in enumerate(pipeline.get_stream(e, fds, size, stage=stage)):
+                    assert chunk == st[b, :k].tobytes(), f"get_stream block {b} (lost {lost})"
+            finally:
+                for fd in fds:
+                    if fd is not None:
+                        os.close(fd)
+        entry("get_stream_all_present", best_ms(lambda: get(())),
+              {"batch_blocks": pipeline.DEFAULT_BATCH_BLOCKS})
+        entry("get_stream_2_data_lost", best_ms(lambda: get((0, 3))),
+              {"batch_blocks": pipeline.DEFAULT_BATCH_BLOCKS})
+        stage.close()
+        body = os.path.join(root, "body")
+        with open(body, "wb") as f:  # the object: block b is stripe b's k data shards
+            f.write(np.ascontiguousarray(st[:, :k]).data)
+        wpaths = [os.path.join(root, f"put.{i}") for i in range(t)]
+        pstage = {}
+
+        def put():
+            fds = [os.open(p, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644) for p in wpaths]
+            try:
+                with open(body, "rb", buffering=0) as f:
+                    r = pipeline.put_stream(e, f, size, fds, stage=pstage.get("s"))
+                pstage["s"] = r["stage"]
+            finally:
+                for fd in fds:
+                    os.close(fd)
+
+        ms = best_ms(put)
+        for i in range(t):  # the PUT's shard files equal the records the GET read
+            with open(wpaths[i], "rb") as a_, open(paths[i], "rb") as b_:
+                assert a_.read() == b_.read(), f"put_stream shard file {i}"
+        entry("put_stream_hh256s", ms, {"batch_blocks": pipeline.DEFAULT_BATCH_BLOCKS,
+                                        "inflight_batches": pipeline.DEFAULT_INFLIGHT_BATCHES})
+        out["files"] = "shard files and object body in tmpfs (/dev/shm): the host pipeline's rate, not a disk's"
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+    return out
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     a = parse(argv)
@@ -718,6 +931,8 @@ def main(argv=None):
             extras["rs12_4"] = rs12_4_extras(a, dev, stream)
         if not a.no_config_extras:
             extras.update(config_extras(a, e, stripes, k, m, dev, stream, rank, world))
+        if not a.no_host_path and world == 1:
+            extras["host_path"] = host_path_extras(dev, stream, a.host_path_blocks)
 
     traffic = pmc_traffic(k, m, S, n, a.digests)
 

@@ -46,11 +46,11 @@ typedef enum rsg_status {
     RSG_ERR_ZERO_DATA_SHARDS = 2,      /* ErasureConstructionError::ZeroDataShards, erasure.rs:90 */
     RSG_ERR_ZERO_PARITY_SHARDS = 3,    /* reed_solomon_erasure::Error::TooFewParityShards */
     RSG_ERR_TOO_MANY_SHARDS = 4,       /* UnsupportedModernShardCount, erasure.rs:102 */
-    RSG_ERR_INVALID_SHARD_COUNT = 5,   /* "invalid shard count", erasure.rs:510 */
-    RSG_ERR_INCONSISTENT_LENGTH = 6,   /* "inconsistent shard length", erasure.rs:527 */
+    RSG_ERR_INVALID_SHARD_COUNT = 5,   /* "invalid shard count", erasure.rs:512 */
+    RSG_ERR_INCONSISTENT_LENGTH = 6,   /* "inconsistent shard length", erasure.rs:536 */
     RSG_ERR_EMPTY_SHARD = 7,           /* reed_solomon_erasure::Error::EmptyShard */
     RSG_ERR_TOO_FEW_SHARDS = 8,        /* Error::TooFewShardsPresent -> "Reed-Solomon reconstruct failed" */
-    RSG_ERR_NO_VALID_SHARDS = 9,       /* "No valid shards found", erasure.rs:519 */
+    RSG_ERR_NO_VALID_SHARDS = 9,       /* "No valid shards found", erasure.rs:521 */
     RSG_ERR_INCONSISTENT_SOURCES = 10, /* InvalidData "inconsistent read source shards", bridge.rs:231 */
     RSG_ERR_BITROT_MISMATCH = 11,      /* InvalidData "bitrot hash mismatch", bitrot.rs:241 */
     RSG_ERR_NO_DEVICE = 12,            /* no HIP device / bad ordinal */

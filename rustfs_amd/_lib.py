@@ -189,9 +189,13 @@ class tuned:
         self.saved = {}
 
     def __enter__(self):
-        for k, v in self.knobs.items():
-            self.saved[k] = get_tuning(k)
-            set_tuning(k, v)
+        try:
+            for k, v in self.knobs.items():
+                self.saved[k] = get_tuning(k)
+                set_tuning(k, v)
+        except Exception:  # a bad name or value: undo the knobs already set, then raise
+            self.__exit__()
+            raise
         return self
 
     def __exit__(self, *exc):

@@ -306,8 +306,9 @@ hipError_t RSG_NET_NAME(launch_encode_hash_net, )(GfApplyParams p, HashParams h,
         return hipErrorInvalidValue;
     p.n_store = 4;
     p.copy_mask = 0;
-    p.cached_stores = tuning().get_cached ? 1u : 0u;
-    p.wave_prio = (uint32_t)tuning().get_prio;
+    const Tuning& t = tuning();  // one snapshot for the whole launch
+    p.cached_stores = t.get_cached ? 1u : 0u;
+    p.wave_prio = (uint32_t)t.get_prio;
     p.units = (uint32_t)((shard_len + dma::CH - 1) / dma::CH);
     p.byte_end = shard_len;
     h.len = shard_len;

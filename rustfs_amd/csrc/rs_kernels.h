@@ -96,7 +96,11 @@ struct HashParams {
     uint8_t* out;            // digests (may be null in verify mode)
     uint64_t out_stride;     // bytes between digests j and j+1 (0 = 32: packed)
     // verify mode (expect != null): compare with the stored digest of message j
-    // at expect + j*expect_stride and clear flags[j] on mismatch
+    // at expect + j*expect_stride and clear flags[j] on mismatch.  Callers set
+    // every flag to 1 first: a multi-file verify that launch_hh256 hands to the
+    // DMA-ring walk (launch_verify_records_dma, rs_verify.hip) writes each
+    // flag whole (1 verified, 0 not), so a flag pre-cleared by the caller is
+    // not kept
     const uint8_t* expect;
     uint64_t expect_stride;
     uint8_t* flags;

@@ -1265,9 +1265,29 @@ std::deque<Tuning>& tuning_store() {
     return d;
 }
 
+bool same_tuning(const Tuning& a, const Tuning& b) {
+    // every Tuning field (rs_kernels.h): a new knob must be added here too
+    return a.fused == b.fused && a.lost_disk_fast == b.lost_disk_fast && a.zero_copy == b.zero_copy &&
+           a.vec_block == b.vec_block && a.vec_occ == b.vec_occ && a.rolled == b.rolled &&
+           a.hash_direct_copy == b.hash_direct_copy && a.hash_depth == b.hash_depth &&
+           a.fused_kind == b.fused_kind && a.fused_spw1 == b.fused_spw1 && a.enc_prio == b.enc_prio &&
+           a.dma_ew == b.dma_ew && a.dma_nt == b.dma_nt && a.dma_spw == b.dma_spw && a.get_prio == b.get_prio &&
+           a.decode_net == b.decode_net && a.net12_rd == b.net12_rd && a.hash_unal == b.hash_unal &&
+           a.get_cached == b.get_cached;
+}
+
+// Snapshots are immutable and never freed (a launch on another thread may
+// still be reading the one it took), so an equal snapshot already published is
+// reused: the store holds at most one per distinct setting, however many
+// rsg_set_tuning calls a long A/B or test process makes.
 const Tuning* publish(const Tuning& v) {  // under g_tuning_mu
-    tuning_store().push_back(v);
-    const Tuning* t = &tuning_store().back();
+    const Tuning* t = nullptr;
+    for (const Tuning& s : tuning_store())
+        if (same_tuning(s, v)) t = &s;
+    if (!t) {
+        tuning_store().push_back(v);
+        t = &tuning_store().back();
+    }
     g_tuning.store(t, std::memory_order_release);
     return t;
 }
@@ -1337,8 +1357,8 @@ static GfKernel pick_vec_r(int R) {
 // Unrolled kernel for C <= 8 inputs and R <= 4 outputs, the rolled one above
 // (k_gf_apply_loop); RSG_ROLLED=1 forces the rolled kernel for A/B runs.
 template <int B, bool PRE>
-static GfKernel pick_vec_b(int C, int R) {
-    if (C <= 8 && R <= 4 && !tuning().rolled) {
+static GfKernel pick_vec_b(const Tuning& t, int C, int R) {
+    if (C <= 8 && R <= 4 && !t.rolled) {
         switch (C) {
             case 1: return pick_vec_r<1, B, PRE>(R);
             case 2: return pick_vec_r<2, B, PRE>(R);
@@ -1352,7 +1372,7 @@ static GfKernel pick_vec_b(int C, int R) {
         return nullptr;
     }
     if (C < 1 || C > kMaxC) return nullptr;
-    if (C > 8 && C <= 12 && R <= 4 && !tuning().rolled) {
+    if (C > 8 && C <= 12 && R <= 4 && !t.rolled) {
         switch (R) {
             case 1: return k_gf_apply_loop<1, B, PRE, 12>;
             case 2: return k_gf_apply_loop<2, B, PRE, 12>;
@@ -1382,8 +1402,8 @@ static GfKernel pick_vec_b(int C, int R) {
 // per KiB for one wave, 33 per 4 KiB for four (RS(12,4) at 1 MiB blocks, S =
 // 87382: encode 1.274 -> 1.112 ms, 0.562 -> 0.644 of HBM,
 // profiles/r04/c/enc12_ab.txt).  Tuning::vec_block forces one for A/B runs.
-static int vec_block_for(const GfApplyParams& p) {
-    if (tuning().vec_block) return tuning().vec_block;
+static int vec_block_for(const Tuning& t, const GfApplyParams& p) {
+    if (t.vec_block) return t.vec_block;
     bool lines = (uintptr_t)p.base % 128 == 0 && (uintptr_t)p.out_base % 128 == 0 && p.stripe_stride % 128 == 0 &&
                  p.out_stripe_stride % 128 == 0;
     for (uint32_t c = 0; c < p.C && lines; ++c) lines = p.in_off[c] % 128 == 0;
@@ -1398,14 +1418,14 @@ static int vec_block_for(const GfApplyParams& p) {
 // inputs, where fewer waves in flight stream better (RS(8,4) n = 4096: 1 lost
 // 0.846 -> 0.814 ms, 2 lost 0.905 -> 0.888 ms; profiles/r02/ab_occ2/), else
 // no cap.  RSG_VEC_OCC forces one value for A/B runs (tools/ab_occ.sh).
-static int vec_occupancy(int C, int R, bool pre) {
-    if (tuning().vec_occ >= 0) return tuning().vec_occ;
+static int vec_occupancy(const Tuning& t, int C, int R, bool pre) {
+    if (t.vec_occ >= 0) return t.vec_occ;
     return (!pre && C == 8 && R <= 2) ? 2 : 0;
 }
 
-static GfKernel pick_vec(int C, int R, bool pre, int B) {
-    if (B == 256) return pre ? pick_vec_b<256, true>(C, R) : pick_vec_b<256, false>(C, R);
-    return pre ? pick_vec_b<64, true>(C, R) : pick_vec_b<64, false>(C, R);
+static GfKernel pick_vec(const Tuning& t, int C, int R, bool pre, int B) {
+    if (B == 256) return pre ? pick_vec_b<256, true>(t, C, R) : pick_vec_b<256, false>(t, C, R);
+    return pre ? pick_vec_b<64, true>(t, C, R) : pick_vec_b<64, false>(t, C, R);
 }
 
 static GfKernel pick_byte(int R) {
@@ -1423,14 +1443,15 @@ static GfKernel pick_byte(int R) {
 }
 
 hipError_t launch_gf_apply_vec(GfApplyParams p, uint64_t n_stripes, hipStream_t stream) {
+    const Tuning& t = tuning();  // one snapshot for the whole launch (rsg_set_tuning may publish another)
     const bool pre = p.mode != GF_MODE_STORE || p.copy_mask != 0;
-    const uint32_t B = (uint32_t)vec_block_for(p);
-    GfKernel k = pick_vec((int)p.C, (int)p.R, pre, (int)B);
+    const uint32_t B = (uint32_t)vec_block_for(t, p);
+    GfKernel k = pick_vec(t, (int)p.C, (int)p.R, pre, (int)B);
     if (!k || p.units == 0 || n_stripes == 0) return hipErrorInvalidValue;
     p.chunks_per_stripe = (p.units + B - 1) / B;
     const uint64_t blocks = (uint64_t)p.chunks_per_stripe * n_stripes;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    const int occ = vec_occupancy((int)p.C, (int)p.R, pre);
+    const int occ = vec_occupancy(t, (int)p.C, (int)p.R, pre);
     const size_t lds = occ ? (size_t)(160 * 1024) / (size_t)(4 * occ * (B / 64)) / 16 * 16 : 0;
     hipLaunchKernelGGL(k, dim3((uint32_t)blocks), dim3(B), lds, stream, p);
     return hipGetLastError();
@@ -1475,8 +1496,9 @@ hipError_t launch_hh256(const HashParams& p, hipStream_t stream) {
     // copy mode: staged 16-byte stores (COPY = 2) by default (Tuning:
     // direct 8-byte stores for A/B runs); 8-packet batches in flight per
     // lane: 2 by default
-    const bool direct_copy = tuning().hash_direct_copy;
-    const int depth = tuning().hash_depth;
+    const Tuning& t = tuning();  // one snapshot for the whole launch
+    const bool direct_copy = t.hash_direct_copy;
+    const int depth = t.hash_depth;
     using HashKernel = void (*)(const HashParams);
     HashKernel k;
     // messages at odd offsets (record pitch 174795 of RS(6,4) at 1 MiB
@@ -1491,7 +1513,7 @@ hipError_t launch_hh256(const HashParams& p, hipStream_t stream) {
     } else {
         even = (uintptr_t)p.data % 2 == 0 && p.stripe_stride % 2 == 0 && p.shard_pitch % 2 == 0;
     }
-    if (!copy && depth == 2 && !even && tuning().hash_unal) k = k_hh256_quad<0, 2, true>;
+    if (!copy && depth == 2 && !even && t.hash_unal) k = k_hh256_quad<0, 2, true>;
     else if (!copy) k = depth == 1 ? k_hh256_quad<0, 1> : depth == 2 ? k_hh256_quad<0, 2> : k_hh256_quad<0, 3>;
     else if (direct_copy) k = depth == 1 ? k_hh256_quad<1, 1> : depth == 2 ? k_hh256_quad<1, 2> : k_hh256_quad<1, 3>;
     else k = depth == 1 ? k_hh256_quad<2, 1> : depth == 2 ? k_hh256_quad<2, 2> : k_hh256_quad<2, 3>;
@@ -1671,8 +1693,9 @@ static hipError_t launch_encode_hash_dma(GfApplyParams p, HashParams h, uint64_t
     // 1.28 ms at n = 4096 (profiles/r02/ab_nt/); dma_spw = 4: four stripes
     // per workgroup, two workgroups per CU — measured slower (n = 4096: 1.39
     // vs 1.25 ms; profiles/r02/ab_spw/)
-    const int ew = tuning().dma_ew, nt = tuning().dma_nt, spw = tuning().dma_spw;
-    p.wave_prio = (uint32_t)tuning().enc_prio;
+    const Tuning& t = tuning();  // one snapshot for the whole launch
+    const int ew = t.dma_ew, nt = t.dma_nt, spw = t.dma_spw;
+    p.wave_prio = (uint32_t)t.enc_prio;
     p.units = (uint32_t)(shard_len / dma::CH);
     h.n = n_stripes;
     const uint64_t blocks = (n_stripes + dma::SPW - 1) / dma::SPW;
@@ -1724,12 +1747,13 @@ hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shar
     // Packed workgroups measured as fast or faster than one stripe per
     // workgroup at every batch size tried (n = 256..65536; tools/sweep_small_batch.sh);
     // Tuning::fused_spw1 selects the unpacked variant for A/B runs.
-    const bool unpacked = tuning().fused_spw1;
+    const Tuning& t = tuning();  // one snapshot for the whole launch
+    const bool unpacked = t.fused_spw1;
     // Few stripes (below ~8 per CU): the ring kernel (one stripe per
     // workgroup, E KiB chunks, next chunk in flight) beats the packed one
     // 1.1-3.2x (tools/kbench/ring_variants.hip);
     // Tuning::fused_kind (packed|ring|dma) forces one for A/B runs.
-    const int kind = tuning().fused_kind;
+    const int kind = t.fused_kind;
     if (kind >= 4 && kind <= 7 && wide_supported(p, shard_len, n_stripes))
         return launch_encode_hash_wide(p, h, shard_len, n_stripes, (kind == 5 || kind == 7) ? 4 : 2, kind >= 6,
                                        stream);

@@ -2,14 +2,15 @@
 heal kernels: the compile-time XOR-network kernels (k_decode_records_net for
 RS(8,4), one kernel per pattern, rs84_decode_nets.h; RS(4,4), RS(6,4),
 RS(10,4), RS(12,4) likewise — the patterns read from the generated tables)
-and the run-time-table kernel k_decode_records_dma for every other k <= 16
-(RS(16,4), and the odd data counts of 5-, 9-, 15-drive sets and the reduced-
-redundancy class: RS(5,4), RS(11,4), RS(15,1), ...; the patterns generated
-here): GET (a data shard lost) and heal (every lost shard a target), on
+and the run-time-table kernel k_decode_records_dma for every other geometry
+of at most 16 shards (the odd data counts of 5-, 9-, 15-drive sets and the
+reduced-redundancy class: RS(5,4), RS(11,4), RS(15,1), ...; the patterns
+generated here).  RS(16,4) (20 shards, more than rustfs stores,
+fileinfo.rs:38) has no one-pass kernel: its GET and heal run the two-pass
+path, forced or not, and are checked here as that path): GET (a data shard lost) and heal (every lost shard a target), on
 oracle-built BitrotWriter records, over a ragged batch (RS(8,4): 19 stripes
 = two full 8-stripe workgroups and a partial one, so every 4-stripe network
-group meets live and dead stripes; RS(16,4): 11 stripes = two full 4-stripe
-workgroups and a partial one), bit-exact against the oracle's shards and
+group meets live and dead stripes; RS(16,4): 11 stripes), bit-exact against the oracle's shards and
 digests; then the same pattern with one
 surplus parity record of one stripe altered and re-hashed must report
 "inconsistent sources" for that stripe only (erasure.rs:935-973,
@@ -149,9 +150,9 @@ def _every_pattern(k, m):
 
 
 # ---------------------------------------------------------------- RS(16,4)
-# no networks since round 5 (rustfs cannot store 20 shards, fileinfo.rs:38):
-# GET on the table kernel, heal on the two-pass path (or the table kernel
-# with the one-pass engine forced, as here)
+# no one-pass kernel since round 5 (rustfs cannot store 20 shards,
+# fileinfo.rs:38; one_pass_geometry requires k + m <= 16): GET and heal run
+# the two-pass path whatever the record-engine setting
 K16, T16, N16 = 16, 20, 11
 LISTED16 = _every_pattern(16, 4)
 
@@ -488,8 +489,9 @@ def test_table_kernel_every_pattern(gpu, oracle, table_records, one_pass, k, m, 
 
 
 def test_rs16_heal_three_lost(gpu, oracle, records16, one_pass):
-    """A heal of three lost shards (the table kernel's widest target set at
-    RS(16,4) with the one-pass engine forced): bit-exact."""
+    """A heal of three lost shards at RS(16,4) (the two-pass path: no
+    one-pass kernel covers 20 shards, even with the one-pass engine forced):
+    bit-exact."""
     import torch
     from rustfs_amd import Erasure
     shards, recs, files = records16

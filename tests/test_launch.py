@@ -230,3 +230,28 @@ def test_engine_plan_rs12_4():
     assert bench.ENGINE_REPS >= 20 and bench.ENGINE_WARM_S >= 0.5
     a = bench.parse([])
     assert a.rs12_batch == 4096 and not a.no_rs12
+
+
+def test_host_path_plan():
+    """extras.host_path (north_star: the rate including pinned hipMemcpyAsync
+    to and from the GPU): RS(8,4), 1 MiB blocks, 1024 blocks per call on the
+    default line; the bytes each entry moves over the link and its link bound
+    at the measured copy rates (both directions overlapped)."""
+    k, m, S, n = 8, 4, 131072, 1024
+    t, rec = k + m, 32 + S
+    plan = {name: (bi, bo, pay) for name, bi, bo, pay in bench.host_path_plan(k, m, S, n)}
+    pay = n * k * S
+    assert pay == 1 << 30
+    assert plan == {
+        "encode_batch_host": (pay, n * m * S, pay),
+        "encode_batch_host_hh256s": (pay, n * m * S + n * t * 32, pay),
+        # every present record in, only the rebuilt data shards out
+        "get_stream_all_present": (n * t * rec, 0, pay),
+        "get_stream_2_data_lost": (n * (t - 2) * rec, 2 * n * S, pay),
+        "put_stream_hh256s": (pay, n * m * S + n * t * 32, pay),
+    }
+    # the larger direction bounds a full-duplex transfer
+    assert bench.link_bound_ms(50e9, 10e9, 50.0, 50.0) == pytest.approx(1000.0)
+    assert bench.link_bound_ms(10e9, 50e9, 50.0, 25.0) == pytest.approx(2000.0)
+    a = bench.parse([])
+    assert a.host_path_blocks == 1024 and not a.no_host_path
