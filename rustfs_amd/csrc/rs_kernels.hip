@@ -1184,15 +1184,15 @@ bool set_knob(Tuning& v, const std::string& name, const char* value) {
         f = (int)x;
         return true;
     };
-    auto one_of = [&](int& f, int a, int b, int c = -1000) {
-        if (!is_num || (x != a && x != b && x != c)) return false;
+    auto one_of = [&](int& f, int a, int b, int c = -1000, int d = -1000, int e = -1000) {
+        if (!is_num || (x != a && x != b && x != c && x != d && x != e)) return false;
         f = (int)x;
         return true;
     };
     if (name == "RSG_FUSED") return flag(v.fused);
     if (name == "RSG_LOST_DISK_FAST") return flag(v.lost_disk_fast);
     if (name == "RSG_ZERO_COPY") return flag(v.zero_copy);
-    if (name == "RSG_VEC_BLOCK") return one_of(v.vec_block, 0, 64, 256);
+    if (name == "RSG_VEC_BLOCK") return one_of(v.vec_block, 0, 64, 256, 512, 1024);
     if (name == "RSG_VEC_OCC") return num(v.vec_occ, -1, 8);
     if (name == "RSG_ROLLED") return flag(v.rolled);
     if (name == "RSG_HASH_COPY") return flag(v.hash_direct_copy);
@@ -1423,7 +1423,23 @@ static int vec_occupancy(const Tuning& t, int C, int R, bool pre) {
     return (!pre && C == 8 && R <= 2) ? 2 : 0;
 }
 
+// Eight- and sixteen-wave workgroups for the rolled kernel (C > 8): a ragged
+// row's chunk boundaries fall mid-line, and each boundary line is fetched by
+// both neighbouring workgroups (A/B: Tuning::vec_block = 512 / 1024).
+template <int B, bool PRE>
+static GfKernel pick_loop_big(int C, int R) {
+    if (C > 8 && C <= 12 && R == 4) return k_gf_apply_loop<4, B, PRE, 12>;
+    if (C > 12 && R == 4) return k_gf_apply_loop<4, B, PRE>;
+    return nullptr;
+}
+
 static GfKernel pick_vec(const Tuning& t, int C, int R, bool pre, int B) {
+    if (B == 512 || B == 1024) {
+        GfKernel k = B == 512 ? (pre ? pick_loop_big<512, true>(C, R) : pick_loop_big<512, false>(C, R))
+                              : (pre ? pick_loop_big<1024, true>(C, R) : pick_loop_big<1024, false>(C, R));
+        if (k && !t.rolled) return k;
+        B = 256;
+    }
     if (B == 256) return pre ? pick_vec_b<256, true>(t, C, R) : pick_vec_b<256, false>(t, C, R);
     return pre ? pick_vec_b<64, true>(t, C, R) : pick_vec_b<64, false>(t, C, R);
 }

@@ -265,12 +265,20 @@ def block_geometry(offset: int, length: int, block_size: int, block: int):
 
 def get_stream(erasure: Erasure, fds: List[Optional[int]], total_length: int, offset: int = 0,
                length: Optional[int] = None, algo: HashAlgorithm = HashAlgorithm.HighwayHash256S,
-               batch_blocks: int = DEFAULT_BATCH_BLOCKS, stage: Optional[GetStage] = None) -> Iterator[bytes]:
+               batch_blocks: int = DEFAULT_BATCH_BLOCKS, stage: Optional[GetStage] = None,
+               views: bool = False) -> Iterator:
     """Yield bytes [offset, offset + length) of an object whose shard files
     are open at `fds` (None: disk unavailable), verifying every record
     before use and rebuilding missing data on the GPU.  Range errors follow
     decode_inner (decode.rs:1716-1742).  `stage`: reusable buffers
-    (GetStage), else allocated for this call."""
+    (GetStage), else allocated for this call.
+
+    views=True: each block's window as a list of memoryviews of the shard
+    buffers it lies in (the verified record bodies in the page-locked read
+    stage, the rebuilt shards in their page-locked slots), in order, without
+    joining them — write_data_blocks' form, which writes straight from the
+    per-shard buffers (decode.rs:1390); a writev-ready iovec.  The views stay
+    valid until the next block is requested (the stages are reused)."""
     if length is None:
         length = total_length - offset
     if offset < 0 or length < 0 or offset + length > total_length:
@@ -288,7 +296,7 @@ def get_stream(erasure: Erasure, fds: List[Optional[int]], total_length: int, of
     start, end = offset // bs, (offset + length - 1) // bs
     full_end = min(end, nfull - 1)  # last full block in the range
     if start <= full_end:
-        yield from _get_full(erasure, fds, start, full_end, offset, length, algo, batch_blocks, stage)
+        yield from _get_full(erasure, fds, start, full_end, offset, length, algo, batch_blocks, stage, views)
     if end >= nfull:  # the short last block: host path, verify-before-use
         tl = total_length - nfull * bs
         s_blk = calc_shard_size(tl, k)
@@ -304,7 +312,7 @@ def get_stream(erasure: Erasure, fds: List[Optional[int]], total_length: int, of
         erasure.decode_data_with_reconstruction_verification(shards)
         blk = b"".join(bytes(shards[i]) for i in range(k))[:tl]
         o, n = block_geometry(offset, length, bs, nfull)
-        yield blk[o:o + n]
+        yield [memoryview(blk)[o:o + n]] if views else blk[o:o + n]
 
 
 class GetStage:
@@ -327,7 +335,11 @@ class GetStage:
         key = (t, k, S, bs, str(dev))
         if self.key != key or self.cnt < cnt_max:
             self.stage = [[_pinned(cnt_max * rec) for _ in range(t)] for _ in range(2)]
-            self.files_dev = [torch.empty(cnt_max * rec, dtype=torch.uint8, device=dev) for _ in range(t)]
+            # two sets: batch j+1's records go up while batch j is decoded
+            self.files_dev = [[torch.empty(cnt_max * rec, dtype=torch.uint8, device=dev) for _ in range(t)]
+                              for _ in range(2)]
+            self.copy_stream = torch.cuda.Stream(dev)
+            self.landed = [torch.cuda.Event(), torch.cuda.Event()]
             self.slots = [torch.empty(cnt_max * S, dtype=torch.uint8, device=dev) for _ in range(k)]
             self.host_slots = [_pinned(cnt_max * S) for _ in range(k)]
             self.key, self.cnt = key, cnt_max
@@ -340,7 +352,7 @@ class GetStage:
             self.pool = None
 
 
-def _get_full(erasure, fds, start, full_end, offset, length, algo, batch_blocks, reuse=None):
+def _get_full(erasure, fds, start, full_end, offset, length, algo, batch_blocks, reuse=None, views=False):
     """Full blocks start..full_end: B-block batches, read-ahead of batch i+1
     into the other page-locked stage while batch i is decoded on the GPU."""
     import torch
@@ -355,14 +367,14 @@ def _get_full(erasure, fds, start, full_end, offset, length, algo, batch_blocks,
         gs.lock.acquire()
     try:
         gs.ensure(t, k, S, bs, cnt_max, dev)
-        yield from _get_batches(erasure, fds, start, full_end, offset, length, algo, cnt_max, gs)
+        yield from _get_batches(erasure, fds, start, full_end, offset, length, algo, cnt_max, gs, views)
     finally:
         gs.lock.release()
         if own:
             gs.close()
 
 
-def _get_batches(erasure, fds, start, full_end, offset, length, algo, cnt_max, gs):
+def _get_batches(erasure, fds, start, full_end, offset, length, algo, cnt_max, gs, views=False):
     """The in-place GET (reconstruct_into's contract, bridge.rs:274-307; the
     blocks written straight from the per-shard buffers, decode.rs:1390): the
     records are verified on the device, only the shards no verified record
@@ -378,7 +390,11 @@ def _get_batches(erasure, fds, start, full_end, offset, length, algo, cnt_max, g
     batches = [(b0, min(cnt_max, full_end + 1 - b0)) for b0 in range(start, full_end + 1, cnt_max)]
     got: dict = {}
 
-    def fetch(j):  # one pread per shard file per batch, files in parallel; a failed read = shard missing
+    def fetch(j):
+        """Batch j: one pread per shard file, files in parallel (a failed read
+        = shard missing), then its records' H2D on the stage's copy stream
+        into device set j & 1 (event landed[j & 1]) — so the copy of batch
+        j+1 overlaps the decode of batch j."""
         b0, cnt = batches[j]
 
         def one(i):
@@ -389,7 +405,14 @@ def _get_batches(erasure, fds, start, full_end, offset, length, algo, cnt_max, g
             except OSError:
                 return False
 
-        got[j] = list(pool.map(one, range(t)))
+        ok = list(pool.map(one, range(t)))
+        with torch.cuda.stream(gs.copy_stream):
+            for i in range(t):
+                if ok[i]:
+                    files_dev[j & 1][i][: cnt * rec].copy_(torch.from_numpy(stage[j & 1][i][: cnt * rec]),
+                                                           non_blocking=True)
+            gs.landed[j & 1].record(gs.copy_stream)
+        got[j] = ok
 
     th = threading.Thread(target=fetch, args=(0,))
     th.start()
@@ -398,19 +421,16 @@ def _get_batches(erasure, fds, start, full_end, offset, length, algo, cnt_max, g
         for j, (b0, cnt) in enumerate(batches):
             th.join()
             ok = got.pop(j)
-            for i in range(t):  # H2D of this batch's records (page-locked -> device)
-                if ok[i]:
-                    files_dev[i][: cnt * rec].copy_(torch.from_numpy(stage[j & 1][i][: cnt * rec]),
-                                                    non_blocking=True)
             if sum(ok) < k:
                 raise _lib.RsgError(_lib.RSG_ERR_TOO_FEW_SHARDS, "read quorum lost")
-            # batch j+1 goes into the other stage, free since batch j-1's
-            # blocks were yielded (each yield is a copy)
+            s.wait_event(gs.landed[j & 1])
+            # batch j+1 goes into the other stage and device set, free since
+            # batch j-1 was decoded and its blocks yielded
             if j + 1 < len(batches):
                 th = threading.Thread(target=fetch, args=(j + 1,))
                 th.start()
             _, src, status = erasure.decode_records_into_batch(
-                [files_dev[i][: cnt * rec] if ok[i] else None for i in range(t)], S, cnt, targets=slots,
+                [files_dev[j & 1][i][: cnt * rec] if ok[i] else None for i in range(t)], S, cnt, targets=slots,
                 target_stride=S, algo=algo.value, stream=s)
             bad = [x for x in status if x != _lib.RSG_OK]
             if bad:
@@ -431,6 +451,6 @@ def _get_batches(erasure, fds, start, full_end, offset, length, algo, cnt_max, g
                     else:
                         parts.append(host_slots[i][b * S + off: b * S + off + take])
                     pos += take
-                yield b"".join(parts)
+                yield [memoryview(x) for x in parts] if views else b"".join(parts)
     finally:
         th.join()

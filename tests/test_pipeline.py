@@ -136,6 +136,33 @@ def test_range_get(gpu, tmp_path, k, m, lost):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lost", [(), (0, 3), (4,)])
+def test_range_get_views(gpu, tmp_path, lost):
+    """get_stream(views=True): each block's window as memoryviews of the
+    record stage and the rebuilt slots (write_data_blocks' form), the same
+    bytes as the joined form, over batches whose device sets alternate
+    (records of batch j+1 copied while batch j is decoded)."""
+    from rustfs_amd.pipeline import get_stream
+    k, m = 4, 2
+    size = 9 * BS + 777
+    es, dirs = _set(tmp_path, k, m)
+    data = np.random.default_rng(9).integers(0, 256, size, dtype=np.uint8).tobytes()
+    es.put_object_stream("b/o", io.BytesIO(data), size, batch_blocks=4)
+    fds = [None if i in lost else os.open(es.part_file(i, "b/o"), os.O_RDONLY) for i in range(k + m)]
+    try:
+        for off, ln in _ranges(size, BS):
+            got = []
+            for blk in get_stream(es.erasure, fds, size, off, ln, batch_blocks=2, views=True):
+                assert all(isinstance(v, memoryview) for v in blk)
+                got.append(b"".join(blk))  # valid until the next block is requested
+            assert b"".join(got) == data[off:off + ln], (off, ln)
+    finally:
+        for fd in fds:
+            if fd is not None:
+                os.close(fd)
+
+
+@pytest.mark.gpu
 def test_range_get_drops_corrupted_records(gpu, tmp_path):
     from rustfs_amd import RsgError
     size = 6 * BS + 100

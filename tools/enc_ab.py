@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--digests", action="store_true")
+    ap.add_argument("--block", type=int, default=1 << 20, help="block bytes (S = ceil(block / k))")
     ap.add_argument("--variant", action="append", default=[],
                     help="name=KNOB:VALUE[,KNOB:VALUE] (empty after = : the defaults)")
     a = ap.parse_args()
@@ -38,8 +39,8 @@ def main():
     for g in a.geoms:
         k, m = map(int, g.split(","))
         t, n = k + m, a.n
-        S = -(-(1 << 20) // k)
-        e = Erasure(k, m, 1 << 20)
+        S = -(-a.block // k)
+        e = Erasure(k, m, a.block)
         st = bench.random_stripes(dev, k, m, S, n, 11 + k)
         dig = torch.empty((n, t, 32), dtype=torch.uint8, device=dev) if a.digests else None
         ref = None
