@@ -629,6 +629,7 @@ def host_path_plan(k, m, S, n):
             ("get_stream_all_present", n * t * rec, 0, n * k * S),
             ("get_stream_2_data_lost", n * (t - 2) * rec, n * 2 * S, n * k * S),
             ("get_stream_bytes_all_present", n * t * rec, 0, n * k * S),
+            ("get_stream_data_shards_only_all_present", n * k * rec, 0, n * k * S),
             ("put_stream_hh256s", n * k * S, n * m * S + n * t * 32, n * k * S)]
 
 
@@ -761,11 +762,11 @@ def host_path_extras(dev, stream, n=1024, reps=5):
         size = n * bs
         stage = pipeline.GetStage()
 
-        def get(lost, views=True):
+        def get(lost, views=True, data_only=False):
             fds = [None if i in lost else os.open(paths[i], os.O_RDONLY) for i in range(t)]
             try:
                 got = 0
-                for chunk in pipeline.get_stream(e, fds, size, stage=stage, views=views):
+                for chunk in pipeline.get_stream(e, fds, size, stage=stage, views=views, data_shards_only=data_only):
                     got += sum(len(v) for v in chunk) if views else len(chunk)
                 assert got == size
             finally:
@@ -789,6 +790,9 @@ def host_path_extras(dev, stream, n=1024, reps=5):
         entry("get_stream_2_data_lost", best_ms(lambda: get((0, 3))), form)
         entry("get_stream_bytes_all_present", best_ms(lambda: get((), views=False)),
               {"batch_blocks": pipeline.DEFAULT_BATCH_BLOCKS, "yields": "bytes: each block joined into one object"})
+        entry("get_stream_data_shards_only_all_present", best_ms(lambda: get((), data_only=True)),
+              dict(form, reads="the k data files only (RUSTFS_GET_LOCKSTEP_DATA_SHARDS_ONLY_ENABLE, "
+                                "decode.rs:125-143; off by default in the reference)"))
         stage.close()
         body = os.path.join(root, "body")
         with open(body, "wb") as f:  # the object: block b is stripe b's k data shards

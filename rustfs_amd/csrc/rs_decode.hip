@@ -257,8 +257,9 @@ using WideLaunch = int (*)(int m, int nf, int th, uint64_t n_stripes, const GfAp
 // to RM = 8 rows (missing data + surplus parity, or heal targets + surplus)
 // for every one- and two-loss pattern — GET with one or two files absent,
 // heal of one target (the other files present, or one more absent) or two —
-// in 4-stripe workgroups (the ring of up to 15 files would not fit 8).  Other
-// patterns take the two-pass path.
+// and (round 6) GET with three or four files absent and the heal of all three
+// or four lost shards, in 4-stripe workgroups (the ring of up to 15 files
+// would not fit 8).  Other patterns take the two-pass path.
 template <int C, int NF, int TH>
 static int launch_wide(uint64_t n_stripes, const GfApplyParams& p, const HashParams& h, bool any_table,
                        hipStream_t stream) {
@@ -282,6 +283,12 @@ static int launch_wide_m(int nf, int th, uint64_t n_stripes, const GfApplyParams
         if (th == 1 && nf == T - 1) return launch_wide<C, T - 1, 1>(n_stripes, p, h, any_table, stream);
         if (th == 1 && nf == T - 2) return launch_wide<C, T - 2, 1>(n_stripes, p, h, any_table, stream);
         if (th == 2 && nf == T - 2) return launch_wide<C, T - 2, 2>(n_stripes, p, h, any_table, stream);
+        // three and four files lost (round 6): the GET, and the heal of
+        // every lost shard — still at most m = 8 rows (missing + surplus)
+        if (th == 0 && nf == T - 3) return launch_wide<C, T - 3, 0>(n_stripes, p, h, any_table, stream);
+        if (th == 0 && nf == T - 4) return launch_wide<C, T - 4, 0>(n_stripes, p, h, any_table, stream);
+        if (th == 3 && nf == T - 3) return launch_wide<C, T - 3, 3>(n_stripes, p, h, any_table, stream);
+        if (th == 4 && nf == T - 4) return launch_wide<C, T - 4, 4>(n_stripes, p, h, any_table, stream);
         return kTabInvalid;
     }
 }
@@ -384,7 +391,7 @@ static int launch_get_any(int k, int m, int nf, int th, uint64_t n_stripes, cons
     if (m > 4) {
         static const WideLaunch wide[7] = {launch_get_wide_5, launch_get_wide_6,  launch_get_wide_7, launch_get_wide_8,
                                            launch_get_wide_9, launch_get_wide_10, launch_get_wide_11};
-        if (k < 5 || k > 11 || m > 8 || th < 0 || th > 2) return kTabInvalid;
+        if (k < 5 || k > 11 || m > 8 || th < 0 || th > 4) return kTabInvalid;
         return wide[k - 5](m, nf, th, n_stripes, p, h, any_table, stream);
     }
     static const TabLaunch parts[16] = {launch_get_tab_1,  launch_get_tab_2,  launch_get_tab_3,  launch_get_tab_4,
@@ -416,13 +423,13 @@ static bool wide_geometry(int k, int m, uint64_t shard_len) {
 static int rows_max(int m) { return m > 4 ? 8 : 4; }
 
 bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len) {
-    if (wide_geometry(k, m, shard_len)) return nf >= k + m - 2 && nf < k + m;
+    if (wide_geometry(k, m, shard_len)) return nf >= k + m - 4 && nf < k + m;
     return one_pass_geometry(k, m, shard_len) && nf >= k && nf < k + m;
 }
 
 bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len) {
     if (wide_geometry(k, m, shard_len))
-        return (targets == 1 && nf >= k + m - 2 && nf <= k + m - 1) || (targets == 2 && nf == k + m - 2);
+        return (targets == 1 && nf >= k + m - 2 && nf <= k + m - 1) || (targets >= 2 && targets <= 4 && nf == k + m - targets);
     return one_pass_geometry(k, m, shard_len) && nf >= k && targets >= 1 && nf + targets <= k + m;
 }
 
@@ -438,12 +445,14 @@ bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len) {
 // RS(11,4) (44) GET 1.50 vs 2.26 ms, RS(13,3) (39) GET 1.25 vs 1.86.
 bool table_one_pass_preferred(int k, int R, bool two_per_cu) { return two_per_cu || k * R <= 40; }
 
-// Patterns with a compile-time XOR network (RS(4,4), RS(6,4), RS(8,4):
+// Patterns with a compile-time XOR network (RS(6,4), RS(8,4):
 // rs_decode_net.hip; RS(10,4), RS(12,4): rs_decode_netq.hip): the launch's
 // coefficient rows are matched byte for byte against the generated table; a
 // listed pattern runs its network kernel, anything else the run-time-table
-// kernel above.  Tuning::decode_net = false (RSG_DECODE_NET=0)
-// keeps the table kernel for A/B runs.
+// kernel above (RS(4,4) too: its networks were 2-5 % faster than the table
+// kernel, profiles/r05/netab/, and were dropped in round 6 for build time).
+// Tuning::decode_net = false (RSG_DECODE_NET=0) keeps the table kernel for
+// A/B runs.
 static bool launch_net_if_listed(int heal, int k, int m, int nf, const uint8_t* coef, uint64_t n_stripes,
                                  const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
     if (m != 4 || !coef || !tuning().decode_net || p.C != (uint32_t)k) return false;
@@ -464,10 +473,9 @@ static bool launch_net_if_listed(int heal, int k, int m, int nf, const uint8_t* 
                                                     launch_records_net10_part6, launch_records_net10_part7};
         return (k == 12 ? parts12 : parts10)[pid % RSG_NET_PARTS](pid, blocks, p, h, stream);
     }
-    if (k != 8 && k != 6 && k != 4) return false;
-    const int pid = k == 8   ? records_net_pattern(heal, nf, (int)p.R, (int)p.n_store, coef)
-                    : k == 6 ? records_net6_pattern(heal, nf, (int)p.R, (int)p.n_store, coef)
-                             : records_net4_pattern(heal, nf, (int)p.R, (int)p.n_store, coef);
+    if (k != 8 && k != 6) return false;
+    const int pid = k == 8 ? records_net_pattern(heal, nf, (int)p.R, (int)p.n_store, coef)
+                           : records_net6_pattern(heal, nf, (int)p.R, (int)p.n_store, coef);
     if (pid < 0) return false;
     GfApplyParams q = p;
     q.cached_stores = tuning().get_cached ? 1u : 0u;
@@ -481,11 +489,7 @@ static bool launch_net_if_listed(int heal, int k, int m, int nf, const uint8_t* 
                                                launch_records_net6_part2, launch_records_net6_part3,
                                                launch_records_net6_part4, launch_records_net6_part5,
                                                launch_records_net6_part6, launch_records_net6_part7};
-    static const Part parts4[RSG_NET_PARTS] = {launch_records_net4_part0, launch_records_net4_part1,
-                                               launch_records_net4_part2, launch_records_net4_part3,
-                                               launch_records_net4_part4, launch_records_net4_part5,
-                                               launch_records_net4_part6, launch_records_net4_part7};
-    return (k == 8 ? parts : k == 6 ? parts6 : parts4)[pid % RSG_NET_PARTS](pid, blocks, q, h, stream);
+    return (k == 8 ? parts : parts6)[pid % RSG_NET_PARTS](pid, blocks, q, h, stream);
 }
 
 // The record files' layout the DMA ring can walk: LDS-DMA takes sources at

@@ -1,10 +1,9 @@
-// rs_decode_net.hip — the one-pass GET / heal kernel for RS(8,4), RS(6,4)
-// and RS(4,4) (the default geometries of 12-, 10- and 8-drive sets,
-// storageclass.rs:24-31) with its rows as a compile-time XOR network per
-// erasure pattern (k_decode_records_net<PID> / _net6 / _net4; the networks
-// in the generated rs84_decode_nets.h / rs64_decode_nets.h /
-// rs44_decode_nets.h, tools/gen_decode_nets.py [--k 6|4]).  Compiled
-// RSG_NET_PARTS times per geometry (Makefile: RSG_NET_K = 8, 6 or 4), part
+// rs_decode_net.hip — the one-pass GET / heal kernel for RS(8,4) and RS(6,4)
+// (the default geometries of 12- and 10-drive sets, storageclass.rs:24-31)
+// with its rows as a compile-time XOR network per erasure pattern
+// (k_decode_records_net<PID> / _net6; the networks in the generated
+// rs84_decode_nets.h / rs64_decode_nets.h, tools/gen_decode_nets.py [--k 6]).
+// Compiled RSG_NET_PARTS times per geometry (Makefile: RSG_NET_K = 8 or 6), part
 // RSG_NET_PART instantiating
 // the patterns with PID % RSG_NET_PARTS == RSG_NET_PART, so the kernels
 // build in parallel.
@@ -48,10 +47,8 @@
 #define RSG_NET_TAG  // k_decode_records_net, launch_records_net_partN, records_net_pattern
 #elif RSG_NET_K == 6
 #define RSG_NET_TAG 6  // k_decode_records_net6, launch_records_net6_partN, records_net6_pattern
-#elif RSG_NET_K == 4
-#define RSG_NET_TAG 4  // k_decode_records_net4, launch_records_net4_partN, records_net4_pattern
 #else
-#error "RSG_NET_K is 8, 6 or 4"
+#error "RSG_NET_K is 8 or 6"
 #endif
 #define RSG_NET_NAME(pre, post) RSG_NET_CAT(RSG_NET_CAT(pre, RSG_NET_TAG), post)
 
@@ -62,9 +59,6 @@ namespace rsg {
 #elif RSG_NET_K == 6
 #include "rs64_decode_nets.h"
 namespace decnet = decnet6;
-#else
-#include "rs44_decode_nets.h"
-namespace decnet = decnet4;
 #endif
 constexpr int kNetC = RSG_NET_K;  // survivors (data shards)
 
@@ -152,7 +146,7 @@ __device__ __forceinline__ void net_wave(const GfApplyParams& p, uint64_t n, uin
         }
         const bool part = s + 1 == steps && tail != CH;  // wave-uniform
         uint32_t O[32];
-#if RSG_NET_ABLATE  // experiment builds only (exp/, tools/ab_ablate.sh): no arithmetic, rows = survivors
+#if RSG_NET_ABLATE  // experiment builds only (round 3, profiles/KERNEL_NOTES.md): no arithmetic, rows = survivors
 #pragma unroll
         for (int i = 0; i < 32; ++i) O[i] = P[i];
 #else
@@ -277,7 +271,7 @@ bool RSG_NET_NAME(launch_records_net, RSG_NET_CAT(_part, RSG_NET_PART))(int pid,
 }
 
 #if RSG_NET_PART == 0
-// The fused encode + HH256S of RS(8,4) / RS(6,4) / RS(4,4) (BitrotWriter over
+// The fused encode + HH256S of RS(8,4) / RS(6,4) (BitrotWriter over
 // an encoded block, bitrot.rs:464-510 after erasure encode): the heal kernel
 // of all four parity shards (pattern kEncodePid, rows = the encode matrix)
 // walking the data shards of a stripe buffer in place, as

@@ -147,16 +147,13 @@ hipError_t launch_encode_hash_net10(GfApplyParams p, HashParams h, uint64_t shar
 // <= 16, m <= 4 (rs_decode.hip, ENC).
 hipError_t launch_encode_hash_table(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                     hipStream_t stream);
-// ... and RS(8,4)'s, RS(6,4)'s, RS(4,4)'s (rs_decode_net.hip, 8-stripe
+// ... and RS(8,4)'s, RS(6,4)'s (rs_decode_net.hip, 8-stripe
 // workgroups, two network waves).
 const uint8_t* encode_net_coef();
 const uint8_t* encode_net6_coef();
-const uint8_t* encode_net4_coef();
 hipError_t launch_encode_hash_net(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                   hipStream_t stream);
 hipError_t launch_encode_hash_net6(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
-                                   hipStream_t stream);
-hipError_t launch_encode_hash_net4(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                    hipStream_t stream);
 // One-pass degraded GET (k_decode_records_dma) for RS(k, m), k <= 16, m <= 4,
 // any shard length (a ragged last step), over nf (k..k+m-1) present record
@@ -217,20 +214,6 @@ RSG_NET10_PART_DECL(5)
 RSG_NET10_PART_DECL(6)
 RSG_NET10_PART_DECL(7)
 #undef RSG_NET10_PART_DECL
-// RS(4,4) (rs_decode_net.hip built with RSG_NET_K=4, k_decode_records_net4): the same for R x 4 rows
-int records_net4_pattern(int heal, int nf, int R, int n_store, const uint8_t* coef);
-#define RSG_NET4_PART_DECL(i)                                                                                \
-    bool launch_records_net4_part##i(int pid, uint64_t blocks, const GfApplyParams& p, const HashParams& h, \
-                                     hipStream_t stream);
-RSG_NET4_PART_DECL(0)
-RSG_NET4_PART_DECL(1)
-RSG_NET4_PART_DECL(2)
-RSG_NET4_PART_DECL(3)
-RSG_NET4_PART_DECL(4)
-RSG_NET4_PART_DECL(5)
-RSG_NET4_PART_DECL(6)
-RSG_NET4_PART_DECL(7)
-#undef RSG_NET4_PART_DECL
 // RS(6,4) (rs_decode_net.hip built with RSG_NET_K=6, k_decode_records_net6): the same for R x 6 rows
 int records_net6_pattern(int heal, int nf, int R, int n_store, const uint8_t* coef);
 #define RSG_NET6_PART_DECL(i)                                                                                \

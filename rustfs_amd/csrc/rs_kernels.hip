@@ -1192,7 +1192,7 @@ bool set_knob(Tuning& v, const std::string& name, const char* value) {
     if (name == "RSG_FUSED") return flag(v.fused);
     if (name == "RSG_LOST_DISK_FAST") return flag(v.lost_disk_fast);
     if (name == "RSG_ZERO_COPY") return flag(v.zero_copy);
-    if (name == "RSG_VEC_BLOCK") return one_of(v.vec_block, 0, 64, 256, 512, 1024);
+    if (name == "RSG_VEC_BLOCK") return one_of(v.vec_block, 0, 64, 256);
     if (name == "RSG_VEC_OCC") return num(v.vec_occ, -1, 8);
     if (name == "RSG_ROLLED") return flag(v.rolled);
     if (name == "RSG_HASH_COPY") return flag(v.hash_direct_copy);
@@ -1402,6 +1402,8 @@ static GfKernel pick_vec_b(const Tuning& t, int C, int R) {
 // per KiB for one wave, 33 per 4 KiB for four (RS(12,4) at 1 MiB blocks, S =
 // 87382: encode 1.274 -> 1.112 ms, 0.562 -> 0.644 of HBM,
 // profiles/r04/c/enc12_ab.txt).  Tuning::vec_block forces one for A/B runs.
+// (Eight- and sixteen-wave workgroups for the rolled kernel measured slower
+// again in round 6: RS(12,4) 1.066 -> 1.214 / 1.501 ms, profiles/r06/enc12/.)
 static int vec_block_for(const Tuning& t, const GfApplyParams& p) {
     if (t.vec_block) return t.vec_block;
     bool lines = (uintptr_t)p.base % 128 == 0 && (uintptr_t)p.out_base % 128 == 0 && p.stripe_stride % 128 == 0 &&
@@ -1417,29 +1419,13 @@ static int vec_block_for(const Tuning& t, const GfApplyParams& p) {
 // each).  Default: 2 for the read-heavy rebuilds of one or two shards from 8
 // inputs, where fewer waves in flight stream better (RS(8,4) n = 4096: 1 lost
 // 0.846 -> 0.814 ms, 2 lost 0.905 -> 0.888 ms; profiles/r02/ab_occ2/), else
-// no cap.  RSG_VEC_OCC forces one value for A/B runs (tools/ab_occ.sh).
+// no cap.  RSG_VEC_OCC forces one value for A/B runs (tools/enc_ab.py).
 static int vec_occupancy(const Tuning& t, int C, int R, bool pre) {
     if (t.vec_occ >= 0) return t.vec_occ;
     return (!pre && C == 8 && R <= 2) ? 2 : 0;
 }
 
-// Eight- and sixteen-wave workgroups for the rolled kernel (C > 8): a ragged
-// row's chunk boundaries fall mid-line, and each boundary line is fetched by
-// both neighbouring workgroups (A/B: Tuning::vec_block = 512 / 1024).
-template <int B, bool PRE>
-static GfKernel pick_loop_big(int C, int R) {
-    if (C > 8 && C <= 12 && R == 4) return k_gf_apply_loop<4, B, PRE, 12>;
-    if (C > 12 && R == 4) return k_gf_apply_loop<4, B, PRE>;
-    return nullptr;
-}
-
 static GfKernel pick_vec(const Tuning& t, int C, int R, bool pre, int B) {
-    if (B == 512 || B == 1024) {
-        GfKernel k = B == 512 ? (pre ? pick_loop_big<512, true>(C, R) : pick_loop_big<512, false>(C, R))
-                              : (pre ? pick_loop_big<1024, true>(C, R) : pick_loop_big<1024, false>(C, R));
-        if (k && !t.rolled) return k;
-        B = 256;
-    }
     if (B == 256) return pre ? pick_vec_b<256, true>(t, C, R) : pick_vec_b<256, false>(t, C, R);
     return pre ? pick_vec_b<64, true>(t, C, R) : pick_vec_b<64, false>(t, C, R);
 }
@@ -1652,22 +1638,21 @@ static bool tables_match(const GfApplyParams& p, const uint8_t* coef, int C, int
 // RS(12,4) / RS(10,4) encode in place over 1024+ stripes (256+ workgroups of
 // 4): the fused network kernel (rs_decode_netq.hip, k_decode_records_net12 /
 // _net10 with ENC).
-// RS(8,4) / RS(6,4) / RS(4,4) encode in place: the 8-stripe network kernel
-// with ENC (rs_decode_net.hip) — from 2048 stripes (256+ workgroups).
+// RS(8,4) / RS(6,4) encode in place: the 8-stripe network kernel with ENC
+// (rs_decode_net.hip) — from 2048 stripes (256+ workgroups).
 static bool net_enc_supported(const GfApplyParams& p, uint64_t n_stripes) {
-    if ((p.C != 8 && p.C != 6 && p.C != 4) || p.R != 4 || p.mode != GF_MODE_STORE || p.copy_mask ||
+    if ((p.C != 8 && p.C != 6) || p.R != 4 || p.mode != GF_MODE_STORE || p.copy_mask ||
         p.base != p.out_base || p.stripe_stride != p.out_stripe_stride || n_stripes < 2048 ||
         5 * p.stripe_stride >= (1ull << 32))
         return false;
-    const uint8_t* coef = p.C == 8 ? encode_net_coef() : p.C == 6 ? encode_net6_coef() : encode_net4_coef();
+    const uint8_t* coef = p.C == 8 ? encode_net_coef() : encode_net6_coef();
     return tables_match(p, coef, (int)p.C, 4);
 }
 
 static hipError_t launch_encode_hash_net_c(const GfApplyParams& p, const HashParams& h, uint64_t shard_len,
                                            uint64_t n_stripes, hipStream_t stream) {
     if (p.C == 8) return launch_encode_hash_net(p, h, shard_len, n_stripes, stream);
-    if (p.C == 6) return launch_encode_hash_net6(p, h, shard_len, n_stripes, stream);
-    return launch_encode_hash_net4(p, h, shard_len, n_stripes, stream);
+    return launch_encode_hash_net6(p, h, shard_len, n_stripes, stream);
 }
 
 // k >= 9 (m <= 4, k + m <= 16) or RS(4,4) encode in place: the run-time-table
@@ -1761,7 +1746,7 @@ static hipError_t launch_encode_hash_wide(GfApplyParams p, HashParams h, uint64_
 hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shard_len, uint64_t n_stripes,
                                     hipStream_t stream) {
     // Packed workgroups measured as fast or faster than one stripe per
-    // workgroup at every batch size tried (n = 256..65536; tools/sweep_small_batch.sh);
+    // workgroup at every batch size tried (n = 256..65536; profiles/r01/README.md);
     // Tuning::fused_spw1 selects the unpacked variant for A/B runs.
     const Tuning& t = tuning();  // one snapshot for the whole launch
     const bool unpacked = t.fused_spw1;

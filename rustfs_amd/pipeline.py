@@ -266,7 +266,7 @@ def block_geometry(offset: int, length: int, block_size: int, block: int):
 def get_stream(erasure: Erasure, fds: List[Optional[int]], total_length: int, offset: int = 0,
                length: Optional[int] = None, algo: HashAlgorithm = HashAlgorithm.HighwayHash256S,
                batch_blocks: int = DEFAULT_BATCH_BLOCKS, stage: Optional[GetStage] = None,
-               views: bool = False) -> Iterator:
+               views: bool = False, data_shards_only: bool = False) -> Iterator:
     """Yield bytes [offset, offset + length) of an object whose shard files
     are open at `fds` (None: disk unavailable), verifying every record
     before use and rebuilding missing data on the GPU.  Range errors follow
@@ -278,7 +278,16 @@ def get_stream(erasure: Erasure, fds: List[Optional[int]], total_length: int, of
     stage, the rebuilt shards in their page-locked slots), in order, without
     joining them — write_data_blocks' form, which writes straight from the
     per-shard buffers (decode.rs:1390); a writev-ready iovec.  The views stay
-    valid until the next block is requested (the stages are reused)."""
+    valid until the next block is requested (the stages are reused).
+
+    data_shards_only=True: the reference's optional data-shards-only read
+    (RUSTFS_GET_LOCKSTEP_DATA_SHARDS_ONLY_ENABLE, decode.rs:125-143,
+    1031-1090; off by default there and here): while every data file is
+    readable only the k data files are read; with data files missing, that
+    many parity files plus one more (so the surplus check stays on) are
+    engaged from the start; a batch whose verify finds a record it cannot
+    serve engages every remaining parity file for the rest of the object and
+    is read and decoded again with them."""
     if length is None:
         length = total_length - offset
     if offset < 0 or length < 0 or offset + length > total_length:
@@ -296,7 +305,8 @@ def get_stream(erasure: Erasure, fds: List[Optional[int]], total_length: int, of
     start, end = offset // bs, (offset + length - 1) // bs
     full_end = min(end, nfull - 1)  # last full block in the range
     if start <= full_end:
-        yield from _get_full(erasure, fds, start, full_end, offset, length, algo, batch_blocks, stage, views)
+        yield from _get_full(erasure, fds, start, full_end, offset, length, algo, batch_blocks, stage, views,
+                             data_shards_only)
     if end >= nfull:  # the short last block: host path, verify-before-use
         tl = total_length - nfull * bs
         s_blk = calc_shard_size(tl, k)
@@ -352,7 +362,8 @@ class GetStage:
             self.pool = None
 
 
-def _get_full(erasure, fds, start, full_end, offset, length, algo, batch_blocks, reuse=None, views=False):
+def _get_full(erasure, fds, start, full_end, offset, length, algo, batch_blocks, reuse=None, views=False,
+              data_only=False):
     """Full blocks start..full_end: B-block batches, read-ahead of batch i+1
     into the other page-locked stage while batch i is decoded on the GPU."""
     import torch
@@ -367,14 +378,14 @@ def _get_full(erasure, fds, start, full_end, offset, length, algo, batch_blocks,
         gs.lock.acquire()
     try:
         gs.ensure(t, k, S, bs, cnt_max, dev)
-        yield from _get_batches(erasure, fds, start, full_end, offset, length, algo, cnt_max, gs, views)
+        yield from _get_batches(erasure, fds, start, full_end, offset, length, algo, cnt_max, gs, views, data_only)
     finally:
         gs.lock.release()
         if own:
             gs.close()
 
 
-def _get_batches(erasure, fds, start, full_end, offset, length, algo, cnt_max, gs, views=False):
+def _get_batches(erasure, fds, start, full_end, offset, length, algo, cnt_max, gs, views=False, data_only=False):
     """The in-place GET (reconstruct_into's contract, bridge.rs:274-307; the
     blocks written straight from the per-shard buffers, decode.rs:1390): the
     records are verified on the device, only the shards no verified record
@@ -389,6 +400,32 @@ def _get_batches(erasure, fds, start, full_end, offset, length, algo, cnt_max, g
     stage, files_dev, slots, host_slots, pool = gs.stage, gs.files_dev, gs.slots, gs.host_slots, gs.pool
     batches = [(b0, min(cnt_max, full_end + 1 - b0)) for b0 in range(start, full_end + 1, cnt_max)]
     got: dict = {}
+    # the files read (data_only: the data files, plus parity engaged as
+    # decode.rs:1069-1090 does; else every available file)
+    engaged = [fds[i] is not None and (not data_only or i < k) for i in range(t)]
+
+    def engage_parity(want):
+        have = sum(engaged[k:])
+        for i in range(k, t):
+            if have >= want:
+                break
+            if fds[i] is not None and not engaged[i]:
+                engaged[i] = True
+                have += 1
+
+    if data_only:
+        missing = sum(fds[i] is None for i in range(k))
+        if missing:
+            engage_parity(missing + 1)
+
+    def read_one(j, i):
+        b0, cnt = batches[j]
+        if fds[i] is None:
+            return False
+        try:
+            return os.preadv(fds[i], [memoryview(stage[j & 1][i][: cnt * rec])], b0 * rec) == cnt * rec
+        except OSError:
+            return False
 
     def fetch(j):
         """Batch j: one pread per shard file, files in parallel (a failed read
@@ -396,16 +433,8 @@ def _get_batches(erasure, fds, start, full_end, offset, length, algo, cnt_max, g
         into device set j & 1 (event landed[j & 1]) — so the copy of batch
         j+1 overlaps the decode of batch j."""
         b0, cnt = batches[j]
-
-        def one(i):
-            if fds[i] is None:
-                return False
-            try:
-                return os.preadv(fds[i], [memoryview(stage[j & 1][i][: cnt * rec])], b0 * rec) == cnt * rec
-            except OSError:
-                return False
-
-        ok = list(pool.map(one, range(t)))
+        want = list(engaged)
+        ok = list(pool.map(lambda i: want[i] and read_one(j, i), range(t)))
         with torch.cuda.stream(gs.copy_stream):
             for i in range(t):
                 if ok[i]:
@@ -433,6 +462,18 @@ def _get_batches(erasure, fds, start, full_end, offset, length, algo, cnt_max, g
                 [files_dev[j & 1][i][: cnt * rec] if ok[i] else None for i in range(t)], S, cnt, targets=slots,
                 target_stride=S, algo=algo.value, stream=s)
             bad = [x for x in status if x != _lib.RSG_OK]
+            more = [i for i in range(t) if fds[i] is not None and not ok[i] and i >= k]
+            if bad and data_only and more:  # a record it could not serve: engage every parity file, redo
+                engage_parity(t)
+                for i, r in zip(more, pool.map(lambda i: read_one(j, i), more)):
+                    ok[i] = r
+                    if r:
+                        files_dev[j & 1][i][: cnt * rec].copy_(torch.from_numpy(stage[j & 1][i][: cnt * rec]),
+                                                               non_blocking=True)
+                _, src, status = erasure.decode_records_into_batch(
+                    [files_dev[j & 1][i][: cnt * rec] if ok[i] else None for i in range(t)], S, cnt,
+                    targets=slots, target_stride=S, algo=algo.value, stream=s)
+                bad = [x for x in status if x != _lib.RSG_OK]
             if bad:
                 _lib.check(bad[0], "erasure decode")
             for i in range(k):  # only the rebuilt shards cross the link back

@@ -332,7 +332,6 @@ GEOS = {(6, 4): (11, 1001), (10, 4): (9, 1002), (4, 4): (13, 1003),
         # storageclass.rs:480-498): the table kernel with 8 row slots
         (8, 8): (7, 1031), (10, 6): (5, 1033), (5, 5): (9, 1035), (11, 5): (5, 1037), (7, 7): (7, 1039),
         (9, 7): (5, 1041)}
-LISTED4 = _listed("rs44_decode_nets.h", 8)
 LISTED6 = _listed("rs64_decode_nets.h", 10)
 LISTED10 = _listed("rs104_decode_nets.h", 14)
 
@@ -363,18 +362,12 @@ def records10(gpu, oracle):
     return _geo_records(oracle, 10, 4)
 
 
-@pytest.fixture(scope="module")
-def records4(gpu, oracle):
-    return _geo_records(oracle, 4, 4)
-
-
 def test_rs6_rs10_tables_list_every_pattern():
     """Every one- and two-shard loss: RS(6,4) 6 + 39 GET patterns (a data
     shard among the lost) and 10 + 45 heal patterns; RS(10,4) 10 + 85 and
     14 + 91; each + the heal of all four parity shards (the fused encode's)."""
     assert len([x for x in LISTED6 if not x[0]]) == 6 + 39 and len([x for x in LISTED6 if x[0]]) == 10 + 45 + 1
     assert len([x for x in LISTED10 if not x[0]]) == 10 + 85 and len([x for x in LISTED10 if x[0]]) == 14 + 91 + 1
-    assert len([x for x in LISTED4 if not x[0]]) == 4 + 22 and len([x for x in LISTED4 if x[0]]) == 8 + 28 + 1
 
 
 def _geo_case(oracle, k, data, heal, lost, m=4):
@@ -436,12 +429,6 @@ def test_rs6_every_listed_pattern(gpu, oracle, records6, one_pass, heal, lost):
     _geo_case(oracle, 6, records6, heal, lost, 4)
 
 
-@pytest.mark.parametrize("heal,lost", LISTED4, ids=lambda x: str(x))
-def test_rs4_every_listed_pattern(gpu, oracle, records4, one_pass, heal, lost):
-    """k_decode_records_net4 (rs_decode_net.hip over 4 survivors)."""
-    _geo_case(oracle, 4, records4, heal, lost, 4)
-
-
 @pytest.mark.parametrize("heal,lost", LISTED10, ids=lambda x: str(x))
 def test_rs10_every_listed_pattern(gpu, oracle, records10, one_pass, heal, lost):
     """k_decode_records_net10 (rs_decode_netq.hip, parts of 3, 3, 2, 2
@@ -450,7 +437,7 @@ def test_rs10_every_listed_pattern(gpu, oracle, records10, one_pass, heal, lost)
     _geo_case(oracle, 10, records10, heal, lost, 4)
 
 
-TABLE_GEOS = [(5, 4), (11, 4), (15, 1), (3, 2), (7, 1), (13, 3), (1, 1), (9, 4), (14, 2),
+TABLE_GEOS = [(5, 4), (11, 4), (15, 1), (3, 2), (7, 1), (13, 3), (1, 1), (9, 4), (14, 2), (4, 4),
               (8, 8), (10, 6), (5, 5), (11, 5), (7, 7), (9, 7)]
 TABLE_CASES = [(k, m, heal, lost) for k, m in TABLE_GEOS for heal, lost in _every_pattern(k, m)]
 
@@ -464,6 +451,46 @@ def table_records(gpu, oracle):
             cache[(k, m)] = _geo_records(oracle, k, m)
         return cache[(k, m)]
     return get
+
+
+def _multi_loss_patterns(k, m, count, seed):
+    """`count` three-loss and `count` four-loss patterns of RS(k, m) (seeded
+    sample, every one with a data shard among the lost for the GET), each as
+    a GET and as the heal of every lost shard — EC:5..8's one-pass kernels
+    for three and four lost drives (round 6; more take the two-pass path)."""
+    rng = np.random.default_rng(seed)
+    t, out = k + m, []
+    for e in (3, 4):
+        seen = set()
+        while len(seen) < count:
+            lost = tuple(sorted(int(x) for x in rng.choice(t, e, replace=False)))
+            if min(lost) < k:
+                seen.add(lost)
+        for lost in sorted(seen):
+            out += [(k, m, 0, lost), (k, m, 1, lost)]
+    return out
+
+
+MULTI_CASES = (_multi_loss_patterns(8, 8, 12, 88) + _multi_loss_patterns(10, 6, 12, 106) +
+               _multi_loss_patterns(5, 5, 6, 55) + _multi_loss_patterns(9, 7, 6, 97))
+
+
+@pytest.mark.parametrize("k,m,heal,lost", MULTI_CASES, ids=str)
+@pytest.mark.parametrize("engine", ["one_pass", "two_pass"])
+def test_ec58_three_four_lost(gpu, oracle, table_records, engine, k, m, heal, lost):
+    """EC:5..8 (m = 5..8 parity shards, storageclass.rs:480-498) with three
+    and four shards lost: GET in both forms and the heal of every lost shard,
+    bit-exact against the oracle's shards and digests, an altered surplus
+    parity reported for its stripe alone — through the one-pass table kernel
+    (8 row slots: missing + surplus <= m) and through the two-pass path."""
+    from rustfs_amd import _lib
+    L = _lib.load()
+    code = _lib.RSG_RECORD_ENGINE_ONE_PASS if engine == "one_pass" else _lib.RSG_RECORD_ENGINE_TWO_PASS
+    _lib.check(L.rsg_set_record_engine(gpu.handle, code))
+    try:
+        _geo_case(oracle, k, table_records(k, m), heal, lost, m)
+    finally:
+        _lib.check(L.rsg_set_record_engine(gpu.handle, _lib.RSG_RECORD_ENGINE_AUTO))
 
 
 def test_table_patterns_cover_every_loss():

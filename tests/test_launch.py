@@ -249,6 +249,7 @@ def test_host_path_plan():
         "get_stream_all_present": (n * t * rec, 0, pay),
         "get_stream_2_data_lost": (n * (t - 2) * rec, 2 * n * S, pay),
         "get_stream_bytes_all_present": (n * t * rec, 0, pay),
+        "get_stream_data_shards_only_all_present": (n * k * rec, 0, pay),
         "put_stream_hh256s": (pay, n * m * S + n * t * 32, pay),
     }
     # the larger direction bounds a full-duplex transfer

@@ -163,6 +163,41 @@ def test_range_get_views(gpu, tmp_path, lost):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("case", ["healthy", "data_lost", "rotten_data", "rotten_and_lost"])
+def test_get_data_shards_only(gpu, tmp_path, case):
+    """data_shards_only=True (the reference's RUSTFS_GET_LOCKSTEP_DATA_SHARDS_ONLY
+    read, decode.rs:1031-1090): the data files alone while they serve, missing
+    + 1 parity files engaged for lost data files, every parity file engaged
+    (and the batch decoded again) once a record cannot be served — the same
+    bytes as the default read in every case."""
+    from rustfs_amd.pipeline import get_stream
+    k, m = 4, 2
+    size = 9 * BS + 555
+    es, dirs = _set(tmp_path, k, m)
+    data = np.random.default_rng(11).integers(0, 256, size, dtype=np.uint8).tobytes()
+    es.put_object_stream("b/o", io.BytesIO(data), size, batch_blocks=4)
+    rec = 32 + BS // k
+    lost = (1,) if case in ("data_lost", "rotten_and_lost") else ()
+    if case in ("rotten_data", "rotten_and_lost"):
+        p = es.part_file(2, "b/o")
+        raw = bytearray(open(p, "rb").read())
+        raw[5 * rec + 32 + 99] ^= 0x10  # block 5, data shard 2's body: its digest no longer matches
+        open(p, "wb").write(bytes(raw))
+    for i in lost:
+        os.remove(es.part_file(i, "b/o"))
+    fds = [None if i in lost else os.open(es.part_file(i, "b/o"), os.O_RDONLY) for i in range(k + m)]
+    try:
+        for off, ln in [(0, size), (3 * BS + 7, 4 * BS), (size - 100, 100)]:
+            got = b"".join(b"".join(v) for v in get_stream(es.erasure, fds, size, off, ln, batch_blocks=2, views=True,
+                                                           data_shards_only=True))
+            assert got == data[off:off + ln], (case, off, ln)
+    finally:
+        for fd in fds:
+            if fd is not None:
+                os.close(fd)
+
+
+@pytest.mark.gpu
 def test_range_get_drops_corrupted_records(gpu, tmp_path):
     from rustfs_amd import RsgError
     size = 6 * BS + 100

@@ -27,10 +27,11 @@ RS(10,4) (`--k 10`, the default geometry of a 14-drive set) gets four
 parts (survivors 0-2 / 3-5 / 6-7 / 8-9) like RS(12,4) (rs104_decode_nets.h,
 rs_decode_netq.hip built with RSG_NETQ_K=10).
 
-RS(6,4) (`--k 6`, the default geometry of a 10-drive set) and RS(4,4)
-(`--k 4`, 8 drives) are generated like RS(8,4), one network over their 6 / 4
-survivors (rs64_decode_nets.h / rs44_decode_nets.h, run by rs_decode_net.hip
-built with RSG_NET_K=6 / 4).
+RS(6,4) (`--k 6`, the default geometry of a 10-drive set) is generated like
+RS(8,4), one network over its 6 survivors (rs64_decode_nets.h, run by
+rs_decode_net.hip built with RSG_NET_K=6).  `--k 4` (RS(4,4)) still
+generates, but the library no longer builds it (round 6: 2-5 % over the
+table kernel did not pay for its compile time).
 
 RS(16,4) (`--k 16`) and RS(12,4) (`--k 12`, the default geometry of a
 16-drive set, storageclass.rs:24-31): the survivors' 128 / 96 planes do not
