@@ -51,6 +51,9 @@
 #ifndef RSG_NET_PART
 #error "RSG_NET_PART (0 .. RSG_NET_PARTS-1) is set by the Makefile"
 #endif
+#ifndef RSG_NET_ABLATE
+#define RSG_NET_ABLATE 0
+#endif
 #ifndef RSG_NETQ_K
 #error "RSG_NETQ_K (12 or 10) is set by the Makefile"
 #endif
@@ -178,15 +181,22 @@ __device__ __forceinline__ void netq_wave(const GfApplyParams& p, uint64_t n, ui
             uint2 a[4];
             row4(slot + (C0 + c) * HS * IP, a);
             uint32_t w[8] = {a[0].x, a[0].y, a[1].x, a[1].y, a[2].x, a[2].y, a[3].x, a[3].y};
+#if !RSG_NET_ABLATE
             dma::transpose(w, m4, m2, m1);
+#endif
 #pragma unroll
             for (int j = 0; j < 8; ++j) P[8 * c + j] = w[j];
         }
         uint32_t O[32];
+#if RSG_NET_ABLATE  // experiment builds only: no arithmetic, rows = survivors (2: no LDS exchange either)
+#pragma unroll
+        for (int i = 0; i < 32; ++i) O[i] = P[i % (8 * NC)];
+#else
         decq::net_q<PID, Q>(P, O);
+#endif
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            if (r == Q) continue;
+            if (r == Q || RSG_NET_ABLATE >= 2) continue;
             uint32_t* xo = xb_at(r, t);
 #pragma unroll
             for (int i = 0; i < 8; ++i)
@@ -226,7 +236,9 @@ __device__ __forceinline__ void netq_wave(const GfApplyParams& p, uint64_t n, ui
 #pragma unroll
             for (int i = 0; i < 8; ++i) xa[64 * i] = 0u;
         }
+#if !RSG_NET_ABLATE
         dma::transpose(w, m4, m2, m1);
+#endif
         if constexpr (Q < NST) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
