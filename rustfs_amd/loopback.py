@@ -300,19 +300,22 @@ class LocalErasureSet:
         return fds
 
     def get_object_stream(self, name: str, offset: int = 0, length: Optional[int] = None,
-                          batch_blocks: int = DEFAULT_BATCH_BLOCKS) -> Iterator[bytes]:
+                          batch_blocks: int = DEFAULT_BATCH_BLOCKS, data_shards_only: bool = False) -> Iterator[bytes]:
         """Stream bytes [offset, offset + length) (default: to the end) of
         `name`: decode_inner's range read (decode.rs:1702-1968) with full
         blocks verified and rebuilt on the GPU B blocks at a time, the next
         batch read from the shard files while this one decodes.  The set's
         reusable GET stage stays locked while the stream is open: close() an
         abandoned stream (or consume it) so other GETs can reuse the stage;
-        get_object_range does."""
+        get_object_range does.  data_shards_only: the reference's optional
+        data-shards-only read (RUSTFS_GET_LOCKSTEP_DATA_SHARDS_ONLY_ENABLE,
+        pipeline.get_stream)."""
         meta = self._meta(name)
         size = meta["size"]
         fds = self._open_shards(name, size, meta["version"], meta["disks"])
         try:
-            yield from get_stream(self.erasure, fds, size, offset, length, self.algo, batch_blocks, self._get_stage)
+            yield from get_stream(self.erasure, fds, size, offset, length, self.algo, batch_blocks, self._get_stage,
+                                  data_shards_only=data_shards_only)
         finally:
             for fd in fds:
                 if fd is not None:

@@ -85,3 +85,28 @@ def test_engines_every_stripe_at_bench_size(gpu, oracle, k, m, S):
     got = slots.view(n, k, S)
     assert torch.equal(got[:, 0], st[:, 0])
     assert torch.equal(got[rot, 5], st[rot, 5])
+
+
+@pytest.mark.parametrize("k,m,S,lost", [(8, 8, 131072, (0, 3, 5)), (10, 6, 104858, (1, 4, 7, 12))])
+def test_ec58_multi_loss_every_stripe_at_bench_size(gpu, k, m, S, lost):
+    """EC:5..8 (storageclass.rs:480-498) at n = 4096 records of 1 MiB blocks
+    with three / four shards lost (round 6: the one-pass table kernel with 8
+    row slots): the GET's rebuilt data shards equal the encoded data and the
+    heal of every lost shard writes the encoder's record files, digest
+    headers included, in every stripe."""
+    import torch
+    n = 4096
+    t, rec = k + m, 32 + S
+    e, st, dig, files = _records(torch, k, m, S, n, seed=k * 31 + m)
+    slots = torch.full((n, k * S), 0xA5, dtype=torch.uint8, device="cuda")
+    _, src, status = e.decode_records_into_batch([None if i in lost else files[i] for i in range(t)], S, n,
+                                                 targets=slots)
+    assert status == [0] * n
+    got = slots.view(n, k, S)
+    for i in lost:
+        if i < k:
+            assert not src[i].any() and torch.equal(got[:, i], st[:, i]), f"rebuilt shard {i}"
+    tg = [torch.zeros(n * rec, dtype=torch.uint8, device="cuda") if i in lost else None for i in range(t)]
+    assert e.heal_records_batch([None if i in lost else files[i] for i in range(t)], tg, S, n) == [0] * n
+    for i in lost:
+        assert torch.equal(tg[i], files[i]), f"healed file {i}"
