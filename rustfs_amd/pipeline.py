@@ -447,12 +447,27 @@ def _get_batches(erasure, fds, start, full_end, offset, length, algo, cnt_max, g
     th.start()
     try:
         s = torch.cuda.current_stream(dev)
+        def read_parity_now(j, ok):
+            """data_only: every available parity file not read for batch j,
+            read and copied up now (on the compute stream, before its decode)."""
+            engage_parity(t)
+            cnt = batches[j][1]
+            more = [i for i in range(k, t) if fds[i] is not None and not ok[i]]
+            for i, r in zip(more, pool.map(lambda i: read_one(j, i), more)):
+                ok[i] = r
+                if r:
+                    files_dev[j & 1][i][: cnt * rec].copy_(torch.from_numpy(stage[j & 1][i][: cnt * rec]),
+                                                           non_blocking=True)
+            return bool(more)
+
         for j, (b0, cnt) in enumerate(batches):
             th.join()
             ok = got.pop(j)
+            s.wait_event(gs.landed[j & 1])
+            if data_only and not all(ok[i] for i in range(k) if fds[i] is not None):
+                read_parity_now(j, ok)  # a data file failed to read: its reader is replaced by parity
             if sum(ok) < k:
                 raise _lib.RsgError(_lib.RSG_ERR_TOO_FEW_SHARDS, "read quorum lost")
-            s.wait_event(gs.landed[j & 1])
             # batch j+1 goes into the other stage and device set, free since
             # batch j-1 was decoded and its blocks yielded
             if j + 1 < len(batches):
@@ -462,14 +477,8 @@ def _get_batches(erasure, fds, start, full_end, offset, length, algo, cnt_max, g
                 [files_dev[j & 1][i][: cnt * rec] if ok[i] else None for i in range(t)], S, cnt, targets=slots,
                 target_stride=S, algo=algo.value, stream=s)
             bad = [x for x in status if x != _lib.RSG_OK]
-            more = [i for i in range(t) if fds[i] is not None and not ok[i] and i >= k]
-            if bad and data_only and more:  # a record it could not serve: engage every parity file, redo
-                engage_parity(t)
-                for i, r in zip(more, pool.map(lambda i: read_one(j, i), more)):
-                    ok[i] = r
-                    if r:
-                        files_dev[j & 1][i][: cnt * rec].copy_(torch.from_numpy(stage[j & 1][i][: cnt * rec]),
-                                                               non_blocking=True)
+            # a record it could not serve: engage every parity file, decode again
+            if bad and data_only and read_parity_now(j, ok):
                 _, src, status = erasure.decode_records_into_batch(
                     [files_dev[j & 1][i][: cnt * rec] if ok[i] else None for i in range(t)], S, cnt,
                     targets=slots, target_stride=S, algo=algo.value, stream=s)

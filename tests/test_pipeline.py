@@ -163,7 +163,7 @@ def test_range_get_views(gpu, tmp_path, lost):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["healthy", "data_lost", "rotten_data", "rotten_and_lost"])
+@pytest.mark.parametrize("case", ["healthy", "data_lost", "rotten_data", "rotten_and_lost", "truncated_data"])
 def test_get_data_shards_only(gpu, tmp_path, case):
     """data_shards_only=True (the reference's RUSTFS_GET_LOCKSTEP_DATA_SHARDS_ONLY
     read, decode.rs:1031-1090): the data files alone while they serve, missing
@@ -185,6 +185,8 @@ def test_get_data_shards_only(gpu, tmp_path, case):
         open(p, "wb").write(bytes(raw))
     for i in lost:
         os.remove(es.part_file(i, "b/o"))
+    if case == "truncated_data":  # data file 3 ends after 4 records: its later reads fail mid-object
+        os.truncate(es.part_file(3, "b/o"), 4 * rec)
     fds = [None if i in lost else os.open(es.part_file(i, "b/o"), os.O_RDONLY) for i in range(k + m)]
     try:
         for off, ln in [(0, size), (3 * BS + 7, 4 * BS), (size - 100, 100)]:
