@@ -41,6 +41,7 @@ from .erasure import Erasure, calc_shard_size
 
 DEFAULT_BATCH_BLOCKS = 64      # blocks per GPU job (the reference batches 4 on the CPU)
 DEFAULT_INFLIGHT_BATCHES = 2   # encoded batches queued for the writers
+IO_THREADS = 16                # shard-file readers (GET) / writers (PUT), capped at one per shard file
 
 
 def _pinned(shape) -> np.ndarray:
@@ -154,7 +155,7 @@ def put_stream(erasure: Erasure, reader, size: int, fds: List[Optional[int]],
         free.put(i)
     done: "queue.Queue" = queue.Queue(maxsize=inflight_batches)
     errors: List[BaseException] = []
-    pool = ThreadPoolExecutor(max_workers=min(t, 8))
+    pool = ThreadPoolExecutor(max_workers=min(t, IO_THREADS))
     src = _file_source(reader) if read_threads > 1 else None
     rpool = ThreadPoolExecutor(max_workers=read_threads) if src else None
     clock = {"read_s": 0.0, "submit_s": 0.0, "wait_s": 0.0, "write_s": 0.0}
@@ -354,7 +355,7 @@ class GetStage:
             self.host_slots = [_pinned(cnt_max * S) for _ in range(k)]
             self.key, self.cnt = key, cnt_max
         if self.pool is None:
-            self.pool = ThreadPoolExecutor(max_workers=min(t, 8))
+            self.pool = ThreadPoolExecutor(max_workers=min(t, IO_THREADS))
 
     def close(self) -> None:
         if self.pool is not None:
