@@ -65,6 +65,74 @@ struct GetShape : RecRing<NF, G, TH> {
     static constexpr int WPE = RD == 2 ? (2 * WAVES + 3) / 4 : 1;
 };
 
+// One step's GF rows 0..ROWS-1 of a table-kernel GF wave: acc[r] = sum over
+// survivors c of tab[c][r] * x[c] (8 bytes a lane), the (c, r) terms in
+// c-major order in units of 4, unit u + 1's coefficient tables read from the
+// LDS while unit u's perms run (sched_barrier keeps that order; 2 x 20
+// registers of tables), one basic block a step.  Rows past ROWS are not
+// touched.  (A loop with a per-row `r < R` exit made every term its own block
+// with its LDS read's latency exposed: RS(8,8) GET 2.74 -> 2.35 ms, RS(9,4)
+// 1.59 -> 1.52 this way; computing all RM rows whatever R instead cost more
+// than that where R < RM: RS(3,2) GET, R = 2 of 4, 1.55 -> 1.78 ms;
+// profiles/r06/gf_pipe/.)
+template <int C, int RM, int ROWS>
+__device__ __forceinline__ void gf_rows(const uint2 (&x)[C], const uint8_t* tb, uint32_t m7, uint32_t m3,
+                                        uint32_t (&acc)[RM][2], uint32_t (&pend)[RM][2]) {
+    constexpr int N = C * ROWS, UW = C > 8 ? 2 : 4, U = (N + UW - 1) / UW;  // (C > 8: 4 would spill)
+    uint4 ta[2][UW];
+    uint32_t tc[2][UW];
+    auto load_unit = [&](int u, int b) {
+#pragma unroll
+        for (int j = 0; j < UW; ++j) {
+            const int i = u * UW + j;
+            if (i >= N) break;
+            const uint8_t* tp = tb + ((i / ROWS) * RM + i % ROWS) * 32;
+            ta[b][j] = *(const uint4*)tp;
+            tc[b][j] = *(const uint32_t*)(tp + 16);
+        }
+    };
+    load_unit(0, 0);
+    // this variant's own masks: the selectors below are not hoisted above
+    // the caller's choice of variant (all C x 6 live at once)
+    asm volatile("" : "+v"(m7), "+v"(m3));
+    uint32_t sel[C][6];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if (u + 1 < U) load_unit(u + 1, (u + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < UW; ++j) {
+            const int i = u * UW + j, c = i / ROWS, r = i % ROWS, b = u & 1;
+            if (i >= N) break;
+            if (r == 0) {
+                sel[c][0] = x[c].x & m7, sel[c][1] = x[c].y & m7;
+                sel[c][2] = (x[c].x >> 3) & m7, sel[c][3] = (x[c].y >> 3) & m7;
+                sel[c][4] = (x[c].x >> 6) & m3, sel[c][5] = (x[c].y >> 6) & m3;
+            }
+            const uint4 t4 = ta[b][j];
+            const uint32_t t2 = tc[b][j];
+            gf_fold(c & 1, acc[r][0], pend[r][0], __builtin_amdgcn_perm(t4.y, t4.x, sel[c][0]),
+                    __builtin_amdgcn_perm(t4.w, t4.z, sel[c][2]), __builtin_amdgcn_perm(t2, t2, sel[c][4]));
+            gf_fold(c & 1, acc[r][1], pend[r][1], __builtin_amdgcn_perm(t4.y, t4.x, sel[c][1]),
+                    __builtin_amdgcn_perm(t4.w, t4.z, sel[c][3]), __builtin_amdgcn_perm(t2, t2, sel[c][5]));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// gf_rows where a step has at least 16 (c, r) terms (fewer: the per-row loop
+// is as fast — RS(3,2) GET, 6 terms, 1.60 against 1.66 ms); false otherwise.
+template <int C, int RM, int ROWS>
+__device__ __forceinline__ bool gf_rows_pipe(const uint2 (&x)[C], const uint8_t* tb, uint32_t m7, uint32_t m3,
+                                             uint32_t (&acc)[RM][2], uint32_t (&pend)[RM][2]) {
+    if constexpr (C * ROWS >= 16) {
+        gf_rows<C, RM, ROWS>(x, tb, m7, m3, acc, pend);
+        return true;
+    } else {
+        return false;
+    }
+}
+
 // ENC: the fused encode + HH256S over a stripe buffer (launch_encode_hash_table:
 // the heal of every parity shard, p.out_* the parity rows in place, every
 // digest to h.out in the batch digest layout instead of verified / written
@@ -136,21 +204,37 @@ __attribute__((amdgpu_waves_per_eu(GetShape<NF, G, TH, RD>::WPE))) void k_decode
             uint32_t acc[RM][2], pend[RM][2];
 #pragma unroll
             for (int r = 0; r < RM; ++r) acc[r][0] = acc[r][1] = pend[r][0] = pend[r][1] = 0u;
+            // R rows a step, R = RM or (RM = 4) fewer: the rebuilt rows plus the
+            // surplus compared, m rows for a data-shard loss (wave-uniform)
+            bool piped = false;
+            if constexpr (RM == 4) {
+                if (R == 4) piped = gf_rows_pipe<C, 4, 4>(x, tb, m7, m3, acc, pend);
+                else if (R == 3) piped = gf_rows_pipe<C, 4, 3>(x, tb, m7, m3, acc, pend);
+                else if (R == 2) piped = gf_rows_pipe<C, 4, 2>(x, tb, m7, m3, acc, pend);
+                else piped = gf_rows_pipe<C, 4, 1>(x, tb, m7, m3, acc, pend);
+            } else {  // EC:5..8: m rows for a data-shard loss, m = 5..8
+                if (R == 8) piped = gf_rows_pipe<C, RM, 8>(x, tb, m7, m3, acc, pend);
+                else if (R == 7) piped = gf_rows_pipe<C, RM, 7>(x, tb, m7, m3, acc, pend);
+                else if (R == 6) piped = gf_rows_pipe<C, RM, 6>(x, tb, m7, m3, acc, pend);
+                else if (R == 5) piped = gf_rows_pipe<C, RM, 5>(x, tb, m7, m3, acc, pend);
+            }
+            if (!piped) {  // few terms, or EC:5..8 with at most 4 rows: per row
 #pragma unroll
-            for (int c = 0; c < C; ++c) {
-                const uint32_t s0a = x[c].x & m7, s0b = x[c].y & m7;
-                const uint32_t s1a = (x[c].x >> 3) & m7, s1b = (x[c].y >> 3) & m7;
-                const uint32_t s2a = (x[c].x >> 6) & m3, s2b = (x[c].y >> 6) & m3;
+                for (int c = 0; c < C; ++c) {
+                    const uint32_t s0a = x[c].x & m7, s0b = x[c].y & m7;
+                    const uint32_t s1a = (x[c].x >> 3) & m7, s1b = (x[c].y >> 3) & m7;
+                    const uint32_t s2a = (x[c].x >> 6) & m3, s2b = (x[c].y >> 6) & m3;
 #pragma unroll
-                for (int r = 0; r < RM; ++r) {
-                    if ((uint32_t)r >= R) break;  // wave-uniform
-                    const uint8_t* tp = tb + (c * RM + r) * 32;
-                    const uint4 t4 = *(const uint4*)tp;
-                    const uint32_t t2 = *(const uint32_t*)(tp + 16);
-                    gf_fold(c & 1, acc[r][0], pend[r][0], __builtin_amdgcn_perm(t4.y, t4.x, s0a),
-                            __builtin_amdgcn_perm(t4.w, t4.z, s1a), __builtin_amdgcn_perm(t2, t2, s2a));
-                    gf_fold(c & 1, acc[r][1], pend[r][1], __builtin_amdgcn_perm(t4.y, t4.x, s0b),
-                            __builtin_amdgcn_perm(t4.w, t4.z, s1b), __builtin_amdgcn_perm(t2, t2, s2b));
+                    for (int r = 0; r < RM; ++r) {
+                        if ((uint32_t)r >= R) break;  // wave-uniform
+                        const uint8_t* tp = tb + (c * RM + r) * 32;
+                        const uint4 t4 = *(const uint4*)tp;
+                        const uint32_t t2 = *(const uint32_t*)(tp + 16);
+                        gf_fold(c & 1, acc[r][0], pend[r][0], __builtin_amdgcn_perm(t4.y, t4.x, s0a),
+                                __builtin_amdgcn_perm(t4.w, t4.z, s1a), __builtin_amdgcn_perm(t2, t2, s2a));
+                        gf_fold(c & 1, acc[r][1], pend[r][1], __builtin_amdgcn_perm(t4.y, t4.x, s0b),
+                                __builtin_amdgcn_perm(t4.w, t4.z, s1b), __builtin_amdgcn_perm(t2, t2, s2b));
+                    }
                 }
             }
             if constexpr (C & 1) {  // an odd survivor count leaves its last coefficient's third term pending
@@ -160,6 +244,10 @@ __attribute__((amdgpu_waves_per_eu(GetShape<NF, G, TH, RD>::WPE))) void k_decode
                     acc[r][1] ^= pend[r][1];
                 }
             }
+            // the rows exist here, whatever uses them below (not sunk into the
+            // conditional store / compare blocks, with their table reads)
+#pragma unroll
+            for (int r = 0; r < RM; ++r) asm volatile("" : "+v"(acc[r][0]), "+v"(acc[r][1]));
             const bool part = s + 1 == steps && tail != CH;  // wave-uniform
             const uint64_t keep = part ? part_mask8(lane * 8u, tail) : ~0ull;
 #pragma unroll
