@@ -395,8 +395,7 @@ int RSG_DEC_CAT(launch_get_wide_, RSG_DECODE_C)(int m, int nf, int th, uint64_t 
 #elif defined(RSG_DECODE_C)
 // This part's fused encode + HH256S (k = C data shards, m = 1..4 parity):
 // the heal of every parity shard with ENC — built where the fused launcher
-// takes it (table_enc_geometry: k >= 9, and RS(4,4)); false elsewhere.
-constexpr bool table_enc_geometry(int k, int m) { return (k >= 9 && k + m <= 16) || (k == 4 && m == 4); }
+// takes it (table_enc_geometry, rs_kernels.h); false elsewhere.
 template <int C, int M>
 static bool launch_enc_m(uint64_t blocks, const GfApplyParams& p, const HashParams& h, hipStream_t stream) {
     if constexpr (!table_enc_geometry(C, M)) {

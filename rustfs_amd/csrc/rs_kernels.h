@@ -178,6 +178,15 @@ bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len);
 // survivors and R rows (rebuilt / healed + compared), two_per_cu: the launch
 // shape fits two workgroups a CU (rs_decode.hip).
 bool table_one_pass_preferred(int k, int R, bool two_per_cu);
+// The fused encode + HH256S (config 4's kernel for other geometries) on the
+// run-time-table one-pass kernel with ENC, where it measured faster than the
+// packed k_encode_hash_fused at 1 MiB blocks, n = 4096 (k >= 9: 2-9 %,
+// profiles/r05/fused_table/; k = 4..8 since round 6's gf_rows: 2-9 %, RS(3,3)
+// 3 %, profiles/r06/fused_table/) — not RS(4,3) / RS(5,3) (1-5 % slower),
+// RS(2,2) (13 % slower), RS(3,2) (level) or k + m > 16.
+constexpr bool table_enc_geometry(int k, int m) {
+    return m >= 1 && m <= 4 && k + m <= 16 && (k >= 4 || (k == 3 && m == 3)) && !(m == 3 && (k == 4 || k == 5));
+}
 hipError_t launch_heal_records_dma(GfApplyParams p, HashParams h, int k, int m, int nf, int targets,
                                    uint64_t shard_len, uint64_t n_stripes, const uint8_t* coef, bool any_table,
                                    hipStream_t stream);

@@ -1655,10 +1655,10 @@ static hipError_t launch_encode_hash_net_c(const GfApplyParams& p, const HashPar
     return launch_encode_hash_net6(p, h, shard_len, n_stripes, stream);
 }
 
-// k >= 9 (m <= 4, k + m <= 16) or RS(4,4) encode in place: the run-time-table
-// one-pass kernel with ENC (rs_decode.hip builds it for those geometries only).
+// Encode in place on the run-time-table one-pass kernel with ENC, for the
+// geometries rs_decode.hip builds it for (table_enc_geometry).
 static bool table_enc_supported(const GfApplyParams& p, uint64_t n_stripes) {
-    return ((p.C >= 9 && p.C + p.R <= 16) || (p.C == 4 && p.R == 4)) && p.R >= 1 && p.R <= 4 &&
+    return table_enc_geometry((int)p.C, (int)p.R) &&
            p.mode == GF_MODE_STORE && !p.copy_mask &&
            p.base == p.out_base && p.stripe_stride == p.out_stripe_stride && n_stripes >= 1 &&
            5 * p.stripe_stride < (1ull << 32);
@@ -1791,11 +1791,9 @@ hipError_t launch_encode_hash_fused(GfApplyParams p, HashParams h, uint64_t shar
     // table kernel and keeps it, profiles/r05/ab_fused_net/)
     if (kind != 1 && p.C == 6 && net_enc_supported(p, n_stripes))
         return launch_encode_hash_net_c(p, h, shard_len, n_stripes, stream);
-    // k >= 9 without a network (RS(9,4), RS(11,4), RS(13,3), RS(14,2),
-    // RS(15,1), ...) and RS(4,4), 1024+ stripes: the run-time-table one-pass
-    // kernel with ENC — 2-9 % faster than the packed kernel there (4-stripe
-    // workgroups, two a CU), 6-12 % slower at k <= 8 otherwise
-    // (profiles/r05/fused_table/)
+    // Geometries without a network, 1024+ stripes: the run-time-table
+    // one-pass kernel with ENC where it measured faster than the packed
+    // kernel (table_enc_geometry: k >= 9, and most of k = 3..8 since round 6)
     if (kind != 1 && n_stripes >= 1024 && table_enc_supported(p, n_stripes))
         return launch_encode_hash_table(p, h, shard_len, n_stripes, stream);
     const FusedPick f = pick_fused((int)p.C, (int)p.R, !unpacked);

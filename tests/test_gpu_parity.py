@@ -384,17 +384,28 @@ def test_fused_net_kernel_forced_rs84(gpu, oracle, n, S):
 
 @pytest.mark.parametrize("k,m,S,n", [(4, 4, 1000, 19), (11, 4, 4099, 9), (9, 2, 31, 7), (14, 2, 1536, 5),
                                      (12, 3, 600, 6), (10, 1, 100, 3), (9, 4, 1024, 13), (13, 3, 2049, 4),
-                                     (12, 4, 4096, 10), (15, 1, 513, 11)])
+                                     (12, 4, 4096, 10), (15, 1, 513, 11), (3, 3, 777, 9), (5, 4, 512, 17),
+                                     (7, 4, 1500, 8), (6, 2, 33, 5), (8, 1, 2048, 12), (5, 2, 96, 3),
+                                     (7, 3, 4097, 10), (4, 1, 640, 1)])
 def test_fused_table_kernel_forced(gpu, oracle, k, m, S, n):
     """The fused encode + HH256S on the run-time-table one-pass kernel (ENC:
     the heal of every parity shard over the stripe buffer; RSG_FUSED_KIND=
     table through rsg_set_tuning): parity and every digest against the oracle
-    — RS(4,4)'s 8-stripe and k >= 9's 4-stripe workgroups (the geometries it
-    is built for), partial last workgroups, ragged walks, a lone remainder
-    packet."""
+    — the 8-stripe workgroups of k <= 8 and the 4-stripe ones of k >= 9 (the
+    geometries it is built for, table_enc_geometry), partial last workgroups,
+    ragged walks, a lone remainder packet."""
     from rustfs_amd import _lib
     with _lib.tuned(RSG_FUSED_KIND="table"):
         test_fused_kernel_selection_matches_oracle(gpu, oracle, k, m, S, n)
+
+
+@pytest.mark.parametrize("k,m,S,n", [(7, 4, 520, 2050), (3, 3, 64, 2048), (6, 2, 1000, 2051), (5, 3, 96, 2049)])
+def test_fused_default_selection_small_k(gpu, oracle, k, m, S, n):
+    """From 2048 stripes the default fused encode of k = 3..8 geometries
+    without a network runs the table kernel's ENC mode where it is built
+    (RS(7,4), RS(3,3), RS(6,2)) and the packed kernel elsewhere (RS(5,3)):
+    parity and every digest against the oracle on a sample of stripes."""
+    test_fused_kernel_selection_matches_oracle(gpu, oracle, k, m, S, n)
 
 
 @pytest.mark.parametrize("k,m,S", [(200, 56, 67), (128, 128, 48), (255, 1, 33), (1, 255, 40)])
