@@ -345,18 +345,40 @@ using WideLaunch = int (*)(int m, int nf, int th, uint64_t n_stripes, const GfAp
 // to RM = 8 rows (missing data + surplus parity, or heal targets + surplus)
 // for every one- and two-loss pattern — GET with one or two files absent,
 // heal of one target (the other files present, or one more absent) or two —
-// and (round 6) GET with three or four files absent and the heal of all three
-// or four lost shards, in 4-stripe workgroups (the ring of up to 15 files
-// would not fit 8).  Other patterns take the two-pass path.
+// and (round 6) GET with three to m files absent and the heal of all of
+// them, in 4-stripe workgroups (the ring of up to 15 files would not fit 8).
+// Other patterns (a heal of some of several lost shards) take the two-pass
+// path.
+// Preferred (not forced): as table_one_pass_preferred, and the heal of five
+// or more lost shards (9-wave workgroups, one a CU: RS(8,8) heal of 5 lost
+// 2.74 vs 3.21 ms two-pass, RS(10,6) of 6 2.23 vs 2.62), but not a GET that
+// rebuilds 8 rows (RS(8,8) with every data shard lost: 2.70 vs 2.25 ms;
+// profiles/r06/ec58/many_lost/).
 template <int C, int NF, int TH>
 static int launch_wide(uint64_t n_stripes, const GfApplyParams& p, const HashParams& h, bool any_table,
                        hipStream_t stream) {
     constexpr int G = 4, RM = 8;
-    if (!any_table && !table_one_pass_preferred(C, (int)p.R, table_rd<C, NF, G, TH, RM>() == 2)) return kTabDeclined;
+    const bool pref = (TH >= 5 || table_one_pass_preferred(C, (int)p.R, table_rd<C, NF, G, TH, RM>() == 2)) &&
+                      !(TH == 0 && p.n_store >= 8);
+    if (!any_table && !pref) return kTabDeclined;
     const uint64_t blocks = (n_stripes + G - 1) / G;
     if (blocks > 0x7fffffffull) return kTabInvalid;
     launch_get<C, NF, G, TH, RM>(blocks, p, h, stream);
     return kTabLaunched;
+}
+
+// L = 5..M files lost: the GET (th = 0) and the heal of all L (th = L)
+template <int C, int M, int L>
+static int launch_wide_many(int nf, int th, uint64_t n_stripes, const GfApplyParams& p, const HashParams& h,
+                            bool any_table, hipStream_t stream) {
+    if constexpr (L > M) {
+        return kTabInvalid;
+    } else {
+        constexpr int T = C + M;
+        if (nf == T - L && th == 0) return launch_wide<C, T - L, 0>(n_stripes, p, h, any_table, stream);
+        if (nf == T - L && th == L) return launch_wide<C, T - L, L>(n_stripes, p, h, any_table, stream);
+        return launch_wide_many<C, M, L + 1>(nf, th, n_stripes, p, h, any_table, stream);
+    }
 }
 
 template <int C, int M>
@@ -371,13 +393,13 @@ static int launch_wide_m(int nf, int th, uint64_t n_stripes, const GfApplyParams
         if (th == 1 && nf == T - 1) return launch_wide<C, T - 1, 1>(n_stripes, p, h, any_table, stream);
         if (th == 1 && nf == T - 2) return launch_wide<C, T - 2, 1>(n_stripes, p, h, any_table, stream);
         if (th == 2 && nf == T - 2) return launch_wide<C, T - 2, 2>(n_stripes, p, h, any_table, stream);
-        // three and four files lost (round 6): the GET, and the heal of
-        // every lost shard — still at most m = 8 rows (missing + surplus)
+        // three to m files lost (round 6): the GET, and the heal of every
+        // lost shard — still at most m rows (missing + surplus)
         if (th == 0 && nf == T - 3) return launch_wide<C, T - 3, 0>(n_stripes, p, h, any_table, stream);
         if (th == 0 && nf == T - 4) return launch_wide<C, T - 4, 0>(n_stripes, p, h, any_table, stream);
         if (th == 3 && nf == T - 3) return launch_wide<C, T - 3, 3>(n_stripes, p, h, any_table, stream);
         if (th == 4 && nf == T - 4) return launch_wide<C, T - 4, 4>(n_stripes, p, h, any_table, stream);
-        return kTabInvalid;
+        return launch_wide_many<C, M, 5>(nf, th, n_stripes, p, h, any_table, stream);
     }
 }
 
@@ -478,7 +500,7 @@ static int launch_get_any(int k, int m, int nf, int th, uint64_t n_stripes, cons
     if (m > 4) {
         static const WideLaunch wide[7] = {launch_get_wide_5, launch_get_wide_6,  launch_get_wide_7, launch_get_wide_8,
                                            launch_get_wide_9, launch_get_wide_10, launch_get_wide_11};
-        if (k < 5 || k > 11 || m > 8 || th < 0 || th > 4) return kTabInvalid;
+        if (k < 5 || k > 11 || m > 8 || th < 0 || th > m) return kTabInvalid;
         return wide[k - 5](m, nf, th, n_stripes, p, h, any_table, stream);
     }
     static const TabLaunch parts[16] = {launch_get_tab_1,  launch_get_tab_2,  launch_get_tab_3,  launch_get_tab_4,
@@ -510,13 +532,13 @@ static bool wide_geometry(int k, int m, uint64_t shard_len) {
 static int rows_max(int m) { return m > 4 ? 8 : 4; }
 
 bool decode_dma_supported(int k, int m, int nf, uint64_t shard_len) {
-    if (wide_geometry(k, m, shard_len)) return nf >= k + m - 4 && nf < k + m;
+    if (wide_geometry(k, m, shard_len)) return nf >= k && nf < k + m;
     return one_pass_geometry(k, m, shard_len) && nf >= k && nf < k + m;
 }
 
 bool heal_dma_supported(int k, int m, int nf, int targets, uint64_t shard_len) {
     if (wide_geometry(k, m, shard_len))
-        return (targets == 1 && nf >= k + m - 2 && nf <= k + m - 1) || (targets >= 2 && targets <= 4 && nf == k + m - targets);
+        return (targets == 1 && nf >= k + m - 2 && nf <= k + m - 1) || (targets >= 2 && targets <= m && nf == k + m - targets);
     return one_pass_geometry(k, m, shard_len) && nf >= k && targets >= 1 && nf + targets <= k + m;
 }
 

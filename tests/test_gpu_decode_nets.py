@@ -453,14 +453,14 @@ def table_records(gpu, oracle):
     return get
 
 
-def _multi_loss_patterns(k, m, count, seed):
-    """`count` three-loss and `count` four-loss patterns of RS(k, m) (seeded
+def _multi_loss_patterns(k, m, count, seed, losses=(3, 4)):
+    """`count` patterns of RS(k, m) per loss count in `losses` (seeded
     sample, every one with a data shard among the lost for the GET), each as
     a GET and as the heal of every lost shard — EC:5..8's one-pass kernels
-    for three and four lost drives (round 6; more take the two-pass path)."""
+    for three to m lost drives (round 6)."""
     rng = np.random.default_rng(seed)
     t, out = k + m, []
-    for e in (3, 4):
+    for e in losses:
         seen = set()
         while len(seen) < count:
             lost = tuple(sorted(int(x) for x in rng.choice(t, e, replace=False)))
@@ -491,6 +491,20 @@ def test_ec58_three_four_lost(gpu, oracle, table_records, engine, k, m, heal, lo
         _geo_case(oracle, k, table_records(k, m), heal, lost, m)
     finally:
         _lib.check(L.rsg_set_record_engine(gpu.handle, _lib.RSG_RECORD_ENGINE_AUTO))
+
+
+MANY_CASES = (_multi_loss_patterns(8, 8, 3, 808, range(5, 9)) + _multi_loss_patterns(10, 6, 3, 1006, (5, 6)) +
+              _multi_loss_patterns(5, 5, 3, 505, (5,)) + _multi_loss_patterns(9, 7, 2, 907, (5, 6, 7)))
+
+
+@pytest.mark.parametrize("k,m,heal,lost", MANY_CASES, ids=str)
+@pytest.mark.parametrize("engine", ["one_pass", "two_pass"])
+def test_ec58_five_or_more_lost(gpu, oracle, table_records, engine, k, m, heal, lost):
+    """EC:5..8 with five to m shards lost (every parity shard spent at RS(8,8)
+    with 8 lost: no surplus to compare): GET in both forms and the heal of
+    every lost shard, bit-exact against the oracle, through the one-pass
+    table kernel (round 6) and through the two-pass path."""
+    test_ec58_three_four_lost(gpu, oracle, table_records, engine, k, m, heal, lost)
 
 
 def test_table_patterns_cover_every_loss():
