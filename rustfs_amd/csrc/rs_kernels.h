@@ -40,7 +40,7 @@ struct Tuning {
     bool hash_direct_copy = false;  // RSG_HASH_COPY=1: 8-byte copy stores in the GET gather
     int hash_depth = 2;           // RSG_HASH_DEPTH=1..3: 8-packet batches in flight per lane
     int fused_kind = 0;  // RSG_FUSED_KIND=packed|ring|dma|wide2|wide4|split2|split4|net|table (0: by batch size)
-    bool fused_spw1 = false;      // RSG_FUSED_SPW1=1: one stripe per packed workgroup
+    bool fused_spw1 = false;      // RSG_FUSED_SPW1=1: one stripe per packed workgroup (measurement builds; no effect in the product)
     int enc_prio = 0;             // RSG_ENC_PRIO=<0..3>: wave priorities of the fused DMA kernel
     int dma_ew = 2;               // RSG_DMA_EW=4: two encoder waves per stripe group (split, alternate steps)
     int dma_nt = 3;               // RSG_DMA_NT=<0..3>: non-temporal loads (bit 0) / stores (bit 1)

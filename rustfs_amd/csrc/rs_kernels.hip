@@ -1531,12 +1531,20 @@ struct FusedPick {
 };
 
 // packed: SPW = fused_spw (full hasher waves); !packed: one stripe per
-// workgroup (A/B only).
+// workgroup (A/B only, measurement builds).
 template <int C, int R>
 static FusedPick fused_entry(bool packed) {
     constexpr int spw = fused_spw<C + R>();
-    if (!packed || spw == 1) return {k_encode_hash_fused<C, R, 1>, 1, 1 + (C + R + 15) / 16};
-    return {k_encode_hash_fused<C, R, spw>, spw, spw + (spw * (C + R) + 15) / 16};
+    if constexpr (spw == 1) {
+        (void)packed;
+        return {k_encode_hash_fused<C, R, 1>, 1, 1 + (C + R + 15) / 16};
+    } else {
+#if RSG_MEASUREMENT_BUILD  // the unpacked A/B variants (~60 kernels) stay out of the product library
+        if (!packed) return {k_encode_hash_fused<C, R, 1>, 1, 1 + (C + R + 15) / 16};
+#endif
+        (void)packed;
+        return {k_encode_hash_fused<C, R, spw>, spw, spw + (spw * (C + R) + 15) / 16};
+    }
 }
 
 template <int C>
