@@ -111,7 +111,7 @@ def put_stream(erasure: Erasure, reader, size: int, fds: List[Optional[int]],
                algo: HashAlgorithm = HashAlgorithm.HighwayHash256S,
                batch_blocks: int = DEFAULT_BATCH_BLOCKS,
                inflight_batches: int = DEFAULT_INFLIGHT_BATCHES,
-               stage: Optional[PutStage] = None, read_threads: int = 4,
+               stage: Optional[PutStage] = None, read_threads: int = 8,
                write_quorum: Optional[int] = None) -> dict:
     """Encode `size` bytes read from `reader` (``readinto``) and append one
     BitrotWriter record per block to each shard file descriptor in `fds`
