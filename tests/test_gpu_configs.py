@@ -146,6 +146,27 @@ def test_config5_geometry_full_batch_per_gpu(gpu, oracle):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("k,m", [(7, 4), (5, 4), (3, 3), (9, 4)])
+def test_fused_table_enc_full_batch(gpu, oracle, k, m):
+    """Config 4's kernel for geometries without a network (the table kernel's
+    ENC mode: RS(7,4) 11 drives, RS(5,4) 9, RS(3,3) 6, RS(9,4) 13) at 1 MiB
+    blocks, n = 4096 (ragged S, records at odd offsets): parity and every
+    digest of sampled stripes against the oracle, the whole batch verified
+    on the device."""
+    import torch
+    from rustfs_amd import Erasure
+    S, n = -(-(1 << 20) // k), 4096
+    st = _fill(torch, n, k, m, S, seed=40 + k)
+    dig = torch.zeros((n, k + m, 32), dtype=torch.uint8, device="cuda")
+    e = Erasure(k, m, 1 << 20)
+    e.encode_batch(st, dig)
+    torch.cuda.synchronize()
+    _check_stripes(oracle, st, dig, k, m, _sample(n, 4))
+    assert bool(e.verify_batch(st).all())
+    del st, dig
+    torch.cuda.empty_cache()
+
+
 _VARIANT_SNIPPET = r"""
 import sys, numpy as np, torch
 sys.path.insert(0, {root!r})
