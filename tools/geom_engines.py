@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--tune", action="append", default=[])
     ap.add_argument("--get-lost", default=None, help="shards lost for the GET, e.g. 0 or 0,3 (default: 0,k-1)")
     ap.add_argument("--heal-lost", default=None, help="shards healed, e.g. 1,10 (default: 1,k)")
+    ap.add_argument("--block", type=int, default=1 << 20, help="block bytes (S = ceil(block / k))")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the output checks (ablation builds whose kernels skip arithmetic)")
     a = ap.parse_args()
@@ -44,9 +45,9 @@ def main():
     for g in a.geoms:
         k, m = map(int, g.split(","))
         t, n = k + m, a.n
-        S = -(-(1 << 20) // k)
+        S = -(-a.block // k)
         rec = 32 + S
-        e = Erasure(k, m, 1 << 20)
+        e = Erasure(k, m, a.block)
         st = bench.random_stripes(torch.device("cuda", 0), k, m, S, n, 77 + k)
         dig = torch.empty((n, t, 32), dtype=torch.uint8, device="cuda")
         e.encode_batch(st, dig)
