@@ -507,6 +507,22 @@ def test_ec58_five_or_more_lost(gpu, oracle, table_records, engine, k, m, heal, 
     test_ec58_three_four_lost(gpu, oracle, table_records, engine, k, m, heal, lost)
 
 
+EC5_MANY = [(heal, lost) for e in (3, 4, 5) for lost in itertools.combinations(range(10), e) for heal in (0, 1)
+            if heal or min(lost) < 5]
+
+
+@pytest.mark.parametrize("heal,lost", EC5_MANY, ids=str)
+def test_ec5_every_three_to_five_loss_pattern(gpu, oracle, table_records, heal, lost):
+    """RS(5,5) (EC:5 on 10 drives) with every choice of three, four and five
+    lost shards (five: the most the class survives; one and two are in
+    test_table_kernel_every_pattern): GET (every pattern with a data shard
+    lost) and the heal of all of them, through the one-pass table kernel
+    (round 6: R = lost data + surplus rows a step, gf_rows for R = 5, the
+    per-row loop below; an altered surplus parity reported where one is
+    left)."""
+    test_ec58_three_four_lost(gpu, oracle, table_records, "one_pass", 5, 5, heal, lost)
+
+
 def test_table_patterns_cover_every_loss():
     """RS(5,4): 5 + (36 - 6) GET (every pair but the 6 all-parity ones) and
     9 + 36 heal patterns; RS(15,1): 15 GET and 16 heal (one parity shard: one
