@@ -493,15 +493,17 @@ def test_ec58_three_four_lost(gpu, oracle, table_records, engine, k, m, heal, lo
         _lib.check(L.rsg_set_record_engine(gpu.handle, _lib.RSG_RECORD_ENGINE_AUTO))
 
 
-MANY_CASES = (_multi_loss_patterns(8, 8, 3, 808, range(5, 9)) + _multi_loss_patterns(10, 6, 3, 1006, (5, 6)) +
-              _multi_loss_patterns(5, 5, 3, 505, (5,)) + _multi_loss_patterns(9, 7, 2, 907, (5, 6, 7)))
+MANY_CASES = (_multi_loss_patterns(8, 8, 12, 808, range(5, 9)) + _multi_loss_patterns(10, 6, 10, 1006, (5, 6)) +
+              _multi_loss_patterns(7, 7, 10, 707, range(5, 8)) + _multi_loss_patterns(11, 5, 10, 1105, (5,)) +
+              _multi_loss_patterns(9, 7, 8, 907, (5, 6, 7)))
 
 
 @pytest.mark.parametrize("k,m,heal,lost", MANY_CASES, ids=str)
 @pytest.mark.parametrize("engine", ["one_pass", "two_pass"])
 def test_ec58_five_or_more_lost(gpu, oracle, table_records, engine, k, m, heal, lost):
-    """EC:5..8 with five to m shards lost (every parity shard spent at RS(8,8)
-    with 8 lost: no surplus to compare): GET in both forms and the heal of
+    """EC:5..8 with five to m shards lost (seeded samples of RS(8,8), RS(10,6),
+    RS(7,7), RS(11,5), RS(9,7); every parity shard spent at RS(8,8) with 8
+    lost: no surplus to compare): GET in both forms and the heal of
     every lost shard, bit-exact against the oracle, through the one-pass
     table kernel (round 6) and through the two-pass path."""
     test_ec58_three_four_lost(gpu, oracle, table_records, engine, k, m, heal, lost)
