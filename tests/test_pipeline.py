@@ -136,6 +136,24 @@ def test_range_get(gpu, tmp_path, k, m, lost):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lost", [(0, 3, 7), (0, 1, 2, 5, 9)])
+def test_range_get_ec5_many_lost_one_pass(gpu, tmp_path, lost):
+    """EC:5 (RS(5,5), 10 drives) with three and with five drives lost, read in
+    batches of 1100 blocks (>= 1024: the one-pass table kernel, five rows a
+    step with five lost) — the whole object and two ranges."""
+    k, m, nblk = 5, 5, 1100
+    size = nblk * BS + 999
+    es, dirs = _set(tmp_path, k, m)
+    data = np.random.default_rng(55).integers(0, 256, size, dtype=np.uint8).tobytes()
+    es.put_object_stream("b/o", io.BytesIO(data), size, batch_blocks=256)
+    for i in lost:
+        os.remove(es.part_file(i, "b/o"))
+    for off, ln in ((0, size), (3 * BS + 17, 1050 * BS), (size - BS - 5, BS + 5)):
+        got = b"".join(es.get_object_stream("b/o", off, ln, batch_blocks=nblk))
+        assert got == data[off:off + ln], (off, ln)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("lost", [(), (0, 3), (4,)])
 def test_range_get_views(gpu, tmp_path, lost):
     """get_stream(views=True): each block's window as memoryviews of the
